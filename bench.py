@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: served tokens/s on an auto-deployed Llama-3-8B (+ p50 CR->ready).
+
+BASELINE.json metric: "served tokens/sec/MI355X on auto-deployed Llama-3-8B +
+p50 CR-reconcile->ready".  Each rank (one process per GPU, launched by
+torch.distributed.run for N > 1) is one data-parallel serving replica (the
+reference's predictor ``replicas``; Llama-3-8B bf16 = 16 GB fits one 288 GB
+MI355X, so replicas scale weakly with N):
+
+  1. deploy: an ``MlflowModel`` CR is reconciled by the operator into a
+     SeldonDeployment whose predictor is this runtime; the runtime
+     random-initialises Llama-3-8B bf16 on the GPU, captures its decode
+     hipGraphs and reports ready -> CR->ready seconds (p50 over ranks);
+  2. serve: a closed-loop load of ``--batch`` concurrent requests
+     (``--prompt-len`` random prompt tokens, ``--output-len`` generated tokens,
+     the first cohort at staggered ages so the engine is in steady state),
+     continuous batching with chunked prefill and graph-replayed decode;
+  3. time exactly ``--steps`` engine steps after ``--warmup`` untimed ones,
+     bracketed by barrier + device synchronize; value = generated tokens over
+     all ranks / max rank time.
+
+Synthetic data, random-init weights (no checkpoints / datasets offline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=256, help="concurrent requests per GPU")
+    ap.add_argument("--prompt-len", type=int, default=256)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--prefill-min-batch", type=int, default=16)
+    ap.add_argument("--max-decode-gap", type=int, default=24)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
+    ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    from mlopamd.parallel.comm import env_rank_info, init_distributed
+    import torch.distributed as dist
+
+    rank, local_rank, world = env_rank_info()
+    if world > 1:
+        init_distributed()
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+
+    from mlopamd.runtime.deploy import deploy_for_bench
+
+    t0 = time.perf_counter()
+    engine, ready_s, deploy_info = deploy_for_bench(
+        model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank,
+        engine_kwargs=dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
+                           max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
+                           prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
+                           seed=a.seed + rank))
+    from mlopamd.runtime.sampler import SamplingParams
+
+    rng = np.random.default_rng(1234 + rank)
+    V = engine.model.cfg.vocab_size
+    P, O = a.prompt_len, a.output_len
+
+    def new_request(max_tokens):
+        prompt = rng.integers(1000, V - 1000, size=P).tolist()
+        engine.add_request(prompt, SamplingParams(max_tokens=int(max_tokens), temperature=a.temperature,
+                                                  top_k=50 if a.temperature > 0 else 0, ignore_eos=True))
+
+    # first cohort at uniformly staggered remaining lengths (steady-state age mix)
+    for i in range(a.batch):
+        new_request(1 + (i * O) // a.batch)
+
+    def run_steps(n):
+        gen = 0
+        for _ in range(n):
+            outs = engine.step()
+            gen += len(outs)
+            for o in outs:
+                if o.finished:
+                    new_request(O)
+        return gen
+
+    run_steps(a.warmup)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    s0 = dict(engine.stats)
+    t_start = time.perf_counter()
+    gen = run_steps(a.steps)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    stats = {k: engine.stats[k] - s0.get(k, 0) for k in engine.stats}
+
+    tot = torch.tensor([float(gen), elapsed, ready_s, float(stats.get("prefill_tokens", 0))], dtype=torch.float64)
+    if world > 1:
+        tt = tot.to(dev) if dev.type == "cuda" else tot
+        gl = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(gl, tt)
+        gathered = [g.cpu() for g in gl]
+    else:
+        gathered = [tot]
+    total_gen = sum(float(g[0]) for g in gathered)
+    max_t = max(float(g[1]) for g in gathered)
+    readies = sorted(float(g[2]) for g in gathered)
+    p50_ready = readies[len(readies) // 2] if len(readies) % 2 else 0.5 * (readies[len(readies) // 2 - 1] + readies[len(readies) // 2])
+    total_prefill = sum(float(g[3]) for g in gathered)
+    value = total_gen / max_t
+    if rank == 0:
+        res = {
+            "metric": "served_tokens_per_sec",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * max_t / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random prompt tokens, random-init weights)",
+            "config": {"model": "Llama-3-8B", "global_batch": a.batch * world, "seq_len": P + O,
+                       "prompt_len": P, "output_len": O, "parallelism": f"dp{world}",
+                       "graphs": not a.no_graphs},
+            "p50_cr_ready_s": round(p50_ready, 3),
+            "served_tokens_per_sec_per_gpu": round(value / world, 2),
+            "prefill_tokens_per_sec": round(total_prefill / max_t, 2),
+            "step_mix": stats,
+            "deploy": deploy_info,
+        }
+        print(json.dumps(res), flush=True)
+    engine.shutdown() if hasattr(engine, "shutdown") else None
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+"""Llama-3 decoder (8B / 70B shapes) for the serving runtime.
+
+Flattened ragged batches (every scheduled token of every sequence in one
+[T, H] matrix, vLLM-style) so prefill chunks and decode tokens share one
+forward.  Per layer:
+
+  add_rmsnorm -> QKV GEMM -> rope_cache (RoPE + paged KV write) -> paged_attention
+  -> O GEMM -> [TP all-reduce] -> add_rmsnorm -> gate_up GEMM -> silu_mul
+  -> down GEMM -> [TP all-reduce]
+
+Tensor parallel (Megatron): column-parallel QKV / gate_up, row-parallel O /
+down, vocab-parallel embedding and LM head (2 all-reduces per layer over RCCL).
+Weights are random-initialised on device (no checkpoints in this environment).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..parallel.comm import ParallelState, single
+from .config import ModelConfig
+from .layers import init_norm, init_weight, linear, rope_table
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16,
+                 pstate: ParallelState | None = None, seed: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.ps = pstate or single()
+        tp, r = self.ps.tp_size, self.ps.tp_rank
+        assert cfg.num_heads % tp == 0, "q heads must divide by TP"
+        assert cfg.intermediate_size % tp == 0 and cfg.vocab_size % tp == 0
+        self.n_q = cfg.num_heads // tp
+        # kv heads: sharded when tp <= Hkv, replicated otherwise
+        self.n_kv = max(1, cfg.num_kv_heads // tp)
+        self.inter = cfg.intermediate_size // tp
+        self.vocab_local = cfg.vocab_size // tp
+        self.vocab_start = r * self.vocab_local
+        D, H = cfg.head_dim, cfg.hidden_size
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed * 1000 + r)
+        w = lambda *s: init_weight(s, self.device, dtype, gen=gen)  # noqa: E731
+        self.embed = w(self.vocab_local, H)
+        self.layers = []
+        for _ in range(cfg.num_layers):
+            layer = {
+                "in_norm": init_norm(H, self.device, dtype),
+                "post_norm": init_norm(H, self.device, dtype),
+                "qkv": w((self.n_q + 2 * self.n_kv) * D, H),
+                "o": w(H, self.n_q * D),
+            }
+            layer.update(self._init_mlp(w))
+            self.layers.append(layer)
+        self.final_norm = init_norm(H, self.device, dtype)
+        self.lm_head = self.embed if cfg.tie_embeddings else w(self.vocab_local, H)
+        self.cos_sin = rope_table(D, cfg.max_position, cfg.rope_theta, cfg.rope_scaling, self.device)
+
+    # ---------------------------------------------------------------- MLP --
+    def _init_mlp(self, w):
+        H = self.cfg.hidden_size
+        return {"gate_up": w(2 * self.inter, H), "down": w(H, self.inter)}
+
+    def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        L = self.layers[i]
+        gu = linear(x, L["gate_up"])
+        return linear(ops.silu_mul(gu), L["down"])
+
+    # ------------------------------------------------------------ forward --
+    def weight_tensors(self):
+        yield self.embed
+        for L in self.layers:
+            yield from (v for v in L.values() if isinstance(v, torch.Tensor))
+        yield self.final_norm
+        if self.lm_head is not self.embed:
+            yield self.lm_head
+
+    def weight_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.weight_tensors())
+
+    def forward(self, ids: torch.Tensor, meta, kv) -> torch.Tensor:
+        """ids [T] int64; meta: AttnMeta (positions/slots/tables); kv: KVCache.
+        Returns the final-normed hidden states of every token [T, H]."""
+        cfg, tp = self.cfg, self.ps.tp
+        eps = cfg.rms_eps
+        h = ops.embedding(ids, self.embed, self.vocab_start)
+        tp.all_reduce(h)
+        residual = h
+        x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
+        for i, L in enumerate(self.layers):
+            qkv = linear(x, L["qkv"])
+            q = ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i], self.n_q)
+            a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
+            o = linear(a.view(a.shape[0], -1), L["o"])
+            tp.all_reduce(o)
+            x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
+            m = self.mlp(i, x)
+            tp.all_reduce(m)
+            nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
+            x = ops.add_rmsnorm(m, residual, nxt, eps)
+        return x
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """[n, H] -> full-vocab logits [n, V] (fp32), gathered over the TP group."""
+        lg = linear(hidden, self.lm_head)
+        lg = self.ps.tp.all_gather(lg, dim=-1)
+        return lg.float()

@@ -1,0 +1,46 @@
+"""Mixtral-8x7B (sparse MoE, top-2 of 8 experts) on the Llama attention stack.
+
+MoE block (SURVEY.md §2.5 K11-K14 + CL4):
+  router GEMM -> fused softmax/top-k/renormalise (K11) -> expert-sorted
+  permutation (K12) -> grouped GEMM over all experts in ONE launch (K13,
+  gate_up + SiLU-mul, then down) -> weighted un-permute/combine (K14).
+
+Expert parallel: with ``ep > 1`` each rank owns E/ep experts; routed token
+rows travel to their expert's rank with an all-to-all (dispatch) and back
+(combine) over RCCL, see ``mlopamd.parallel.moe``.  Attention stays TP.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .layers import linear
+from .llama import LlamaModel
+
+
+class MixtralModel(LlamaModel):
+    def _init_mlp(self, w):
+        cfg = self.cfg
+        E, H, I = cfg.num_experts, cfg.hidden_size, cfg.intermediate_size
+        ep = self.ps.ep.size
+        assert E % ep == 0, "experts must divide by EP size"
+        self.n_local_experts = E // ep
+        self.expert_start = self.ps.ep.rank * self.n_local_experts
+        return {
+            "router": w(E, H),
+            "w13": w(self.n_local_experts, 2 * I, H),
+            "w2": w(self.n_local_experts, H, I),
+        }
+
+    def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        from ..parallel.moe import moe_forward
+
+        L = self.layers[i]
+        return moe_forward(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.ps.ep,
+                           self.expert_start, self.n_local_experts)
+
+    def forward(self, ids, meta, kv):
+        # MoE output is already complete per token (EP combine) -> no TP all-reduce
+        # when attention runs TP=1 inside an EP group; the base forward all-reduces
+        # over the TP group which is a no-op at tp=1.
+        return super().forward(ids, meta, kv)

@@ -1,0 +1,278 @@
+// Paged attention over the block-table KV cache (K6 decode, and the ragged /
+// chunked-prefill path of K7) with MFMA 16x16x32 bf16 on gfx950.
+//
+// Layouts (written by rope_cache.hip):
+//   k_cache[page, Hkv, 16, 128]  token-major  -> A operand of  S^T = K . Q^T
+//   v_cache[page, Hkv, 128, 16]  dim-major    -> A operand of  O^T = V^T . P^T
+// Both products keep the q-row on the lane (col = lane&15), so the online
+// softmax (max, exp2, rescale of O) is entirely lane-local except the two
+// cross-lane max steps (xor 16, xor 32), and P^T feeds the second MFMA straight
+// from the first one's accumulator registers (cdna_hip_programming.md §3
+// "An accumulator tile as the next MFMA's operand", with a permuted k order:
+// lane group g = lane>>4 owns tokens {4g..4g+3} of page A and {4g..4g+3} of page B).
+//
+// MFMA rows: 16 q-rows per tile = (16/G query tokens) x (G heads of one kv head).
+// A workgroup = 4 waves = one (tile, kv head, kv partition); the waves split
+// the partition's page pairs round-robin and merge (m, l, O) through LDS.
+// Partitions > 1 (long context, small batch: fill 256 CUs) write fp32 partials
+// that attn_reduce_kernel combines.
+//
+// Memory-bound: each K/V byte is loaded once per tile into VGPRs (no LDS
+// staging: "GEMV / M <= 16" row of the glds table, cdna_hip_programming.md §5).
+//
+// REQUIREMENT: the cache is zero-initialised at allocation (masked lanes multiply
+// p = 0 with whatever the unused slots hold; NaN garbage would poison O).
+#include "common.h"
+#include "launch.h"
+
+namespace mlop {
+
+constexpr int kD = 128;
+constexpr int kBS = 16;
+constexpr float kNegBig = -1.0e30f;
+
+template <int G>
+__global__ void __launch_bounds__(256) paged_attn_kernel(
+    uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ tile_seq, const int* __restrict__ tile_q0,
+    const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int part_tokens,
+    int nparts, int num_blocks) {
+  constexpr int QT = 16 / G;
+  __shared__ float sm_o[4][16][kD + 4];
+  __shared__ float sm_m[4][16];
+  __shared__ float sm_l[4][16];
+
+  const int tile = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int s = tile_seq[tile], q0 = tile_q0[tile];
+  const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
+  const int last_q = min(q0 + QT, ql) - 1;           // last valid query of the tile
+  const int kv_end = last_q >= 0 ? ctx - ql + last_q + 1 : 0;
+  const int p_begin = part * part_tokens;
+  const int p_end = min(kv_end, p_begin + part_tokens);
+  if (p_begin >= p_end && nparts > 1) return;        // reducer skips empty partitions
+
+  // this lane's q-row (B operand column) and its causal limit
+  const int r = lane & 15, g4 = lane >> 4;
+  const int qi = q0 + r / G;
+  const bool row_ok = qi < ql;
+  const int head = kvh * G + (r % G);
+  const int pos_r = row_ok ? ctx - ql + qi : -1;
+
+  bf16x8 qf[4];
+  {
+    const uint16_t* qrow = q + ((size_t)(qs + (row_ok ? qi : 0)) * Hq + head) * kD;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + g4 * 8);
+      qf[kk] = row_ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f32x4 o[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = kNegBig, l = 0.f;
+
+  const int* bt = block_tables + (size_t)s * bt_stride;
+  const int pp_begin = p_begin >> 5;
+  const int pp_end = (p_end + 31) >> 5;
+  const int n_pages = (p_end + kBS - 1) / kBS;
+  const size_t page_stride = (size_t)Hkv * kBS * kD;
+
+  for (int pp = pp_begin + wid; pp < pp_end; pp += 4) {
+    // clamp: a corrupt block table must not become an out-of-bounds fault
+    const int pgA = min(max(bt[2 * pp], 0), num_blocks - 1);
+    const int pgB = (2 * pp + 1 < n_pages) ? min(max(bt[2 * pp + 1], 0), num_blocks - 1) : pgA;
+    const uint16_t* kA = kc + pgA * page_stride + (size_t)kvh * kBS * kD;
+    const uint16_t* kB = kc + pgB * page_stride + (size_t)kvh * kBS * kD;
+    const uint16_t* vA = vc + pgA * page_stride + (size_t)kvh * kD * kBS;
+    const uint16_t* vB = vc + pgB * page_stride + (size_t)kvh * kD * kBS;
+
+    bf16x8 ka[4], kb[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      ka[kk] = *reinterpret_cast<const bf16x8*>(kA + r * kD + kk * 32 + g4 * 8);
+      kb[kk] = *reinterpret_cast<const bf16x8*>(kB + r * kD + kk * 32 + g4 * 8);
+    }
+    bf16x4 va[8], vb[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      va[d] = *reinterpret_cast<const bf16x4*>(vA + (d * 16 + r) * kBS + g4 * 4);
+      vb[d] = *reinterpret_cast<const bf16x4*>(vB + (d * 16 + r) * kBS + g4 * 4);
+    }
+
+    // S^T[token][row]: lane holds row r, tokens 4*g4 + i of each page
+    f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      sa = mfma16(ka[kk], qf[kk], sa);
+      sb = mfma16(kb[kk], qf[kk], sb);
+    }
+    const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
+    float pa[4], pb[4];
+    float mx = kNegBig;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ta = tokA + i, tb = tokB + i;
+      pa[i] = (ta < p_end && ta <= pos_r) ? sa[i] * scale_log2 : -INFINITY;
+      pb[i] = (tb < p_end && tb <= pos_r) ? sb[i] * scale_log2 : -INFINITY;
+      mx = fmaxf(mx, fmaxf(pa[i], pb[i]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = exp2f(m - m_new);
+    m = m_new;
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pa[i] = exp2f(pa[i] - m_new);
+      pb[i] = exp2f(pb[i] - m_new);
+      rs += pa[i] + pb[i];
+    }
+    l = l * alpha + rs;
+    bf16x8 pf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pf[i] = (short)f2bf(pa[i]);
+      pf[4 + i] = (short)f2bf(pb[i]);
+    }
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      o[d] *= alpha;
+      bf16x8 vf = {va[d][0], va[d][1], va[d][2], va[d][3], vb[d][0], vb[d][1], vb[d][2], vb[d][3]};
+      o[d] = mfma16(vf, pf, o[d]);
+    }
+  }
+
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  // O^T[d][row]: lane holds row r, dims 16*dblk + 4*g4 + i
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[wid][r][d * 16 + g4 * 4 + i] = o[d][i];
+  if (g4 == 0) {
+    sm_m[wid][r] = m;
+    sm_l[wid][r] = l;
+  }
+  __syncthreads();
+
+  const int rr = threadIdx.x >> 4, c = (threadIdx.x & 15) * 8;
+  float M = kNegBig;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][rr]);
+  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float f = exp2f(sm_m[w][rr] - M);
+    L += f * sm_l[w][rr];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f * sm_o[w][rr][c + j];
+  }
+  const int qi2 = q0 + rr / G;
+  if (qi2 >= ql) return;
+  const int head2 = kvh * G + (rr % G);
+  if (nparts == 1) {
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    u32x4 ov;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ov[j] = pack2(acc[2 * j] * inv, acc[2 * j + 1] * inv);
+    *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + head2) * kD + c) = ov;
+  } else {
+    const size_t pbase = (((size_t)tile * Hkv + kvh) * nparts + part) * 16 + rr;
+    float4* po = reinterpret_cast<float4*>(part_o + pbase * kD + c);
+    po[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    po[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    if ((threadIdx.x & 15) == 0) {
+      part_ml[pbase * 2] = M;
+      part_ml[pbase * 2 + 1] = L;
+    }
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) attn_reduce_kernel(
+    uint16_t* __restrict__ out, const float* __restrict__ part_o,
+    const float* __restrict__ part_ml, const int* __restrict__ tile_seq,
+    const int* __restrict__ tile_q0, const int* __restrict__ q_start,
+    const int* __restrict__ q_len, const int* __restrict__ ctx_len, int Hq, int Hkv,
+    int part_tokens, int nparts) {
+  constexpr int QT = 16 / G;
+  const int tile = blockIdx.x, kvh = blockIdx.y;
+  const int s = tile_seq[tile], q0 = tile_q0[tile];
+  const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
+  const int last_q = min(q0 + QT, ql) - 1;
+  const int kv_end = last_q >= 0 ? ctx - ql + last_q + 1 : 0;
+  const int nvalid = min(nparts, (kv_end + part_tokens - 1) / part_tokens);
+  const int rr = threadIdx.x >> 4, c = (threadIdx.x & 15) * 8;
+  const int qi = q0 + rr / G;
+  if (qi >= ql) return;
+  const size_t base = ((size_t)tile * Hkv + kvh) * nparts;
+  float M = kNegBig;
+  for (int p = 0; p < nvalid; ++p) M = fmaxf(M, part_ml[((base + p) * 16 + rr) * 2]);
+  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nvalid; ++p) {
+    const size_t pb = (base + p) * 16 + rr;
+    const float f = exp2f(part_ml[pb * 2] - M);
+    L += f * part_ml[pb * 2 + 1];
+    const float4* po = reinterpret_cast<const float4*>(part_o + pb * kD + c);
+    float4 a = po[0], b = po[1];
+    acc[0] += f * a.x; acc[1] += f * a.y; acc[2] += f * a.z; acc[3] += f * a.w;
+    acc[4] += f * b.x; acc[5] += f * b.y; acc[6] += f * b.z; acc[7] += f * b.w;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  u32x4 ov;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ov[j] = pack2(acc[2 * j] * inv, acc[2 * j + 1] * inv);
+  const int head = kvh * G + (rr % G);
+  *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi) * Hq + head) * kD + c) = ov;
+}
+
+template <int G>
+static void launch_g(void* out, float* part_o, float* part_ml, const void* q, const void* kc,
+                     const void* vc, const int* bt, int bt_stride, const int* tile_seq,
+                     const int* tile_q0, const int* q_start, const int* q_len, const int* ctx_len,
+                     int num_tiles, int Hq, int Hkv, float scale_log2, int part_tokens, int nparts,
+                     int num_blocks, hipStream_t st) {
+  dim3 grid(num_tiles, Hkv, nparts);
+  paged_attn_kernel<G><<<grid, 256, 0, st>>>((uint16_t*)out, part_o, part_ml, (const uint16_t*)q,
+                                             (const uint16_t*)kc, (const uint16_t*)vc, bt,
+                                             bt_stride, tile_seq, tile_q0, q_start, q_len, ctx_len,
+                                             Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks);
+  if (nparts > 1) {
+    attn_reduce_kernel<G><<<dim3(num_tiles, Hkv), 256, 0, st>>>(
+        (uint16_t*)out, part_o, part_ml, tile_seq, tile_q0, q_start, q_len, ctx_len, Hq, Hkv,
+        part_tokens, nparts);
+  }
+}
+
+void launch_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
+                            const void* kc, const void* vc, const int* bt, int bt_stride,
+                            const int* tile_seq, const int* tile_q0, const int* q_start,
+                            const int* q_len, const int* ctx_len, int num_tiles, int Hq, int Hkv,
+                            float scale_log2, int part_tokens, int nparts, int num_blocks,
+                            hipStream_t st) {
+  if (num_tiles == 0) return;
+  const int G = Hq / Hkv;
+#define MLOP_ATTN_CASE(GG)                                                                        \
+  case GG:                                                                                        \
+    launch_g<GG>(out, part_o, part_ml, q, kc, vc, bt, bt_stride, tile_seq, tile_q0, q_start,     \
+                 q_len, ctx_len, num_tiles, Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, st);        \
+    break;
+  switch (G) {
+    MLOP_ATTN_CASE(1)
+    MLOP_ATTN_CASE(2)
+    MLOP_ATTN_CASE(4)
+    MLOP_ATTN_CASE(8)
+    MLOP_ATTN_CASE(16)
+    default: break;
+  }
+#undef MLOP_ATTN_CASE
+}
+
+}  // namespace mlop

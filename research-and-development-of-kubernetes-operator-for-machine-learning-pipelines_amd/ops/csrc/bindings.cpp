@@ -1,0 +1,198 @@
+// torch.ops.mlop.* registrations for the gfx950 kernels.
+//
+// Every op validates dtype / contiguity / shape on the host before launching
+// (a faulting kernel can reset every GPU of the node), runs on the current
+// HIP stream (so it is hipGraph-capturable) and mutates pre-allocated outputs
+// (no allocation inside: graph-capture safe, cdna_hip_programming.md Guideline 9).
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <cmath>
+
+#include "launch.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_i32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kInt, name, " must be int32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void rmsnorm(Tensor out, Tensor x, Tensor w, double eps) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && H <= 65536, "hidden size must be a multiple of 8");
+  TORCH_CHECK(w.numel() == H && out.numel() == x.numel(), "rmsnorm shape mismatch");
+  c10::hip::HIPGuard g(x.device());
+  mlop::launch_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), (float)eps,
+                       (int)(x.numel() / H), (int)H, cur_stream());
+}
+
+void add_rmsnorm(Tensor out, Tensor residual, Tensor x, Tensor w, double eps) {
+  check_bf16(out, "out"); check_bf16(residual, "residual"); check_bf16(x, "x"); check_bf16(w, "w");
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && H <= 65536, "hidden size must be a multiple of 8");
+  TORCH_CHECK(w.numel() == H && out.numel() == x.numel() && residual.numel() == x.numel(),
+              "add_rmsnorm shape mismatch");
+  c10::hip::HIPGuard g(x.device());
+  mlop::launch_add_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), w.data_ptr(),
+                           (float)eps, (int)(x.numel() / H), (int)H, cur_stream());
+}
+
+void rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor qkv, Tensor pos,
+                Tensor cos_sin, Tensor slots) {
+  check_bf16(q_out, "q_out"); check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
+  check_i32(pos, "pos"); check_i32(slots, "slots");
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.stride(-1) == 1,
+              "qkv must be bf16 with unit inner stride");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous(), "cos_sin f32");
+  TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "rope_cache ranks");
+  const int T = (int)q_out.size(0), Hq = (int)q_out.size(1), D = (int)q_out.size(2);
+  const int Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
+  TORCH_CHECK(k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
+                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
+              "cache layouts: k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(D % 16 == 0, "head dim must be a multiple of 16");
+  TORCH_CHECK(qkv.size(0) == T && qkv.size(-1) >= (Hq + 2 * Hkv) * D, "qkv shape");
+  TORCH_CHECK(pos.numel() == T && slots.numel() == T, "pos/slots length");
+  TORCH_CHECK(cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
+  c10::hip::HIPGuard g(qkv.device());
+  mlop::launch_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), qkv.data_ptr(),
+                          pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), T,
+                          Hq, Hkv, D, (int)qkv.stride(0), BS, cur_stream());
+}
+
+void silu_mul(Tensor out, Tensor x) {
+  check_bf16(out, "out"); check_bf16(x, "x");
+  const int64_t I2 = x.size(-1);
+  TORCH_CHECK(I2 % 16 == 0, "gate_up width must be a multiple of 16");
+  const int64_t M = x.numel() / I2;
+  TORCH_CHECK(out.numel() == M * (I2 / 2), "silu_mul shape mismatch");
+  c10::hip::HIPGuard g(x.device());
+  mlop::launch_silu_mul(out.data_ptr(), x.data_ptr(), (int)M, (int)(I2 / 2), cur_stream());
+}
+
+void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_start) {
+  check_bf16(out, "out"); check_bf16(table, "table");
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids int64");
+  const int64_t H = table.size(1);
+  TORCH_CHECK(H % 8 == 0 && out.size(-1) == H && out.numel() == ids.numel() * H, "embedding shape");
+  c10::hip::HIPGuard g(table.device());
+  mlop::launch_embedding(out.data_ptr(), table.data_ptr(), ids.data_ptr<int64_t>(),
+                         (int)ids.numel(), (int)H, vocab_start, vocab_start + table.size(0),
+                         cur_stream());
+}
+
+void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_cache,
+                     Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0,
+                     Tensor q_start, Tensor q_len, Tensor ctx_len, double scale,
+                     int64_t part_tokens, int64_t nparts) {
+  check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables"); check_i32(tile_seq, "tile_seq");
+  check_i32(tile_q0, "tile_q0"); check_i32(q_start, "q_start"); check_i32(q_len, "q_len");
+  check_i32(ctx_len, "ctx_len");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
+              "k_cache must be [NB, Hkv, 16, 128]");
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 128, 16}),
+              "v_cache must be [NB, Hkv, 128, 16]");
+  const int Hq = (int)q.size(1), Hkv = (int)k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "GQA group must divide 16");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(tile_seq.numel() == tile_q0.numel(), "tile arrays");
+  TORCH_CHECK(q_start.numel() == q_len.numel() && q_len.numel() == ctx_len.numel() &&
+                  block_tables.size(0) >= q_len.numel(),
+              "per-sequence arrays");
+  TORCH_CHECK(part_tokens % 32 == 0 && part_tokens > 0 && nparts >= 1, "partition size");
+  const int num_tiles = (int)tile_seq.numel();
+  if (nparts > 1) {
+    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
+                "partials f32");
+    TORCH_CHECK(part_o.numel() >= (int64_t)num_tiles * Hkv * nparts * 16 * 128 &&
+                    part_ml.numel() >= (int64_t)num_tiles * Hkv * nparts * 16 * 2,
+                "partial workspace too small");
+  }
+  c10::hip::HIPGuard g(q.device());
+  const float scale_log2 = (float)(scale * 1.4426950408889634);
+  mlop::launch_paged_attention(
+      out.data_ptr(), nparts > 1 ? part_o.data_ptr<float>() : nullptr,
+      nparts > 1 ? part_ml.data_ptr<float>() : nullptr, q.data_ptr(), k_cache.data_ptr(),
+      v_cache.data_ptr(), block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+      tile_seq.data_ptr<int>(), tile_q0.data_ptr<int>(), q_start.data_ptr<int>(),
+      q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), num_tiles, Hq, Hkv, scale_log2,
+      (int)part_tokens, (int)nparts, (int)k_cache.size(0), cur_stream());
+}
+
+void check_logits(const Tensor& logits) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 &&
+                  logits.stride(1) == 1 && logits.stride(0) % 4 == 0,
+              "logits must be f32 [n, V] with unit inner stride and 16-B aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0, "logits 16-B aligned");
+}
+
+void argmax(Tensor out, Tensor logits) {
+  check_logits(logits);
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == logits.size(0), "out int64 [n]");
+  c10::hip::HIPGuard g(logits.device());
+  mlop::launch_argmax(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)logits.size(0),
+                      (int)logits.size(1), logits.stride(0), cur_stream());
+}
+
+void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, Tensor uniform) {
+  check_logits(logits);
+  const int64_t n = logits.size(0);
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == n, "out int64 [n]");
+  TORCH_CHECK(temps.scalar_type() == at::kFloat && temps.numel() == n && temps.is_cuda(), "temps");
+  TORCH_CHECK(top_ps.scalar_type() == at::kFloat && top_ps.numel() == n && top_ps.is_cuda(), "top_ps");
+  TORCH_CHECK(uniform.scalar_type() == at::kFloat && uniform.numel() == n && uniform.is_cuda(), "u");
+  check_i32(top_ks, "top_ks");
+  TORCH_CHECK(top_ks.numel() == n, "top_ks");
+  c10::hip::HIPGuard g(logits.device());
+  mlop::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)n,
+                      (int)logits.size(1), logits.stride(0), temps.data_ptr<float>(),
+                      top_ks.data_ptr<int>(), top_ps.data_ptr<float>(), uniform.data_ptr<float>(),
+                      cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(mlop, m) {
+  m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
+  m.def("sample(Tensor(a!) out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, "
+        "Tensor uniform) -> ()");
+  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
+  m.def("add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
+  m.def("rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "
+        "Tensor pos, Tensor cos_sin, Tensor slots) -> ()");
+  m.def("silu_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def("embedding(Tensor(a!) out, Tensor table, Tensor ids, int vocab_start) -> ()");
+  m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor q, "
+        "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0, "
+        "Tensor q_start, Tensor q_len, Tensor ctx_len, float scale, int part_tokens, "
+        "int nparts) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("add_rmsnorm", &add_rmsnorm);
+  m.impl("rope_cache", &rope_cache);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("embedding", &embedding);
+  m.impl("paged_attention", &paged_attention);
+  m.impl("argmax", &argmax);
+  m.impl("sample", &sample);
+}

@@ -1,0 +1,30 @@
+// Host-side launchers of the gfx950 kernels (raw pointers + stream; no torch
+// headers here so the .hip files compile quickly).  Bound to torch in bindings.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+namespace mlop {
+
+void launch_rmsnorm(void* out, const void* x, const void* w, float eps, int M, int H,
+                    hipStream_t st);
+void launch_add_rmsnorm(void* out, void* residual, const void* x, const void* w, float eps, int M,
+                        int H, hipStream_t st);
+void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, const int* pos,
+                       const float* cos_sin, const int* slots, int T, int Hq, int Hkv, int D,
+                       int qkv_stride, int BS, hipStream_t st);
+void launch_silu_mul(void* out, const void* x, int M, int I, hipStream_t st);
+void launch_embedding(void* out, const void* table, const long* ids, int T, int H, long vocab_start,
+                      long vocab_end, hipStream_t st);
+void launch_paged_attention(void* out, float* part_o, float* part_ml, const void* q,
+                            const void* kc, const void* vc, const int* bt, int bt_stride,
+                            const int* tile_seq, const int* tile_q0, const int* q_start,
+                            const int* q_len, const int* ctx_len, int num_tiles, int Hq, int Hkv,
+                            float scale_log2, int part_tokens, int nparts, int num_blocks,
+                            hipStream_t st);
+void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st);
+void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
+                   const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);
+
+}  // namespace mlop

@@ -1,0 +1,101 @@
+// RMSNorm (K3) and fused residual-add + RMSNorm for gfx950.
+//
+// One workgroup per token row; every thread keeps VPT 16-byte vectors of the
+// row in registers, so the row is read from HBM exactly once and written once
+// (memory-bound: the target is the HBM roof, cdna_hip_programming.md App. B
+// "Element-wise"/"Reduction").  Residual-add semantics follow the Llama
+// decoder: residual <- bf16(residual + x); y <- bf16(rms(residual) * w).
+#include "common.h"
+#include "launch.h"
+
+namespace mlop {
+
+template <int VPT, bool ADD>
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ out,
+                                                      uint16_t* __restrict__ residual,
+                                                      const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ w, float eps,
+                                                      int H) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nvec = H >> 3;
+  const size_t base = (size_t)row * H;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      u32x4 a = *reinterpret_cast<const u32x4*>(x + base + vi * 8);
+      if constexpr (ADD) {
+        u32x4 r = *reinterpret_cast<const u32x4*>(residual + base + vi * 8);
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // round the sum to bf16 exactly as the bf16 residual stream does
+          float s0 = lo_bf(a[j]) + lo_bf(r[j]);
+          float s1 = hi_bf(a[j]) + hi_bf(r[j]);
+          o[j] = pack2(s0, s1);
+          v[i][2 * j] = lo_bf(o[j]);
+          v[i][2 * j + 1] = hi_bf(o[j]);
+        }
+        *reinterpret_cast<u32x4*>(residual + base + vi * 8) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[i][2 * j] = lo_bf(a[j]);
+          v[i][2 * j + 1] = hi_bf(a[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      u32x4 wv = *reinterpret_cast<const u32x4*>(w + vi * 8);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // HF LlamaRMSNorm: weight * bf16(x * inv)
+        float a0 = bf2f(f2bf(v[i][2 * j] * inv)) * lo_bf(wv[j]);
+        float a1 = bf2f(f2bf(v[i][2 * j + 1] * inv)) * hi_bf(wv[j]);
+        o[j] = pack2(a0, a1);
+      }
+      *reinterpret_cast<u32x4*>(out + base + vi * 8) = o;
+    }
+  }
+}
+
+template <bool ADD>
+static void dispatch(uint16_t* out, uint16_t* residual, const uint16_t* x, const uint16_t* w,
+                     float eps, int M, int H, hipStream_t st) {
+  const int nvec = H / 8;
+  int vpt = 1;
+  while (vpt < 8 && nvec / vpt > 512) vpt <<= 1;
+  int threads = ((cdiv(nvec, vpt) + 63) / 64) * 64;
+  if (M == 0) return;
+  switch (vpt) {
+    case 1: rmsnorm_kernel<1, ADD><<<M, threads, 0, st>>>(out, residual, x, w, eps, H); break;
+    case 2: rmsnorm_kernel<2, ADD><<<M, threads, 0, st>>>(out, residual, x, w, eps, H); break;
+    case 4: rmsnorm_kernel<4, ADD><<<M, threads, 0, st>>>(out, residual, x, w, eps, H); break;
+    default: rmsnorm_kernel<8, ADD><<<M, threads, 0, st>>>(out, residual, x, w, eps, H); break;
+  }
+}
+
+void launch_rmsnorm(void* out, const void* x, const void* w, float eps, int M, int H,
+                    hipStream_t st) {
+  dispatch<false>((uint16_t*)out, nullptr, (const uint16_t*)x, (const uint16_t*)w, eps, M, H, st);
+}
+
+void launch_add_rmsnorm(void* out, void* residual, const void* x, const void* w, float eps, int M,
+                        int H, hipStream_t st) {
+  dispatch<true>((uint16_t*)out, (uint16_t*)residual, (const uint16_t*)x, (const uint16_t*)w, eps,
+                 M, H, st);
+}
+
+}  // namespace mlop

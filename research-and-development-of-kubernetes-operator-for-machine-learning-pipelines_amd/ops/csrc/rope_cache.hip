@@ -1,0 +1,83 @@
+// Fused RoPE (K4) + paged KV-cache write (K5).
+//
+// Input is the raw output of the QKV projection, one row per token:
+//   qkv[t] = [ q (Hq*D) | k (Hkv*D) | v (Hkv*D) ]   (bf16)
+// The kernel rotates q and k (HF "rotate_half" layout, host-precomputed
+// cos/sin table: no on-device trig, cdna_hip_programming.md App. B) and
+//   * writes q to q_out[t, Hq, D] (contiguous, the attention kernel's input);
+//   * writes k to k_cache[block, Hkv, BS, D]   (token-major rows, the A operand of S^T = K.Q^T);
+//   * writes v to v_cache[block, Hkv, D, BS]   (dim-major, the A operand of O^T = V^T.P^T).
+// slot[t] = block*BS + offset, or < 0 for padding tokens (no cache write).
+#include "common.h"
+#include "launch.h"
+
+namespace mlop {
+
+__global__ void __launch_bounds__(256) rope_cache_kernel(
+    uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
+    const uint16_t* __restrict__ qkv, const int* __restrict__ pos, const float* __restrict__ cos_sin,
+    const int* __restrict__ slots, int Hq, int Hkv, int D, int qkv_stride, int BS) {
+  const int t = blockIdx.x;
+  const int half = D >> 1;
+  const int vph = half >> 3;  // 8-element vectors per half-head
+  const int p = pos[t];
+  const int slot = slots ? slots[t] : -1;
+  const float* cs = cos_sin + (size_t)p * D;
+  const uint16_t* row = qkv + (size_t)t * qkv_stride;
+  const int n_rope = (Hq + Hkv) * vph;
+  const int n_v = Hkv * (D >> 3);
+  const int blk = slot >= 0 ? slot / BS : 0;
+  const int off = slot >= 0 ? slot % BS : 0;
+  for (int it = threadIdx.x; it < n_rope + n_v; it += blockDim.x) {
+    if (it < n_rope) {
+      const int h = it / vph, c = (it % vph) * 8;
+      const uint16_t* src = row + h * D;  // q heads then k heads are contiguous
+      u32x4 a = *reinterpret_cast<const u32x4*>(src + c);
+      u32x4 b = *reinterpret_cast<const u32x4*>(src + half + c);
+      const float4* cp = reinterpret_cast<const float4*>(cs + c);
+      const float4* sp = reinterpret_cast<const float4*>(cs + half + c);
+      float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+      float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      u32x4 oa, ob;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x0 = lo_bf(a[j]), x1 = hi_bf(a[j]);
+        float y0 = lo_bf(b[j]), y1 = hi_bf(b[j]);
+        oa[j] = pack2(x0 * cc[2 * j] - y0 * ss[2 * j], x1 * cc[2 * j + 1] - y1 * ss[2 * j + 1]);
+        ob[j] = pack2(y0 * cc[2 * j] + x0 * ss[2 * j], y1 * cc[2 * j + 1] + x1 * ss[2 * j + 1]);
+      }
+      if (h < Hq) {
+        uint16_t* dst = q_out + ((size_t)t * Hq + h) * D;
+        *reinterpret_cast<u32x4*>(dst + c) = oa;
+        *reinterpret_cast<u32x4*>(dst + half + c) = ob;
+      } else if (slot >= 0) {
+        const int kh = h - Hq;
+        uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D;
+        *reinterpret_cast<u32x4*>(dst + c) = oa;
+        *reinterpret_cast<u32x4*>(dst + half + c) = ob;
+      }
+    } else if (slot >= 0) {
+      const int iv = it - n_rope;
+      const int kh = iv / (D >> 3), c = (iv % (D >> 3)) * 8;
+      u32x4 a = *reinterpret_cast<const u32x4*>(row + (Hq + Hkv + kh) * D + c);
+      uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c) * BS + off;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dst[(2 * j) * BS] = (uint16_t)(a[j] & 0xffff);
+        dst[(2 * j + 1) * BS] = (uint16_t)(a[j] >> 16);
+      }
+    }
+  }
+}
+
+void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qkv, const int* pos,
+                       const float* cos_sin, const int* slots, int T, int Hq, int Hkv, int D,
+                       int qkv_stride, int BS, hipStream_t st) {
+  if (T == 0) return;
+  rope_cache_kernel<<<T, 256, 0, st>>>((uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)v_cache,
+                                       (const uint16_t*)qkv, pos, cos_sin, slots, Hq, Hkv, D,
+                                       qkv_stride, BS);
+}
+
+}  // namespace mlop

@@ -1,0 +1,115 @@
+"""Process-group plumbing: one process per GPU, ``torch.distributed`` over RCCL.
+
+On ROCm the ``"nccl"`` backend IS RCCL (xGMI peer links inside a node); CPU
+tests use ``"gloo"`` with the same code.  A ``ParallelState`` carries the
+tensor-parallel (TP) and expert-parallel (EP) groups of one serving replica;
+data-parallel replicas (DP, the reference's per-predictor ``replicas`` /
+traffic split) are independent engines and share nothing.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_info():
+    """(rank, local_rank, world_size) from torchrun-style env vars (defaults: single process)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_distributed(backend: str | None = None, timeout_s: int = 600) -> bool:
+    """Initialise the default process group from env (MASTER_ADDR defaults to 127.0.0.1)."""
+    rank, local_rank, world = env_rank_info()
+    if world <= 1 or dist.is_initialized():
+        return dist.is_initialized()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        kw["device_id"] = torch.device("cuda", local_rank)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return True
+
+
+@dataclass
+class Group:
+    """A communicator: rank/size within it plus the torch group handle (None = world)."""
+
+    rank: int = 0
+    size: int = 1
+    handle: object = None
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(x, group=self.handle)
+        return x
+
+    def all_gather(self, x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+        if self.size == 1:
+            return x
+        parts = [torch.empty_like(x) for _ in range(self.size)]
+        dist.all_gather(parts, x.contiguous(), group=self.handle)
+        return torch.cat(parts, dim=dim)
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
+        if self.size == 1:
+            out.copy_(inp)
+            return out
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.handle)
+        return out
+
+    def broadcast(self, x: torch.Tensor, src_rank_in_group: int = 0) -> torch.Tensor:
+        if self.size > 1:
+            src = dist.get_global_rank(self.handle, src_rank_in_group) if self.handle is not None else src_rank_in_group
+            dist.broadcast(x, src=src, group=self.handle)
+        return x
+
+    def barrier(self):
+        if self.size > 1:
+            dist.barrier(group=self.handle)
+
+
+@dataclass
+class ParallelState:
+    tp: Group
+    ep: Group
+
+    @property
+    def tp_size(self) -> int:
+        return self.tp.size
+
+    @property
+    def tp_rank(self) -> int:
+        return self.tp.rank
+
+
+def single() -> ParallelState:
+    return ParallelState(tp=Group(), ep=Group())
+
+
+def make_parallel_state(tp_size: int = 1, ep_size: int = 1) -> ParallelState:
+    """Split the world into consecutive TP groups (TP inside a node: xGMI is point-to-point,
+    keep TP degree <= 8).  EP reuses the TP ranks (experts sharded over the same GPUs)."""
+    if not dist.is_initialized():
+        assert tp_size == 1 and ep_size == 1, "TP/EP > 1 needs torch.distributed"
+        return single()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    assert world % tp_size == 0, f"world {world} not divisible by tp {tp_size}"
+    tp_handle = None
+    for start in range(0, world, tp_size):
+        ranks = list(range(start, start + tp_size))
+        h = dist.new_group(ranks) if tp_size < world else None
+        if rank in ranks:
+            tp_handle = h
+    tp = Group(rank=rank % tp_size, size=tp_size, handle=tp_handle)
+    ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=tp_handle)
+    return ParallelState(tp=tp, ep=ep)

@@ -1,0 +1,185 @@
+"""Step metadata for the ragged paged-attention kernel.
+
+All int32 metadata of a step lives in ONE pinned host buffer with a fixed
+layout and is shipped with ONE async H2D copy into ONE device buffer; the
+kernel arguments are fixed views into it, so hipGraph-captured decode steps
+see new values on every replay without re-capture.
+
+Sequence-indexed arrays (q_start, q_len, ctx_len, block_tables) are indexed by
+a stable *row* (the sequence's slot in [0, max_seqs)), so the host only
+touches the rows that changed; tiles (16 MFMA q-rows = 16/G query tokens)
+point at rows.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .kv_cache import BLOCK_SIZE
+
+
+@dataclass
+class AttnMeta:
+    positions: torch.Tensor   # int32 [T]
+    slots: torch.Tensor       # int32 [T]
+    block_tables: torch.Tensor  # int32 [max_seqs, max_blocks]
+    tile_seq: torch.Tensor    # int32 [num_tiles]
+    tile_q0: torch.Tensor     # int32 [num_tiles]
+    q_start: torch.Tensor     # int32 [max_seqs]
+    q_len: torch.Tensor       # int32 [max_seqs]
+    ctx_len: torch.Tensor     # int32 [max_seqs]
+    part_tokens: int
+    nparts: int
+    part_o: torch.Tensor
+    part_ml: torch.Tensor
+    logits_idx: torch.Tensor  # int64 [n_logits]
+    num_tokens: int
+
+
+def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int = 256,
+                    target_wgs: int = 1024) -> tuple[int, int]:
+    """Split the KV range so a launch has >= ~target_wgs workgroups (256 CUs),
+    partitions no shorter than ``min_part`` tokens; one partition when the batch
+    already fills the chip (no reduce pass)."""
+    max_ctx = max(32, max_ctx)
+    base = max(1, num_tiles * n_kv)
+    if base >= target_wgs // 2:
+        return ((max_ctx + 31) // 32) * 32, 1
+    nparts = max(1, min((max_ctx + min_part - 1) // min_part, (target_wgs + base - 1) // base))
+    part = (max_ctx + nparts - 1) // nparts
+    part = ((part + 31) // 32) * 32
+    nparts = (max_ctx + part - 1) // part
+    return part, nparts
+
+
+class MetaBuffers:
+    """Fixed-layout pinned host + device buffers for up to ``max_tokens`` tokens
+    and ``max_seqs`` concurrent sequences."""
+
+    def __init__(self, max_tokens: int, max_seqs: int, max_blocks_per_seq: int, group: int,
+                 n_kv: int, max_model_len: int, device):
+        self.device = torch.device(device)
+        self.max_tokens, self.max_seqs, self.mb = max_tokens, max_seqs, max_blocks_per_seq
+        self.G, self.n_kv, self.max_model_len = group, n_kv, max_model_len
+        self.qt = 16 // group
+        self.max_tiles = max_tokens  # worst case: one tile per token
+        sizes = [("positions", max_tokens), ("slots", max_tokens), ("tile_seq", self.max_tiles),
+                 ("tile_q0", self.max_tiles), ("q_start", max_seqs), ("q_len", max_seqs),
+                 ("ctx_len", max_seqs), ("block_tables", max_seqs * max_blocks_per_seq)]
+        self.off = {}
+        o = 0
+        for name, n in sizes:
+            self.off[name] = (o, n)
+            o += (n + 63) // 64 * 64
+        pin = self.device.type == "cuda"
+        self.h = torch.zeros(o, dtype=torch.int32, pin_memory=pin)
+        self.hn = self.h.numpy()
+        self.d = torch.zeros(o, dtype=torch.int32, device=self.device)
+        self.ids_h = torch.zeros(max_tokens, dtype=torch.int64, pin_memory=pin)
+        self.ids_hn = self.ids_h.numpy()
+        self.ids_d = torch.zeros(max_tokens, dtype=torch.int64, device=self.device)
+        self.lidx_h = torch.zeros(max_seqs, dtype=torch.int64, pin_memory=pin)
+        self.lidx_hn = self.lidx_h.numpy()
+        self.lidx_d = torch.zeros(max_seqs, dtype=torch.int64, device=self.device)
+        # partial-softmax workspace for the split-KV path (sized for the worst launch)
+        # plan_partitions only splits launches with < target/2 base workgroups, so
+        # tiles * n_kv * nparts stays <= ~2 * target: size for 4096 partial tiles
+        self.wp_capacity = 4096
+        self.part_o = torch.empty(self.wp_capacity * 16 * 128, dtype=torch.float32, device=self.device)
+        self.part_ml = torch.empty(self.wp_capacity * 16 * 2, dtype=torch.float32, device=self.device)
+        bt = self.view_h("block_tables").reshape(max_seqs, max_blocks_per_seq)
+        self.bt_h = bt  # numpy view [max_seqs, mb]
+
+    def view_h(self, name):
+        o, n = self.off[name]
+        return self.hn[o:o + n]
+
+    def view_d(self, name, n=None):
+        o, cap = self.off[name]
+        return self.d[o:o + (cap if n is None else n)]
+
+    def upload(self, n_ids: int, n_logits: int):
+        """One async H2D of the metadata (+ ids, logits index) on the current stream."""
+        self.d.copy_(self.h, non_blocking=True)
+        if n_ids:
+            self.ids_d[:n_ids].copy_(self.ids_h[:n_ids], non_blocking=True)
+        if n_logits:
+            self.lidx_d[:n_logits].copy_(self.lidx_h[:n_logits], non_blocking=True)
+
+    def meta(self, num_tokens: int, num_tiles: int, n_logits: int, part_tokens: int, nparts: int) -> AttnMeta:
+        if nparts > 1:
+            assert num_tiles * self.n_kv * nparts <= self.wp_capacity, "partial workspace too small"
+        return AttnMeta(
+            positions=self.view_d("positions", num_tokens), slots=self.view_d("slots", num_tokens),
+            block_tables=self.view_d("block_tables").view(self.max_seqs, self.mb),
+            tile_seq=self.view_d("tile_seq", num_tiles), tile_q0=self.view_d("tile_q0", num_tiles),
+            q_start=self.view_d("q_start"), q_len=self.view_d("q_len"), ctx_len=self.view_d("ctx_len"),
+            part_tokens=part_tokens, nparts=nparts, part_o=self.part_o, part_ml=self.part_ml,
+            logits_idx=self.lidx_d[:n_logits], num_tokens=num_tokens)
+
+    def fill(self, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits=None):
+        """Fill host arrays for a ragged batch.
+
+        rows[i]: the row slot of batch sequence i; q_lens[i] new tokens whose
+        KV is written this step; ctx_lens[i] context length AFTER this step;
+        token_ids_per_seq[i]: the q_len input ids. Block tables must already
+        hold the pages covering ctx_lens.  want_logits[i] (default all): emit a
+        logits row for sequence i's last token.  Returns (T, num_tiles, n_logits)."""
+        nl = 0
+        pos_h, slot_h = self.view_h("positions"), self.view_h("slots")
+        ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
+        qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")
+        t = 0
+        nt = 0
+        qt = self.qt
+        for i, row in enumerate(rows):
+            ql, cl = int(q_lens[i]), int(ctx_lens[i])
+            qs_h[row], ql_h[row], cl_h[row] = t, ql, cl
+            p = np.arange(cl - ql, cl, dtype=np.int32)
+            pos_h[t:t + ql] = p
+            slot_h[t:t + ql] = self.bt_h[row, p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
+            self.ids_hn[t:t + ql] = token_ids_per_seq[i]
+            ntile = (ql + qt - 1) // qt
+            ts_h[nt:nt + ntile] = row
+            tq_h[nt:nt + ntile] = np.arange(ntile, dtype=np.int32) * qt
+            nt += ntile
+            t += ql
+            if want_logits is None or want_logits[i]:
+                self.lidx_hn[nl] = t - 1
+                nl += 1
+        return t, nt, nl
+
+    def fill_decode(self, rows: np.ndarray, ctx_lens: np.ndarray, last_tokens: np.ndarray, pad_to: int):
+        """Vectorised decode fill: one query token per sequence, padded to the
+        graph bucket ``pad_to`` with rows that attend to nothing."""
+        B = len(rows)
+        pos_h, slot_h = self.view_h("positions"), self.view_h("slots")
+        ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
+        qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")
+        p = (ctx_lens - 1).astype(np.int32)
+        pos_h[:B] = p
+        slot_h[:B] = self.bt_h[rows, p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
+        ts_h[:B] = rows
+        tq_h[:B] = 0
+        qs_h[rows] = np.arange(B, dtype=np.int32)
+        ql_h[rows] = 1
+        cl_h[rows] = ctx_lens
+        self.ids_hn[:B] = last_tokens
+        self.lidx_hn[:B] = np.arange(B)
+        if pad_to > B:
+            pad_rows = self.pad_rows(pad_to - B)
+            pos_h[B:pad_to] = 0
+            slot_h[B:pad_to] = -1
+            ts_h[B:pad_to] = pad_rows
+            tq_h[B:pad_to] = 0
+            qs_h[pad_rows] = np.arange(B, pad_to, dtype=np.int32)
+            ql_h[pad_rows] = 1
+            cl_h[pad_rows] = 0
+            self.ids_hn[B:pad_to] = 0
+            self.lidx_hn[B:pad_to] = np.arange(B, pad_to)
+
+    def pad_rows(self, n: int) -> np.ndarray:
+        """Rows reserved for graph padding: the top of the row space (never handed to sequences)."""
+        return np.arange(self.max_seqs - n, self.max_seqs, dtype=np.int32)

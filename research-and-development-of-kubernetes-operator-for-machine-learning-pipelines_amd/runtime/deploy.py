@@ -1,0 +1,44 @@
+"""Runtime construction: model + engine from a model name / predictor spec.
+
+``build_engine`` is what a predictor process runs at start-up (random-init
+weights on device, KV cache sized for 288 GB HBM, decode hipGraph capture).
+``deploy_for_bench`` drives the same start-up through the control plane when
+the operator is available (CR -> SeldonDeployment -> in-process predictor ->
+ready), returning the CR->ready time the headline metric reports.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..models import build_model
+from .engine import Engine, EngineConfig
+
+
+def build_engine(model: str = "llama3-8b", device="cuda", seed: int = 0, tp_state=None,
+                 dtype=torch.bfloat16, **engine_kwargs) -> Engine:
+    m = build_model(model, device=device, dtype=dtype, pstate=tp_state, seed=seed)
+    return Engine(m, EngineConfig(**engine_kwargs))
+
+
+def deploy_for_bench(model: str, device, use_operator: bool = True, seed: int = 0,
+                     engine_kwargs: dict | None = None):
+    engine_kwargs = engine_kwargs or {}
+    if use_operator:
+        try:
+            from ..controller.local import deploy_and_wait
+        except ImportError:  # control plane not importable: direct start-up
+            use_operator = False
+    t0 = time.perf_counter()
+    if use_operator:
+        engine, info = deploy_and_wait(model=model, device=device, seed=seed, engine_kwargs=engine_kwargs)
+        ready = time.perf_counter() - t0
+        info["path"] = "operator"
+        return engine, ready, info
+    engine = build_engine(model, device=device, seed=seed, **engine_kwargs)
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize()
+    ready = time.perf_counter() - t0
+    return engine, ready, {"path": "direct", "weight_gb": round(engine.model.weight_bytes() / 1e9, 2),
+                           "kv_blocks": engine.kv.num_blocks}

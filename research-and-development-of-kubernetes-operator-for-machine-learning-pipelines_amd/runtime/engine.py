@@ -1,0 +1,392 @@
+"""Continuous-batching inference engine (G5) with hipGraph-captured decode (G1).
+
+One engine per model replica (DP replica = one engine; a TP replica runs one
+engine per rank in lock-step, rank 0 owning the scheduler and broadcasting
+step metadata).
+
+Step policy:
+  * prefill steps pack up to ``max_num_batched_tokens`` prompt tokens of
+    admitted requests (chunked: a long prompt spans several steps);
+  * decode steps run every running sequence, one token each, replaying the
+    hipGraph captured for the smallest batch bucket >= B (padded rows attend to
+    nothing), so a decode step costs one graph launch + one metadata H2D + one
+    token D2H;
+  * a prefill step is taken when requests wait and either nothing is decoding,
+    enough requests are queued (``prefill_min_batch``) or the oldest has waited
+    ``max_decode_gap`` decode steps (bounded TTFT without fragmenting decode);
+  * KV pages come from a free-list; on exhaustion the newest running sequence
+    is preempted (pages freed, recomputed later).
+"""
+from __future__ import annotations
+
+import collections
+import itertools
+import time
+from dataclasses import dataclass, field
+from enum import Enum
+
+import numpy as np
+import torch
+
+from .attn_meta import MetaBuffers, plan_partitions
+from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, blocks_needed
+from .sampler import Sampler, SamplingParams
+
+
+class Status(Enum):
+    WAITING = 0
+    PREFILL = 1
+    RUNNING = 2
+    FINISHED = 3
+
+
+@dataclass
+class Sequence:
+    seq_id: int
+    prompt: list
+    params: SamplingParams
+    output: list = field(default_factory=list)
+    blocks: list = field(default_factory=list)
+    row: int = -1
+    num_cached: int = 0
+    status: Status = Status.WAITING
+    arrival: float = field(default_factory=time.perf_counter)
+    first_token_time: float | None = None
+    finish_time: float | None = None
+    finish_reason: str | None = None
+
+    @property
+    def length(self) -> int:
+        return len(self.prompt) + len(self.output)
+
+    def token_at(self, i: int) -> int:
+        n = len(self.prompt)
+        return self.prompt[i] if i < n else self.output[i - n]
+
+    def tokens(self, a: int, b: int):
+        n = len(self.prompt)
+        if b <= n:
+            return self.prompt[a:b]
+        if a >= n:
+            return self.output[a - n:b - n]
+        return list(self.prompt[a:]) + self.output[:b - n]
+
+
+@dataclass
+class EngineConfig:
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 4096
+    num_kv_blocks: int | None = None       # None: size from kv_cache_bytes / free HBM
+    kv_cache_bytes: int | None = None
+    gpu_memory_utilization: float = 0.90
+    use_graphs: bool = True
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+    prefill_min_batch: int = 1
+    max_decode_gap: int = 0
+    seed: int = 0
+
+
+@dataclass
+class StepOutput:
+    seq_id: int
+    token: int
+    finished: bool
+    finish_reason: str | None = None
+
+
+class Engine:
+    def __init__(self, model, cfg: EngineConfig | None = None):
+        self.model = model
+        self.cfg = cfg = cfg or EngineConfig()
+        self.device = model.device
+        mc = model.cfg
+        self.max_model_len = min(cfg.max_model_len, mc.max_position)
+        nb = cfg.num_kv_blocks or self._auto_blocks()
+        self.kv = KVCache(mc.num_layers, nb, model.n_kv, mc.head_dim, self.device, model.dtype)
+        self.alloc = BlockAllocator(nb)
+        self.max_blocks_per_seq = blocks_needed(self.max_model_len)
+        self.buckets = sorted(b for b in cfg.graph_buckets if b <= cfg.max_num_seqs) or [cfg.max_num_seqs]
+        if self.buckets[-1] < cfg.max_num_seqs:
+            self.buckets.append(cfg.max_num_seqs)
+        self.G = model.n_q // model.n_kv
+        self.meta = MetaBuffers(max(cfg.max_num_batched_tokens, cfg.max_num_seqs),
+                                cfg.max_num_seqs + self.buckets[-1], self.max_blocks_per_seq,
+                                self.G, model.n_kv, self.max_model_len, self.device)
+        self.free_rows = list(range(cfg.max_num_seqs - 1, -1, -1))
+        self.sampler = Sampler(self.device, cfg.seed)
+        self.waiting: collections.deque[Sequence] = collections.deque()
+        self.prefilling: list[Sequence] = []
+        self.running: list[Sequence] = []
+        self.seqs: dict[int, Sequence] = {}
+        self._ids = itertools.count()
+        self._decode_since_prefill = 0
+        self.graphs: dict[int, tuple] = {}
+        self.graph_pool = None
+        self.stats = collections.Counter()
+        if cfg.use_graphs and self.device.type == "cuda":
+            self.capture_graphs()
+
+    # ----------------------------------------------------------- sizing --
+    def _auto_blocks(self) -> int:
+        mc, m = self.model.cfg, self.model
+        if self.cfg.kv_cache_bytes:
+            budget = self.cfg.kv_cache_bytes
+        elif self.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.device)
+            reserve = total * (1 - self.cfg.gpu_memory_utilization) + 4 * 2**30
+            budget = int(max(free - reserve, 2**30))
+        else:
+            budget = 64 * 2**20
+        need = self.cfg.max_num_seqs * blocks_needed(min(self.cfg.max_model_len, mc.max_position)) + 1
+        nb = blocks_for_budget(budget, mc.num_layers, m.n_kv, mc.head_dim)
+        return int(min(nb, need))
+
+    # -------------------------------------------------------- requests --
+    def add_request(self, prompt, params: SamplingParams | None = None, seq_id: int | None = None) -> Sequence:
+        params = params or SamplingParams()
+        prompt = list(prompt)
+        if not prompt:
+            raise ValueError("empty prompt")
+        if len(prompt) >= self.max_model_len:
+            raise ValueError(f"prompt of {len(prompt)} tokens exceeds max_model_len {self.max_model_len}")
+        sid = next(self._ids) if seq_id is None else seq_id
+        seq = Sequence(sid, prompt, params)
+        self.seqs[sid] = seq
+        self.waiting.append(seq)
+        return seq
+
+    def abort(self, seq_id: int) -> None:
+        seq = self.seqs.get(seq_id)
+        if seq is None or seq.status == Status.FINISHED:
+            return
+        for lst in (self.prefilling, self.running):
+            if seq in lst:
+                lst.remove(seq)
+        if seq in self.waiting:
+            self.waiting.remove(seq)
+        self._finish(seq, "abort")
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.prefilling or self.running)
+
+    @property
+    def num_running(self) -> int:
+        return len(self.running) + len(self.prefilling)
+
+    def kv_usage(self) -> float:
+        return self.alloc.usage()
+
+    # ------------------------------------------------------ bookkeeping --
+    def _ensure_blocks(self, seq: Sequence, ctx: int) -> bool:
+        need = blocks_needed(ctx) - len(seq.blocks)
+        if need <= 0:
+            return True
+        if not self.alloc.can_allocate(need):
+            return False
+        new = self.alloc.allocate(need)
+        start = len(seq.blocks)
+        seq.blocks.extend(new)
+        self.meta.bt_h[seq.row, start:start + need] = new
+        return True
+
+    def _release(self, seq: Sequence):
+        if seq.blocks:
+            self.alloc.free(seq.blocks)
+            seq.blocks = []
+        if seq.row >= 0:
+            self.free_rows.append(seq.row)
+            seq.row = -1
+        seq.num_cached = 0
+
+    def _finish(self, seq: Sequence, reason: str):
+        seq.status = Status.FINISHED
+        seq.finish_reason = reason
+        seq.finish_time = time.perf_counter()
+        self._release(seq)
+
+    def _preempt(self, seq: Sequence):
+        self.stats["preemptions"] += 1
+        self._release(seq)
+        seq.status = Status.WAITING
+        self.waiting.appendleft(seq)
+
+    # ------------------------------------------------------- scheduling --
+    def _want_prefill(self) -> bool:
+        if self.prefilling:
+            return True
+        if not self.waiting or not self.free_rows:
+            return False
+        if not self.running:
+            return True
+        c = self.cfg
+        return (len(self.waiting) >= c.prefill_min_batch
+                or (c.max_decode_gap and self._decode_since_prefill >= c.max_decode_gap))
+
+    def step(self) -> list[StepOutput]:
+        if self._want_prefill():
+            out = self._prefill_step()
+            if out is not None:
+                self._decode_since_prefill = 0
+                return out
+        if self.running:
+            self._decode_since_prefill += 1
+            return self._decode_step()
+        return []
+
+    # ---------------------------------------------------------- prefill --
+    def _prefill_step(self):
+        budget = self.cfg.max_num_batched_tokens
+        batch, chunks = [], []
+        for seq in list(self.prefilling):
+            if budget <= 0:
+                break
+            n = min(seq.length - seq.num_cached, budget)
+            if not self._ensure_blocks(seq, seq.num_cached + n):
+                break
+            batch.append(seq)
+            chunks.append(n)
+            budget -= n
+        while budget > 0 and self.waiting and self.free_rows:
+            seq = self.waiting[0]
+            n = min(seq.length, budget)
+            seq.row = self.free_rows.pop()
+            if not self._ensure_blocks(seq, n):
+                self.free_rows.append(seq.row)
+                seq.row = -1
+                break
+            self.waiting.popleft()
+            seq.status = Status.PREFILL
+            self.prefilling.append(seq)
+            batch.append(seq)
+            chunks.append(n)
+            budget -= n
+        if not batch:
+            return None
+        rows = [s.row for s in batch]
+        ctx = [s.num_cached + n for s, n in zip(batch, chunks)]
+        toks = [s.tokens(s.num_cached, c) for s, c in zip(batch, ctx)]
+        done = [c == s.length for s, c in zip(batch, ctx)]
+        T, nt, nl = self.meta.fill(rows, chunks, ctx, toks, want_logits=done)
+        part, nparts = plan_partitions(nt, self.model.n_kv, max(ctx))
+        self.meta.upload(T, nl)
+        meta = self.meta.meta(T, nt, nl, part, nparts)
+        hidden = self.model.forward(self.meta.ids_d[:T], meta, self.kv)
+        tokens = None
+        if nl:
+            logits = self.model.logits(hidden[meta.logits_idx])
+            done_seqs = [s for s, d in zip(batch, done) if d]
+            tokens = self.sampler(logits, [s.params for s in done_seqs]).tolist()
+        else:
+            torch.cuda.synchronize() if self.device.type == "cuda" else None
+        self.stats["prefill_steps"] += 1
+        self.stats["prefill_tokens"] += T
+        outs = []
+        ti = 0
+        for s, c, d in zip(batch, ctx, done):
+            s.num_cached = c
+            if d:
+                self.prefilling.remove(s)
+                s.status = Status.RUNNING
+                self.running.append(s)
+                outs.append(self._append(s, tokens[ti]))
+                ti += 1
+        return outs
+
+    # ----------------------------------------------------------- decode --
+    def _decode_step(self):
+        # every running seq needs a slot for its last token's KV
+        i = 0
+        while i < len(self.running):
+            s = self.running[i]
+            if self._ensure_blocks(s, s.length):
+                i += 1
+                continue
+            victim = self.running.pop()  # newest
+            self._preempt(victim)
+            if victim is s:
+                continue
+        B = len(self.running)
+        if B == 0:
+            return []
+        rows = np.fromiter((s.row for s in self.running), dtype=np.int32, count=B)
+        ctx = np.fromiter((s.length for s in self.running), dtype=np.int32, count=B)
+        last = np.fromiter((s.output[-1] if s.output else s.prompt[-1] for s in self.running),
+                           dtype=np.int64, count=B)
+        bucket = next((b for b in self.buckets if b >= B), None)
+        g = self.graphs.get(bucket) if bucket is not None else None
+        if g is not None:
+            self.meta.fill_decode(rows, ctx, last, pad_to=bucket)
+            self.meta.upload(bucket, bucket)
+            graph, logits_buf = g
+            graph.replay()
+            logits = logits_buf[:B]
+            self.stats["graph_steps"] += 1
+        else:
+            self.meta.fill_decode(rows, ctx, last, pad_to=B)
+            part, nparts = plan_partitions(B, self.model.n_kv, int(ctx.max()))
+            self.meta.upload(B, B)
+            meta = self.meta.meta(B, B, B, part, nparts)
+            hidden = self.model.forward(self.meta.ids_d[:B], meta, self.kv)
+            logits = self.model.logits(hidden[meta.logits_idx])
+            self.stats["eager_decode_steps"] += 1
+        tokens = self.sampler(logits, [s.params for s in self.running]).tolist()
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += B
+        outs = []
+        for s, t in zip(list(self.running), tokens):
+            s.num_cached = s.length
+            outs.append(self._append(s, t))
+        return outs
+
+    def _append(self, s: Sequence, tok: int) -> StepOutput:
+        s.output.append(int(tok))
+        if s.first_token_time is None:
+            s.first_token_time = time.perf_counter()
+        p = s.params
+        reason = None
+        if not p.ignore_eos and (tok == self.model.cfg.eos_token_id or tok in p.stop_token_ids):
+            reason = "stop"
+        elif len(s.output) >= p.max_tokens:
+            reason = "length"
+        elif s.length >= self.max_model_len:
+            reason = "length"
+        if reason:
+            if s in self.running:
+                self.running.remove(s)
+            self._finish(s, reason)
+        return StepOutput(s.seq_id, int(tok), reason is not None, reason)
+
+    # ----------------------------------------------------------- graphs --
+    def capture_graphs(self):
+        """Capture one decode graph per batch bucket (largest first, shared pool)."""
+        m = self.model
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        empty = np.zeros(0, dtype=np.int32)
+        with torch.cuda.stream(stream):
+            for b in sorted(self.buckets, reverse=True):
+                self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=b)
+                self.meta.upload(b, b)
+                part, nparts = plan_partitions(b, m.n_kv, self.max_model_len)
+                meta = self.meta.meta(b, b, b, part, nparts)
+                ids = self.meta.ids_d[:b]
+                for _ in range(2):  # warm-up (allocator, lazy init)
+                    m.logits(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                stream.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
+                    logits = m.logits(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                self.graphs[b] = (g, logits)
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------ offline API --
+    def generate(self, prompts, params: SamplingParams | list | None = None):
+        if not isinstance(params, list):
+            params = [params or SamplingParams()] * len(prompts)
+        seqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+        while any(s.status != Status.FINISHED for s in seqs):
+            self.step()
+        return [s.output for s in seqs]

@@ -1,0 +1,179 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 oracle
+(``mlopamd.ops.reference``), on the MI355X."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from mlopamd import ops
+from mlopamd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+bf = torch.bfloat16
+
+
+def close(a, b, atol=2e-2, rtol=2e-2):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("M,H", [(1, 4096), (7, 4096), (33, 8192), (5, 1024), (3, 5120)])
+def test_rmsnorm(gpu, M, H):
+    x = torch.randn(M, H, device=gpu, dtype=bf)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x, w, 1e-5))
+
+
+@pytest.mark.parametrize("M,H", [(1, 4096), (19, 4096), (4, 8192)])
+def test_add_rmsnorm(gpu, M, H):
+    x = torch.randn(M, H, device=gpu, dtype=bf)
+    r = torch.randn(M, H, device=gpu, dtype=bf)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    y_ref, r_ref = ref.add_rmsnorm(x, r, w, 1e-5)
+    r2 = r.clone()
+    y = ops.add_rmsnorm(x, r2, w, 1e-5)
+    close(r2, r_ref, atol=0, rtol=0)
+    close(y, y_ref)
+
+
+@pytest.mark.parametrize("M,I", [(1, 14336), (37, 14336), (8, 3584)])
+def test_silu_mul(gpu, M, I):
+    x = torch.randn(M, 2 * I, device=gpu, dtype=bf)
+    close(ops.silu_mul(x), ref.silu_mul(x))
+
+
+def test_embedding(gpu):
+    table = torch.randn(1000, 256, device=gpu, dtype=bf)
+    ids = torch.randint(0, 2000, (77,), device=gpu)
+    close(ops.embedding(ids, table, 500), ref.embedding(ids, table, 500), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 16)])
+def test_rope_cache(gpu, Hq, Hkv):
+    from mlopamd.models.layers import rope_table
+
+    D, NB, BS, T = 128, 40, 16, 29
+    cs = rope_table(D, 4096, 5e5, device=gpu)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=gpu, dtype=bf)
+    pos = torch.randint(0, 4000, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:T].to(torch.int32)
+    slots[3] = -1
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = ops.rope_cache(qkv, pos, cs, slots, kc, vc, Hq)
+    q_ref = ref.rope_cache(qkv.cpu(), pos.cpu(), cs.cpu(), slots.cpu(), kc2.cpu(), vc2.cpu(), Hq)
+    close(q, q_ref)
+    # cache contents (ref wrote into the CPU copies)
+    kr, vr = kc2.cpu(), vc2.cpu()
+    ref.rope_cache(qkv.cpu(), pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(kc, kr)
+    close(vc, vr, atol=0, rtol=0)
+
+
+class Meta:
+    pass
+
+
+def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shuffle_rows=True):
+    from mlopamd.runtime.attn_meta import plan_partitions
+
+    S = len(q_lens)
+    MB = max(1, max((c + 15) // 16 for c in ctx_lens))
+    rows = np.random.permutation(S + 3)[:S] if shuffle_rows else np.arange(S)
+    R = S + 3
+    bt = np.zeros((R, MB), dtype=np.int32)
+    pages = np.random.permutation(np.arange(1, NB))
+    p = 0
+    for i, c in enumerate(ctx_lens):
+        n = (c + 15) // 16
+        bt[rows[i], :n] = pages[p:p + n]
+        p += n
+    qt = 16 // G
+    q_start = np.zeros(R, np.int32); q_len = np.zeros(R, np.int32); ctx = np.zeros(R, np.int32)
+    ts, tq = [], []
+    t = 0
+    for i in range(S):
+        r = rows[i]
+        q_start[r], q_len[r], ctx[r] = t, q_lens[i], ctx_lens[i]
+        nt = (q_lens[i] + qt - 1) // qt
+        ts += [r] * nt
+        tq += list(range(0, nt * qt, qt))
+        t += q_lens[i]
+    m = Meta()
+    d = lambda a: torch.tensor(np.asarray(a), dtype=torch.int32, device=gpu)  # noqa: E731
+    m.block_tables, m.q_start, m.q_len, m.ctx_len = d(bt), d(q_start), d(q_len), d(ctx)
+    m.tile_seq, m.tile_q0 = d(ts), d(tq)
+    if part_tokens is None:
+        part_tokens, nparts = plan_partitions(len(ts), Hkv, max(ctx_lens))
+    m.part_tokens, m.nparts = part_tokens, nparts
+    m.part_o = torch.empty(len(ts) * Hkv * nparts * 16 * 128, device=gpu)
+    m.part_ml = torch.empty(len(ts) * Hkv * nparts * 16 * 2, device=gpu)
+    return m, t
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
+@pytest.mark.parametrize("case", ["decode", "prefill", "mixed", "split"])
+def test_paged_attention(gpu, Hq, Hkv, case):
+    torch.manual_seed(0)
+    np.random.seed(0)
+    G = Hq // Hkv
+    NB = 400
+    if case == "decode":
+        q_lens, ctx_lens = [1] * 9, [1, 15, 16, 17, 100, 511, 512, 700, 1300]
+    elif case == "prefill":
+        q_lens = [1, 7, 64, 200]
+        ctx_lens = list(q_lens)
+    elif case == "mixed":
+        q_lens, ctx_lens = [1, 37, 1, 130], [300, 90, 64, 1000]
+    else:  # forced split-KV with a reduce pass
+        q_lens, ctx_lens = [1, 1, 3], [1500, 33, 900]
+    kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    kw = dict(part_tokens=256, nparts=6) if case == "split" else {}
+    m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, **kw)
+    q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
+    out = ops.paged_attention(q, kc, vc, m)
+    exp = ref.paged_attention(q, kc, vc, m)
+    close(out, exp, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_spike_rescale(gpu):
+    """Force the online-softmax rescale branch: a late key dominates."""
+    Hq, Hkv = 32, 8
+    kc = 0.1 * torch.randn(64, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(64, Hkv, 128, 16, device=gpu, dtype=bf)
+    m, T = make_meta(gpu, [1, 4], [600, 700], Hkv, 4, 64, shuffle_rows=False)
+    q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
+    bt = m.block_tables.cpu()
+    page = int(bt[0, 30])
+    kc[page, :, 5, :] = 3.0 * q[0, ::4, :].to(bf)  # key 485 aligned with the query
+    out = ops.paged_attention(q, kc, vc, m)
+    close(out, ref.paged_attention(q, kc, vc, m), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("n,V", [(1, 128256), (64, 128256), (5, 32000), (3, 1000)])
+def test_argmax(gpu, n, V):
+    x = torch.randn(n, V, device=gpu)
+    assert torch.equal(ops.argmax(x).cpu(), x.argmax(-1).cpu())
+
+
+def test_sample_matches_reference(gpu):
+    torch.manual_seed(1)
+    n, V = 16, 32000
+    x = 3 * torch.randn(n, V, device=gpu)
+    temps = torch.tensor([0.0, 0.7, 1.0, 1.3] * 4, device=gpu)
+    ks = torch.tensor([0, 1, 50, 0] * 4, dtype=torch.int32, device=gpu)
+    ps = torch.tensor([1.0, 1.0, 0.9, 0.5] * 4, device=gpu)
+    u = torch.rand(n, device=gpu)
+    got = ops.sample(x, temps, ks, ps, u).cpu()
+    exp = ref_sample = None
+    from mlopamd.runtime.sampler import sample_reference
+
+    exp = sample_reference(x.cpu(), temps.cpu(), ks.cpu(), ps.cpu(), u.cpu())
+    assert (got == exp).float().mean() >= 0.9, (got, exp)
+    # temperature 0 and top_k 1 are exact argmax
+    am = x.argmax(-1).cpu()
+    for i in range(n):
+        if float(temps[i]) == 0 or int(ks[i]) == 1:
+            assert int(got[i]) == int(am[i])
