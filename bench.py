@@ -75,7 +75,7 @@ def main(argv=None):
         engine_kwargs=dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
                            max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
                            prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
-                           seed=a.seed + rank))
+                           ))
     from mlopamd.runtime.sampler import SamplingParams
 
     rng = np.random.default_rng(1234 + rank)

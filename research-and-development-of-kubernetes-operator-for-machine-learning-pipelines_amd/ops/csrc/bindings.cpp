@@ -7,7 +7,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 #include <cmath>
 
 #include "launch.h"
@@ -34,7 +34,7 @@ void rmsnorm(Tensor out, Tensor x, Tensor w, double eps) {
   const int64_t H = x.size(-1);
   TORCH_CHECK(H % 8 == 0 && H <= 65536, "hidden size must be a multiple of 8");
   TORCH_CHECK(w.numel() == H && out.numel() == x.numel(), "rmsnorm shape mismatch");
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   mlop::launch_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), (float)eps,
                        (int)(x.numel() / H), (int)H, cur_stream());
 }
@@ -45,7 +45,7 @@ void add_rmsnorm(Tensor out, Tensor residual, Tensor x, Tensor w, double eps) {
   TORCH_CHECK(H % 8 == 0 && H <= 65536, "hidden size must be a multiple of 8");
   TORCH_CHECK(w.numel() == H && out.numel() == x.numel() && residual.numel() == x.numel(),
               "add_rmsnorm shape mismatch");
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   mlop::launch_add_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(), w.data_ptr(),
                            (float)eps, (int)(x.numel() / H), (int)H, cur_stream());
 }
@@ -67,7 +67,7 @@ void rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor qkv, Tensor
   TORCH_CHECK(qkv.size(0) == T && qkv.size(-1) >= (Hq + 2 * Hkv) * D, "qkv shape");
   TORCH_CHECK(pos.numel() == T && slots.numel() == T, "pos/slots length");
   TORCH_CHECK(cos_sin.size(1) == D, "cos_sin must be [max_pos, D]");
-  c10::hip::HIPGuard g(qkv.device());
+  c10::DeviceGuard g(qkv.device());
   mlop::launch_rope_cache(q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), qkv.data_ptr(),
                           pos.data_ptr<int>(), cos_sin.data_ptr<float>(), slots.data_ptr<int>(), T,
                           Hq, Hkv, D, (int)qkv.stride(0), BS, cur_stream());
@@ -79,7 +79,7 @@ void silu_mul(Tensor out, Tensor x) {
   TORCH_CHECK(I2 % 16 == 0, "gate_up width must be a multiple of 16");
   const int64_t M = x.numel() / I2;
   TORCH_CHECK(out.numel() == M * (I2 / 2), "silu_mul shape mismatch");
-  c10::hip::HIPGuard g(x.device());
+  c10::DeviceGuard g(x.device());
   mlop::launch_silu_mul(out.data_ptr(), x.data_ptr(), (int)M, (int)(I2 / 2), cur_stream());
 }
 
@@ -88,7 +88,7 @@ void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_start) {
   TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids int64");
   const int64_t H = table.size(1);
   TORCH_CHECK(H % 8 == 0 && out.size(-1) == H && out.numel() == ids.numel() * H, "embedding shape");
-  c10::hip::HIPGuard g(table.device());
+  c10::DeviceGuard g(table.device());
   mlop::launch_embedding(out.data_ptr(), table.data_ptr(), ids.data_ptr<int64_t>(),
                          (int)ids.numel(), (int)H, vocab_start, vocab_start + table.size(0),
                          cur_stream());
@@ -126,7 +126,7 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor
                     part_ml.numel() >= (int64_t)num_tiles * Hkv * nparts * 16 * 2,
                 "partial workspace too small");
   }
-  c10::hip::HIPGuard g(q.device());
+  c10::DeviceGuard g(q.device());
   const float scale_log2 = (float)(scale * 1.4426950408889634);
   mlop::launch_paged_attention(
       out.data_ptr(), nparts > 1 ? part_o.data_ptr<float>() : nullptr,
@@ -147,7 +147,7 @@ void check_logits(const Tensor& logits) {
 void argmax(Tensor out, Tensor logits) {
   check_logits(logits);
   TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == logits.size(0), "out int64 [n]");
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   mlop::launch_argmax(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)logits.size(0),
                       (int)logits.size(1), logits.stride(0), cur_stream());
 }
@@ -161,7 +161,7 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
   TORCH_CHECK(uniform.scalar_type() == at::kFloat && uniform.numel() == n && uniform.is_cuda(), "u");
   check_i32(top_ks, "top_ks");
   TORCH_CHECK(top_ks.numel() == n, "top_ks");
-  c10::hip::HIPGuard g(logits.device());
+  c10::DeviceGuard g(logits.device());
   mlop::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)n,
                       (int)logits.size(1), logits.stride(0), temps.data_ptr<float>(),
                       top_ks.data_ptr<int>(), top_ps.data_ptr<float>(), uniform.data_ptr<float>(),

@@ -141,9 +141,9 @@ def test_paged_attention(gpu, Hq, Hkv, case):
 def test_attention_spike_rescale(gpu):
     """Force the online-softmax rescale branch: a late key dominates."""
     Hq, Hkv = 32, 8
-    kc = 0.1 * torch.randn(64, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(64, Hkv, 128, 16, device=gpu, dtype=bf)
-    m, T = make_meta(gpu, [1, 4], [600, 700], Hkv, 4, 64, shuffle_rows=False)
+    kc = 0.1 * torch.randn(100, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(100, Hkv, 128, 16, device=gpu, dtype=bf)
+    m, T = make_meta(gpu, [1, 4], [600, 700], Hkv, 4, 100, shuffle_rows=False)
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
     bt = m.block_tables.cpu()
     page = int(bt[0, 30])
