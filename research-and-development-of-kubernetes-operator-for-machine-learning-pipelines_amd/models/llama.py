@@ -59,13 +59,15 @@ class LlamaModel:
 
     # ---------------------------------------------------------------- MLP --
     def _init_mlp(self, w):
+        # gate_up rows interleaved in groups of 16 (gate, up, gate, up, ...): the
+        # GEMM's SiLU-mul epilogue then sees matching columns in one tile
         H = self.cfg.hidden_size
         return {"gate_up": w(2 * self.inter, H), "down": w(H, self.inter)}
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         L = self.layers[i]
-        gu = linear(x, L["gate_up"])
-        return linear(ops.silu_mul(gu), L["down"])
+        act = ops.gemm(x, L["gate_up"], epi=ops.EPI_SILU_MUL)  # K1/K2 + fused K8
+        return linear(act, L["down"])
 
     # ------------------------------------------------------------ forward --
     def weight_tensors(self):

@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..ops import deinterleave_rows
 from ..ops import reference as ref
 
 
@@ -23,11 +24,11 @@ def _mlp(model, i, x):
             rows, k = (idx == e).nonzero(as_tuple=True)
             if rows.numel() == 0:
                 continue
-            gu = F.linear(x[rows], L["w13"][e].float())
+            gu = F.linear(x[rows], deinterleave_rows(L["w13"][e]).float())
             h = F.linear(ref.silu_mul(gu.to(model.dtype)).float(), L["w2"][e].float())
             out.index_add_(0, rows, h * w[rows, k, None])
         return out
-    gu = F.linear(x, L["gate_up"].float()).to(model.dtype)
+    gu = F.linear(x, deinterleave_rows(L["gate_up"]).float()).to(model.dtype)
     return F.linear(ref.silu_mul(gu).float(), L["down"].float())
 
 

@@ -124,6 +124,67 @@ def paged_attention(q, k_cache, v_cache, meta, out: torch.Tensor | None = None):
     return out
 
 
+EPI_NONE, EPI_SILU_MUL = 0, 1
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, epi: int = EPI_NONE):
+    """y = epi(x @ w^T), w [N, K] bf16.  EPI_SILU_MUL expects gate/up rows
+    interleaved in groups of 16 (``interleave_gate_up``) and returns N/2 columns."""
+    N = w.shape[0]
+    out_n = N if epi == EPI_NONE else N // 2
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x, w) if x.dtype != torch.bfloat16 else \
+            torch.nn.functional.linear(x.float(), w.float()).to(x.dtype)
+        if epi == EPI_SILU_MUL:
+            y = ref.silu_mul(deinterleave_cols(y))
+        if out is not None:
+            out.copy_(y.view_as(out))
+            return out
+        return y
+    _need_gpu()
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1 or x2.stride(0) % 8:
+        x2 = x2.contiguous()
+    M, K = x2.shape
+    o2 = torch.empty(M, out_n, dtype=x.dtype, device=x.device) if out is None else out.view(M, out_n)
+    nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws else _EMPTY.get(x.device)
+    torch.ops.mlop.gemm(o2, x2, w, ws, epi)
+    return o2.view(*lead, out_n) if out is None else out
+
+
+class _EmptyCache(dict):
+    def get(self, dev):  # noqa: D401
+        if dev not in self:
+            self[dev] = torch.empty(0, dtype=torch.float32, device=dev)
+        return self[dev]
+
+
+_EMPTY = _EmptyCache()
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """[I, K] gate and up -> [2I, K] rows [g0..g15, u0..u15, g16.., u16.., ...] (EPI_SILU_MUL layout)."""
+    I, K = gate.shape
+    assert I % group == 0
+    return torch.stack([gate.view(I // group, group, K), up.view(I // group, group, K)], 1).reshape(2 * I, K)
+
+
+def deinterleave_rows(w: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """Inverse of interleave_gate_up: [2I, K] interleaved -> [2I, K] = [gate; up]."""
+    n2, K = w.shape
+    v = w.view(n2 // (2 * group), 2, group, K)
+    return torch.cat([v[:, 0].reshape(-1, K), v[:, 1].reshape(-1, K)], 0)
+
+
+def deinterleave_cols(y: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """Columns of x @ W_interleaved^T -> [gate | up] column order."""
+    *lead, n2 = y.shape
+    v = y.reshape(-1, n2 // (2 * group), 2, group)
+    return torch.cat([v[:, :, 0].reshape(-1, n2 // 2), v[:, :, 1].reshape(-1, n2 // 2)], -1).view(*lead, n2)
+
+
 def argmax(logits: torch.Tensor) -> torch.Tensor:
     if not logits.is_cuda:
         return logits.argmax(-1)
@@ -149,16 +210,15 @@ __all__ = ["argmax", "sample", "load","available", "library_path", "rmsnorm", "a
 
 
 # ------------------------------------------------------------------ MoE --
-
-def _has(name: str) -> bool:
-    _need_gpu()
-    return hasattr(torch.ops.mlop, name)
-
+# Static-shape MoE primitives (graph-capturable): the permuted batch keeps
+# T*k rows; offsets[n_local] is the number of valid rows.
 
 def moe_route(logits: torch.Tensor, top_k: int):
-    if not logits.is_cuda or not _has("moe_route"):
+    """softmax -> top-k -> renormalise; logits bf16 [T, E] -> (w f32 [T,k], idx int32 [T,k])."""
+    if not logits.is_cuda:
         return ref.moe_route(logits, top_k)
-    T, E = logits.shape
+    _need_gpu()
+    T = logits.shape[0]
     w = torch.empty(T, top_k, dtype=torch.float32, device=logits.device)
     idx = torch.empty(T, top_k, dtype=torch.int32, device=logits.device)
     torch.ops.mlop.moe_route(w, idx, logits.contiguous())
@@ -166,27 +226,42 @@ def moe_route(logits: torch.Tensor, top_k: int):
 
 
 def moe_permute(x, topi, e0: int, n_local: int):
-    if not x.is_cuda or not _has("moe_permute"):
+    """Group routed slots by local expert.  Returns (xp [T*k, H], offsets [n_local+1],
+    src [T*k] row->slot, inv [T*k] slot->row or -1)."""
+    if not x.is_cuda:
         return ref.moe_permute(x, topi, e0, n_local)
+    _need_gpu()
     T, k = topi.shape
-    xp = torch.empty(T * k, x.shape[1], dtype=x.dtype, device=x.device)
-    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=x.device)
-    src = torch.empty(T * k, dtype=torch.int32, device=x.device)
-    n = torch.ops.mlop.moe_permute(xp, offsets, src, x, topi, e0, n_local)
-    return xp[:n], offsets, src[:n]
+    dev = x.device
+    xp = torch.empty(T * k, x.shape[1], dtype=x.dtype, device=dev)
+    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
+    src = torch.empty(T * k, dtype=torch.int32, device=dev)
+    inv = torch.empty(T * k, dtype=torch.int32, device=dev)
+    torch.ops.mlop.moe_permute(xp, offsets, src, inv, x.contiguous(), topi.contiguous(), e0, n_local)
+    return xp, offsets, src, inv
 
 
-def grouped_gemm(xp, w, offsets):
-    if not xp.is_cuda or not _has("grouped_gemm"):
-        return ref.grouped_gemm(xp, w, offsets)
-    out = torch.empty(xp.shape[0], w.shape[1], dtype=xp.dtype, device=xp.device)
-    torch.ops.mlop.grouped_gemm(out, xp, w, offsets)
+def moe_combine(y, inv, topw):
+    """out[t] = sum_j topw[t,j] * y[inv[t*k+j]] (inv < 0 skipped), fp32 accumulate."""
+    if not y.is_cuda:
+        return ref.moe_combine(y, inv, topw)
+    _need_gpu()
+    out = torch.empty(topw.shape[0], y.shape[1], dtype=y.dtype, device=y.device)
+    torch.ops.mlop.moe_combine(out, y, inv, topw.contiguous())
     return out
 
 
-def moe_combine(y, src, topw, T: int):
-    if not y.is_cuda or not _has("moe_combine"):
-        return ref.moe_combine(y, src, topw, T)
-    out = torch.empty(T, y.shape[1], dtype=y.dtype, device=y.device)
-    torch.ops.mlop.moe_combine(out, y, src, topw)
+def grouped_gemm(xp, w, offsets, epi: int = EPI_NONE, avg_rows: int | None = None):
+    """Per group e: rows offsets[e]:offsets[e+1] of xp times w[e]^T in ONE launch
+    (tiles enumerate (group, m-tile) pairs on device: no host sync, graph-safe)."""
+    if not xp.is_cuda:
+        y = ref.grouped_gemm(xp, w, offsets)
+        return ref.silu_mul(deinterleave_cols(y)) if epi == EPI_SILU_MUL else y
+    _need_gpu()
+    N = w.shape[1]
+    out = torch.empty(xp.shape[0], N if epi == EPI_NONE else N // 2, dtype=xp.dtype, device=xp.device)
+    if xp.shape[0] == 0:
+        return out
+    rows = avg_rows if avg_rows is not None else max(1, xp.shape[0] // max(1, w.shape[0]))
+    torch.ops.mlop.grouped_gemm(out, xp, w, offsets, rows, epi)
     return out

@@ -137,6 +137,90 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor
       (int)part_tokens, (int)nparts, (int)k_cache.size(0), cur_stream());
 }
 
+int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, (int)epi);
+}
+
+// out[M, N or N/2] = epi(a[M, K] . w[N, K]^T)
+void gemm(Tensor out, Tensor a, Tensor w, Tensor ws, int64_t epi) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1,
+              "a must be bf16 [M, K] with unit inner stride");
+  check_bf16(w, "w");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.dim() == 2 &&
+                  out.stride(1) == 1, "out must be bf16 [M, N]");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "w must be [N, K]");
+  TORCH_CHECK(K % 64 == 0, "K must be a multiple of 64");
+  TORCH_CHECK(N % 8 == 0 && a.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "16-B aligned rows");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi");
+  TORCH_CHECK(epi == 0 || N % 32 == 0, "silu_mul epilogue needs N % 32 == 0");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 0 ? N : N / 2), "out shape");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "16-B aligned data");
+  float* wsp = nullptr;
+  int64_t wsn = 0;
+  if (ws.defined() && ws.numel() > 0) {
+    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat, "ws f32");
+    wsp = ws.data_ptr<float>();
+    wsn = ws.numel();
+  }
+  c10::DeviceGuard g(a.device());
+  mlop::launch_gemm(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, out.data_ptr(),
+                    (int)out.stride(0), wsp, wsn, (int)M, (int)N, (int)K, (int)epi, cur_stream());
+}
+
+// grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
+void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi) {
+  check_bf16(out, "out"); check_bf16(a, "a"); check_bf16(w, "w"); check_i32(offsets, "offsets");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 3 && w.size(2) == a.size(1), "a [M, K], w [G, N, K]");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(1), G = w.size(0);
+  TORCH_CHECK(offsets.numel() == G + 1, "offsets must be [G + 1]");
+  TORCH_CHECK(K % 64 == 0 && N % 32 == 0, "K % 64, N % 32");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 0 ? N : N / 2), "out shape");
+  c10::DeviceGuard g(a.device());
+  mlop::launch_grouped_gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), offsets.data_ptr<int>(),
+                            (int)G, (int)M, (int)N, (int)K, (int)max_rows, (int)epi, cur_stream());
+}
+
+void moe_route(Tensor topw, Tensor topi, Tensor logits) {
+  check_bf16(logits, "router logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 64, "router logits [T, E<=64]");
+  const int64_t T = logits.size(0), E = logits.size(1), k = topi.size(1);
+  TORCH_CHECK(k >= 1 && k <= E && k <= 8, "1 <= top_k <= min(E, 8)");
+  check_i32(topi, "topi");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.numel() == T * k &&
+                  topi.numel() == T * k, "topw/topi [T, k]");
+  c10::DeviceGuard g(logits.device());
+  mlop::launch_moe_route(topw.data_ptr<float>(), topi.data_ptr<int>(), logits.data_ptr(), (int)T,
+                         (int)E, (int)k, cur_stream());
+}
+
+void moe_permute(Tensor xp, Tensor offsets, Tensor src, Tensor inv, Tensor x, Tensor topi,
+                 int64_t e0, int64_t n_local) {
+  check_bf16(xp, "xp"); check_bf16(x, "x"); check_i32(offsets, "offsets"); check_i32(src, "src");
+  check_i32(inv, "inv"); check_i32(topi, "topi");
+  const int64_t T = topi.size(0), k = topi.size(1), H = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.size(0) == T && H % 8 == 0, "x [T, H]");
+  TORCH_CHECK(xp.size(0) == T * k && xp.size(1) == H, "xp [T*k, H]");
+  TORCH_CHECK(n_local >= 1 && n_local <= 256 && offsets.numel() == n_local + 1, "offsets");
+  TORCH_CHECK(src.numel() == T * k && inv.numel() == T * k, "src/inv [T*k]");
+  c10::DeviceGuard g(x.device());
+  mlop::launch_moe_permute(xp.data_ptr(), offsets.data_ptr<int>(), src.data_ptr<int>(),
+                           inv.data_ptr<int>(), x.data_ptr(), topi.data_ptr<int>(), (int)T, (int)k,
+                           (int)H, (int)e0, (int)n_local, cur_stream());
+}
+
+void moe_combine(Tensor out, Tensor y, Tensor inv, Tensor topw) {
+  check_bf16(out, "out"); check_bf16(y, "y"); check_i32(inv, "inv");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.dim() == 2, "topw");
+  const int64_t T = topw.size(0), k = topw.size(1), H = y.size(1);
+  TORCH_CHECK(out.size(0) == T && out.size(1) == H && inv.numel() == T * k && H % 8 == 0,
+              "combine shapes");
+  c10::DeviceGuard g(y.device());
+  mlop::launch_moe_combine(out.data_ptr(), y.data_ptr(), inv.data_ptr<int>(),
+                           topw.data_ptr<float>(), (int)T, (int)k, (int)H, cur_stream());
+}
+
 void check_logits(const Tensor& logits) {
   TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 &&
                   logits.stride(1) == 1 && logits.stride(0) % 4 == 0,
@@ -171,6 +255,14 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
 }  // namespace
 
 TORCH_LIBRARY(mlop, m) {
+  m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
+  m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
+  m.def("grouped_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int max_rows, "
+        "int epi) -> ()");
+  m.def("moe_route(Tensor(a!) topw, Tensor(b!) topi, Tensor logits) -> ()");
+  m.def("moe_permute(Tensor(a!) xp, Tensor(b!) offsets, Tensor(c!) src, Tensor(d!) inv, Tensor x, "
+        "Tensor topi, int e0, int n_local) -> ()");
+  m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor inv, Tensor topw) -> ()");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, "
         "Tensor uniform) -> ()");
@@ -193,6 +285,11 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("embedding", &embedding);
   m.impl("paged_attention", &paged_attention);
+  m.impl("gemm", &gemm);
+  m.impl("grouped_gemm", &grouped_gemm);
+  m.impl("moe_route", &moe_route);
+  m.impl("moe_permute", &moe_permute);
+  m.impl("moe_combine", &moe_combine);
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
 }

@@ -23,6 +23,17 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
                             const int* q_len, const int* ctx_len, int num_tiles, int Hq, int Hkv,
                             float scale_log2, int part_tokens, int nparts, int num_blocks,
                             hipStream_t st);
+long gemm_workspace_floats(int M, int N, int K, int epi);
+void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws,
+                 long ws_floats, int M, int N, int K, int epi, hipStream_t st);
+void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
+                         int M, int N, int K, int max_rows, int epi, hipStream_t st);
+void launch_moe_route(float* topw, int* topi, const void* logits, int T, int E, int k,
+                      hipStream_t st);
+void launch_moe_permute(void* xp, int* offsets, int* src, int* inv, const void* x, const int* topi,
+                        int T, int k, int H, int e0, int n_local, hipStream_t st);
+void launch_moe_combine(void* out, const void* y, const int* inv, const float* topw, int T, int k,
+                        int H, hipStream_t st);
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
                    const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);

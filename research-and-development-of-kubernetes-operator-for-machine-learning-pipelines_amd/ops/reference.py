@@ -114,24 +114,31 @@ def moe_route(logits, top_k):
 
 
 def moe_permute(x, topi, e0, n_local):
-    """Rows routed to local experts, grouped by expert (stable in slot order).
-    Returns (x_perm [N, H], offsets int32 [n_local + 1], src int32 [N] = token*k + slot)."""
-    k = topi.shape[1]
+    """Rows routed to local experts, grouped by expert (stable in slot order), padded to T*k rows.
+    Returns (xp [T*k, H], offsets int32 [n_local+1], src int32 [T*k], inv int32 [T*k])."""
+    T, k = topi.shape
     flat = topi.reshape(-1).long() - e0
     ok = (flat >= 0) & (flat < n_local)
     slots = torch.nonzero(ok, as_tuple=True)[0]
     e = flat[slots]
     order = torch.argsort(e, stable=True)
     slots, e = slots[order], e[order]
+    n = slots.numel()
     counts = torch.bincount(e, minlength=n_local)
     offsets = torch.zeros(n_local + 1, dtype=torch.int32, device=x.device)
     offsets[1:] = torch.cumsum(counts, 0).to(torch.int32)
-    return x[slots // k], offsets, slots.to(torch.int32)
+    xp = torch.zeros(T * k, x.shape[1], dtype=x.dtype, device=x.device)
+    xp[:n] = x[slots // k]
+    src = torch.full((T * k,), -1, dtype=torch.int32, device=x.device)
+    src[:n] = slots.to(torch.int32)
+    inv = torch.full((T * k,), -1, dtype=torch.int32, device=x.device)
+    inv[slots] = torch.arange(n, dtype=torch.int32, device=x.device)
+    return xp, offsets, src, inv
 
 
 def grouped_gemm(xp, w, offsets):
-    """Per expert e: rows [off[e], off[e+1]) of xp times w[e]^T (w: [E, N, K])."""
-    out = torch.empty(xp.shape[0], w.shape[1], dtype=xp.dtype, device=xp.device)
+    """Per group e: rows [off[e], off[e+1]) of xp times w[e]^T (w: [E, N, K]); other rows 0."""
+    out = torch.zeros(xp.shape[0], w.shape[1], dtype=xp.dtype, device=xp.device)
     off = offsets.tolist()
     for e in range(w.shape[0]):
         a, b = off[e], off[e + 1]
@@ -140,11 +147,12 @@ def grouped_gemm(xp, w, offsets):
     return out
 
 
-def moe_combine(y, src, topw, T):
-    """out[t] = sum over routed rows r with src[r] // k == t of topw[t, src%k] * y[r]."""
-    k = topw.shape[1]
+def moe_combine(y, inv, topw):
+    T, k = topw.shape
     out = torch.zeros(T, y.shape[1], dtype=torch.float32, device=y.device)
-    s = src.long()
-    wts = topw.reshape(-1)[s].float()
-    out.index_add_(0, s // k, y.float() * wts[:, None])
+    inv = inv.long().view(T, k)
+    for j in range(k):
+        ok = inv[:, j] >= 0
+        if ok.any():
+            out[ok] += topw[ok, j, None].float() * y[inv[ok, j]].float()
     return out.to(y.dtype)

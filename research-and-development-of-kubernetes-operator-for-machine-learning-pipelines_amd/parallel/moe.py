@@ -28,13 +28,16 @@ def route(x: torch.Tensor, router_w: torch.Tensor, top_k: int):
 
 
 def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int):
-    """Sum over the top-k slots whose expert is in [e0, e0+n_local) of w * expert(x)."""
-    T = x.shape[0]
-    xp, offsets, src = ops.moe_permute(x, topi, e0, n_local)
-    h = ops.grouped_gemm(xp, w13, offsets)
-    a = ops.silu_mul(h)
-    y = ops.grouped_gemm(a, w2, offsets)
-    return ops.moe_combine(y, src, topw, T)
+    """Sum over the top-k slots whose expert is in [e0, e0+n_local) of w * expert(x).
+
+    permute (K12) -> grouped gate_up GEMM with fused SiLU-mul (K13, w13 rows
+    gate/up-interleaved) -> grouped down GEMM (K13) -> weighted gather (K14)."""
+    T, k = topi.shape
+    xp, offsets, src, inv = ops.moe_permute(x, topi, e0, n_local)
+    avg = max(1, (T * k) // max(1, n_local))
+    a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg)
+    y = ops.grouped_gemm(a, w2, offsets, avg_rows=avg)
+    return ops.moe_combine(y, inv, topw)
 
 
 def moe_forward(x, router_w, w13, w2, top_k: int, ep, e0: int, n_local: int, mode: str = "allreduce"):
