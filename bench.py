@@ -153,6 +153,13 @@ def main(argv=None):
             "step_mix": stats,
             "deploy": deploy_info,
         }
+        try:
+            from mlopamd import ops
+
+            ch = ops.gemm_choices()
+            res["gemm_backend"] = {b: sum(1 for c in ch if c["choice"] == b) for b in ("mlop", "hipblaslt")}
+        except Exception:  # noqa: BLE001
+            pass
         print(json.dumps(res), flush=True)
     engine.shutdown() if hasattr(engine, "shutdown") else None
     if world > 1:

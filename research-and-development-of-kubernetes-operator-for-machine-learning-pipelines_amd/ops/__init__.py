@@ -148,10 +148,73 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, epi:
         x2 = x2.contiguous()
     M, K = x2.shape
     o2 = torch.empty(M, out_n, dtype=x.dtype, device=x.device) if out is None else out.view(M, out_n)
-    nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
-    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device) if nws else _EMPTY.get(x.device)
-    torch.ops.mlop.gemm(o2, x2, w, ws, epi)
+    _GEMM_IMPL[_gemm_backend(M, N, K, epi, x2, w, o2)](x2, w, o2, epi)
     return o2.view(*lead, out_n) if out is None else out
+
+
+def _gemm_mlop(x2, w, o2, epi):
+    M, K = x2.shape
+    nws = torch.ops.mlop.gemm_workspace(M, w.shape[0], K, epi)
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x2.device) if nws else _EMPTY.get(x2.device)
+    torch.ops.mlop.gemm(o2, x2, w, ws, epi)
+
+
+def _gemm_hipblaslt(x2, w, o2, epi):
+    """Plain library GEMM (hipBLASLt via torch.matmul); the SiLU-mul epilogue
+    then runs as the separate interleaved silu_mul kernel."""
+    if epi == EPI_NONE:
+        torch.matmul(x2, w.t(), out=o2)
+    else:
+        torch.ops.mlop.silu_mul(o2, torch.matmul(x2, w.t()), 1)
+
+
+_GEMM_IMPL = {"mlop": _gemm_mlop, "hipblaslt": _gemm_hipblaslt}
+_GEMM_CHOICE: dict = {}
+GEMM_BACKEND = os.environ.get("MLOP_GEMM_BACKEND", "auto")  # auto | mlop | hipblaslt
+
+
+def _mbucket(M: int) -> int:
+    b = 1
+    while b < M:
+        b <<= 1
+    return b
+
+
+def _gemm_backend(M, N, K, epi, x2, w, o2) -> str:
+    """Per-shape choice between the hand-written MFMA kernel and hipBLASLt,
+    measured once per (M bucket, N, K, epilogue) on first eager use (never
+    during graph capture).  ``gemm_choices()`` reports the table."""
+    if GEMM_BACKEND != "auto":
+        return GEMM_BACKEND
+    key = (_mbucket(M), N, K, epi)
+    c = _GEMM_CHOICE.get(key)
+    if c is not None:
+        return c
+    if torch.cuda.is_current_stream_capturing():
+        return "mlop"
+    times = {}
+    for name, fn in _GEMM_IMPL.items():
+        fn(x2, w, o2, epi)  # warm (kernel selection, lazy init)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(3):
+            fn(x2, w, o2, epi)
+        e.record()
+        e.synchronize()
+        times[name] = s.elapsed_time(e) / 3
+    c = min(times, key=times.get)
+    _GEMM_CHOICE[key] = c
+    _GEMM_TIMES[key] = times
+    return c
+
+
+_GEMM_TIMES: dict = {}
+
+
+def gemm_choices() -> list:
+    return [dict(M_bucket=k[0], N=k[1], K=k[2], epi=k[3], choice=_GEMM_CHOICE[k],
+                 **{f"{n}_us": round(t * 1e3, 1) for n, t in _GEMM_TIMES.get(k, {}).items()})
+            for k in sorted(_GEMM_CHOICE)]
 
 
 class _EmptyCache(dict):

@@ -73,14 +73,15 @@ void rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor qkv, Tensor
                           Hq, Hkv, D, (int)qkv.stride(0), BS, cur_stream());
 }
 
-void silu_mul(Tensor out, Tensor x) {
+void silu_mul(Tensor out, Tensor x, int64_t interleaved) {
   check_bf16(out, "out"); check_bf16(x, "x");
   const int64_t I2 = x.size(-1);
-  TORCH_CHECK(I2 % 16 == 0, "gate_up width must be a multiple of 16");
+  TORCH_CHECK(I2 % (interleaved ? 32 : 16) == 0, "gate_up width must be a multiple of 16/32");
   const int64_t M = x.numel() / I2;
   TORCH_CHECK(out.numel() == M * (I2 / 2), "silu_mul shape mismatch");
   c10::DeviceGuard g(x.device());
-  mlop::launch_silu_mul(out.data_ptr(), x.data_ptr(), (int)M, (int)(I2 / 2), cur_stream());
+  mlop::launch_silu_mul(out.data_ptr(), x.data_ptr(), (int)M, (int)(I2 / 2), (int)interleaved,
+                        cur_stream());
 }
 
 void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_start) {
@@ -270,7 +271,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> ()");
-  m.def("silu_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def("silu_mul(Tensor(a!) out, Tensor x, int interleaved=0) -> ()");
   m.def("embedding(Tensor(a!) out, Tensor table, Tensor ids, int vocab_start) -> ()");
   m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor q, "
         "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0, "

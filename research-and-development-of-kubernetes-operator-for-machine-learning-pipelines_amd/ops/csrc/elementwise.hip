@@ -5,9 +5,11 @@
 
 namespace mlop {
 
-// out[m, i] = silu(x[m, i]) * x[m, I + i]   (x = fused gate_up projection output)
+// out[m, i] = silu(gate_i) * up_i of the fused gate_up projection output x[m, 2I]:
+//   interleaved = 0: x = [gate | up];  interleaved = 1: groups of 16 (g0..15, u0..15, ...)
 __global__ void __launch_bounds__(256) silu_mul_kernel(uint16_t* __restrict__ out,
-                                                      const uint16_t* __restrict__ x, int M, int I) {
+                                                      const uint16_t* __restrict__ x, int M, int I,
+                                                      int interleaved) {
   const int vpr = I >> 3;
   const long total = (long)M * vpr;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -15,8 +17,10 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(uint16_t* __restrict__ ou
     const long m = idx / vpr;
     const int c = (int)(idx % vpr) * 8;
     const uint16_t* row = x + m * 2 * (long)I;
-    u32x4 g = *reinterpret_cast<const u32x4*>(row + c);
-    u32x4 u = *reinterpret_cast<const u32x4*>(row + I + c);
+    const int gc = interleaved ? (c / 16) * 32 + (c % 16) : c;
+    const int uc = interleaved ? gc + 16 : I + c;
+    u32x4 g = *reinterpret_cast<const u32x4*>(row + gc);
+    u32x4 u = *reinterpret_cast<const u32x4*>(row + uc);
     u32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -30,11 +34,11 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(uint16_t* __restrict__ ou
   }
 }
 
-void launch_silu_mul(void* out, const void* x, int M, int I, hipStream_t st) {
+void launch_silu_mul(void* out, const void* x, int M, int I, int interleaved, hipStream_t st) {
   if (M == 0) return;
   const long total = (long)M * (I / 8);
   int grid = (int)std::min<long>((total + 255) / 256, 2048);
-  silu_mul_kernel<<<grid, 256, 0, st>>>((uint16_t*)out, (const uint16_t*)x, M, I);
+  silu_mul_kernel<<<grid, 256, 0, st>>>((uint16_t*)out, (const uint16_t*)x, M, I, interleaved);
 }
 
 // out[t, :] = table[ids[t] - vocab_start, :] if the id is in this rank's vocab shard, else 0

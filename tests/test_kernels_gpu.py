@@ -211,7 +211,9 @@ def test_moe_pipeline(gpu, T, E, k, H, I):
     logits = torch.randn(T, E, device=gpu, dtype=bf)
     w, idx = ops.moe_route(logits, k)
     w_ref, idx_ref = ref.moe_route(logits, k)
-    assert torch.equal(idx.cpu(), idx_ref.cpu())
+    # bf16 router logits tie often: compare the chosen probabilities, not tie-broken ids
+    p = torch.softmax(logits.float(), -1)
+    torch.testing.assert_close(p.gather(1, idx.long()).cpu(), p.gather(1, idx_ref.long()).cpu())
     close(w, w_ref, atol=1e-5, rtol=1e-4)
     w13 = (0.05 * torch.randn(E, 2 * I, H, device=gpu)).to(bf)
     w2 = (0.05 * torch.randn(E, H, I, device=gpu)).to(bf)
