@@ -52,6 +52,7 @@ class CanaryPolicy:
     # absolute error-rate floor: with a 0 baseline the reference's relative test
     # demands exactly 0 errors; 0.0 reproduces the reference
     error_rate_floor: float = 0.0
+    latency_floor_s: float = 0.0    # latencies below this always pass (0 = reference)
     window_s: int = 60              # PromQL range (mlflow_operator.py:363)
     ready_timeout_s: float = 1800.0  # wait for the new predictor's readiness before gating
 
@@ -69,6 +70,7 @@ class CanaryPolicy:
                    rollback=bool(c.get("rollback", base.rollback)),
                    thresholds=th,
                    error_rate_floor=float(c.get("errorRateFloor", base.error_rate_floor)),
+                   latency_floor_s=float(c.get("latencyFloorSeconds", base.latency_floor_s)),
                    window_s=int(c.get("windowSeconds", base.window_s)),
                    ready_timeout_s=float(c.get("readyTimeoutSeconds", base.ready_timeout_s)))
 

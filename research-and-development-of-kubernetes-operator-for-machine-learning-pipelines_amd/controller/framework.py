@@ -46,6 +46,7 @@ class _Resource:
     on_delete: list = field(default_factory=list)
     on_resume: list = field(default_factory=list)
     daemons: list = field(default_factory=list)
+    on_event: list = field(default_factory=list)
 
 
 def cr_logger(name: str, namespace: str) -> logging.Logger:
@@ -94,6 +95,14 @@ class Operator:
     def on_resume(self, group, version, plural):
         def deco(fn):
             self._r(group, version, plural).on_resume.append(fn)
+            return fn
+        return deco
+
+    def event_handler(self, group, version, plural):
+        """``async def fn(event_type, body, **kw)`` for EVERY watch event (incl. status-only
+        changes, which do not bump ``generation``) — e.g. to react to owned objects."""
+        def deco(fn):
+            self._r(group, version, plural).on_event.append(fn)
             return fn
         return deco
 
@@ -198,6 +207,13 @@ class Operator:
         md = body["metadata"]
         key = (res.plural, md.get("namespace"), md.get("name"))
         gen = md.get("generation", 1)
+        for h in res.on_event:
+            try:
+                await h(event_type=etype, body=body, operator=self)
+            except Exception as e:  # noqa: BLE001 - observers never break dispatch
+                log.warning("event handler %s failed: %s", h.__name__, e)
+        if not (res.on_create or res.on_update or res.on_delete or res.on_resume or res.daemons):
+            return
         if etype == "DELETED":
             self._generation.pop(key, None)
             await self._stop_daemons(key)

@@ -1,0 +1,411 @@
+"""Local "cluster" emulator (no kind / kubectl / network in this environment).
+
+  FakeKube (apiserver)  <->  Operator (our reconciler)  ->  SeldonDeployment
+                                                              |
+  FakeSeldonController: watches SDs, starts one "pod" per predictor through a
+  Launcher, reports per-predictor availability in the SD status (what the real
+  Seldon controller does), and keeps the traffic split for the Router
+  (weighted routing = the Istio VirtualService stand-in).
+
+Launchers:
+  * ``InProcessLauncher`` — builds the predictor backend in this process (the
+    bench: the Llama-3-8B engine on this rank's GPU);
+  * ``ProcessLauncher``  — starts ``python -m mlopamd.runtime.server`` with the
+    container env from the SD, scraped by the fake Prometheus;
+  * ``SimLauncher``      — simulated predictors that write executor metrics into a
+    MetricStore with a per-version latency/error profile (virtual-clock canary tests).
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import os
+import socket
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+
+from . import seldon
+from .clock import RealClock
+from .crd import API_VERSION, GROUP, KIND, PLURAL, SELDON_GROUP, SELDON_PLURAL, SELDON_VERSION, VERSION
+from .kube import ApiError, FakeKube
+
+log = logging.getLogger("mlopamd.local")
+
+
+@dataclass
+class Pod:
+    sd: str
+    namespace: str
+    predictor: str
+    spec: dict
+    endpoint: str | None = None
+    backend: object = None
+    ready: bool = False
+    proc: subprocess.Popen | None = None
+    task: asyncio.Task | None = None
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def key(self):
+        return (self.namespace, self.sd, self.predictor)
+
+
+def _env_of(pred: dict) -> dict:
+    env = {}
+    for cs in pred.get("componentSpecs") or []:
+        for c in cs.get("spec", {}).get("containers", []):
+            for e in c.get("env", []):
+                env[e["name"]] = e.get("value", "")
+    g = pred.get("graph", {})
+    env.setdefault("MLOP_MODEL_URI", g.get("modelUri", ""))
+    env.setdefault("MLOP_RUNTIME", "mlop-sklearn" if g.get("implementation") == "MLFLOW_SERVER" else "mlop-llm")
+    env.setdefault("PREDICTOR_ID", pred.get("name", ""))
+    return env
+
+
+class InProcessLauncher:
+    """factory(pod, env) -> backend (blocking build runs in a worker thread)."""
+
+    def __init__(self, factory):
+        self.factory = factory
+
+    async def start(self, pod: Pod):
+        env = _env_of(pod.spec)
+        pod.backend = await asyncio.get_running_loop().run_in_executor(None, self.factory, pod, env)
+        pod.ready = True
+
+    async def stop(self, pod: Pod):
+        b = pod.backend
+        if b is not None and hasattr(b, "stop"):
+            b.stop()
+        pod.ready = False
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class ProcessLauncher:
+    """One OS process per predictor replica running the V2 runtime server."""
+
+    def __init__(self, scraper=None, extra_env: dict | None = None, python: str = sys.executable,
+                 ready_timeout_s: float = 600.0):
+        self.scraper, self.extra_env, self.python = scraper, extra_env or {}, python
+        self.ready_timeout_s = ready_timeout_s
+
+    async def start(self, pod: Pod):
+        import aiohttp
+
+        port = free_port()
+        env = dict(os.environ)
+        env.update(_env_of(pod.spec))
+        env.update(self.extra_env)
+        env["SELDON_DEPLOYMENT_ID"] = pod.sd
+        env["SELDON_NAMESPACE"] = pod.namespace
+        repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+        pod.proc = subprocess.Popen([self.python, "-m", "mlopamd.runtime.server", "--port", str(port),
+                                     "--host", "127.0.0.1"], env=env, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.DEVNULL, start_new_session=True)
+        pod.endpoint = f"http://127.0.0.1:{port}"
+        t0 = time.monotonic()
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as s:
+            while time.monotonic() - t0 < self.ready_timeout_s:
+                if pod.proc.poll() is not None:
+                    raise RuntimeError(f"predictor {pod.predictor} exited with {pod.proc.returncode}")
+                try:
+                    async with s.get(pod.endpoint + "/v2/health/ready") as r:
+                        if r.status == 200:
+                            pod.ready = True
+                            break
+                except (aiohttp.ClientError, asyncio.TimeoutError, OSError):
+                    pass
+                await asyncio.sleep(0.1)
+        if self.scraper is not None:
+            self.scraper.add_target(pod.endpoint + "/metrics")
+
+    async def stop(self, pod: Pod):
+        if self.scraper is not None and pod.endpoint:
+            self.scraper.remove_target(pod.endpoint + "/metrics")
+        if pod.proc is not None and pod.proc.poll() is None:
+            pod.proc.terminate()
+            try:
+                pod.proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                pod.proc.kill()
+        pod.ready = False
+
+
+class SimLauncher:
+    """Simulated predictors: every ``period`` (virtual) seconds each ready pod
+    records ``rps * period * traffic%`` requests into the MetricStore as the
+    Seldon executor would (cumulative histogram buckets, counts per code).
+    ``profiles[version] = {"latency": s, "error_rate": f, "startup_s": s}``."""
+
+    BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0)
+
+    def __init__(self, store, clock, profiles: dict | None = None, rps: float = 50.0, period: float = 5.0):
+        self.store, self.clock, self.profiles, self.rps, self.period = store, clock, profiles or {}, rps, period
+        self.traffic: dict = {}
+
+    async def start(self, pod: Pod):
+        ver = pod.predictor[1:]
+        prof = self.profiles.get(ver, {})
+        startup = prof.get("startup_s", 0.0)
+        if startup:
+            await self.clock.sleep(startup)
+        pod.ready = True
+        pod.task = asyncio.get_running_loop().create_task(self._emit(pod, prof))
+
+    async def _emit(self, pod: Pod, prof: dict):
+        lbl = {"deployment_name": pod.sd, "predictor_name": pod.predictor, "namespace": pod.namespace}
+        counts = {b: 0.0 for b in self.BUCKETS}
+        inf = lsum = ok = err = 0.0
+        lat = float(prof.get("latency", 0.05))
+        er = float(prof.get("error_rate", 0.0))
+        while True:
+            share = self.traffic.get(pod.key, 0) / 100.0
+            n = self.rps * self.period * share
+            if n > 0:
+                for b in self.BUCKETS:
+                    if lat <= b:
+                        counts[b] += n
+                inf += n
+                lsum += n * lat
+                err += n * er
+                ok += n * (1 - er)
+            t = self.clock.now()
+            for b in self.BUCKETS:
+                self.store.add("seldon_api_executor_client_requests_seconds_bucket", dict(lbl, le=str(b)), counts[b], t)
+            self.store.add("seldon_api_executor_client_requests_seconds_bucket", dict(lbl, le="+Inf"), inf, t)
+            self.store.add("seldon_api_executor_client_requests_seconds_sum", lbl, lsum, t)
+            self.store.add("seldon_api_executor_client_requests_seconds_count", lbl, inf, t)
+            self.store.add("seldon_api_executor_server_requests_seconds_count", dict(lbl, code="200", service="predictions"), ok, t)
+            self.store.add("seldon_api_executor_server_requests_seconds_count", dict(lbl, code="500", service="predictions"), err, t)
+            await self.clock.sleep(self.period)
+
+    async def stop(self, pod: Pod):
+        if pod.task:
+            pod.task.cancel()
+        pod.ready = False
+
+
+class FakeSeldonController:
+    """Turns SeldonDeployments into pods and reports their availability."""
+
+    def __init__(self, kube, launcher, clock=None):
+        self.kube, self.launcher, self.clock = kube, launcher, clock or RealClock()
+        self.pods: dict[tuple, Pod] = {}
+        self.traffic: dict[tuple, int] = {}
+        self._task = None
+        self._starting: dict[tuple, asyncio.Task] = {}
+        self._seen_gen: dict[tuple, int | None] = {}
+
+    def start(self):
+        self._task = asyncio.get_running_loop().create_task(self._run())
+        return self
+
+    async def stop(self):
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+        for t in self._starting.values():
+            t.cancel()
+        for pod in list(self.pods.values()):
+            await self.launcher.stop(pod)
+        self.pods.clear()
+
+    async def _run(self):
+        async for etype, sd in self.kube.watch(SELDON_GROUP, SELDON_VERSION, SELDON_PLURAL):
+            try:
+                await self._reconcile(etype, sd)
+            except Exception as e:  # noqa: BLE001
+                log.exception("seldon controller: %s", e)
+
+    async def _reconcile(self, etype, sd):
+        ns, name = sd["metadata"]["namespace"], sd["metadata"]["name"]
+        gen = sd["metadata"].get("generation")
+        if etype == "MODIFIED" and self._seen_gen.get((ns, name)) == gen:
+            return  # status-only update (our own report): nothing to do
+        self._seen_gen[(ns, name)] = None if etype == "DELETED" else gen
+        preds = {} if etype == "DELETED" else {p["name"]: p for p in sd["spec"].get("predictors", [])}
+        for key in [k for k in self.pods if k[0] == ns and k[1] == name and k[2] not in preds]:
+            pod = self.pods.pop(key)
+            self.traffic.pop(key, None)
+            await self.launcher.stop(pod)
+        for pname, p in preds.items():
+            key = (ns, name, pname)
+            self.traffic[key] = int(p.get("traffic", 0))
+            if key not in self.pods:
+                pod = Pod(name, ns, pname, p)
+                self.pods[key] = pod
+                self._starting[key] = asyncio.get_running_loop().create_task(self._bring_up(pod))
+        if hasattr(self.launcher, "traffic"):
+            self.launcher.traffic = self.traffic
+        if etype != "DELETED":
+            await self._report(ns, name)
+
+    async def _bring_up(self, pod: Pod):
+        try:
+            await self.launcher.start(pod)
+        except Exception as e:  # noqa: BLE001
+            log.error("predictor %s failed to start: %s", pod.predictor, e)
+            pod.extra["error"] = str(e)
+        finally:
+            self._starting.pop(pod.key, None)
+        await self._report(pod.namespace, pod.sd)
+
+    async def _report(self, ns, name):
+        mine = {k: p for k, p in self.pods.items() if k[0] == ns and k[1] == name}
+        ds = {}
+        for (_, _, pname), pod in mine.items():
+            g = seldon.graph_name(pname[1:])
+            ds[f"{name}-{pname}-0-{g}"] = {"replicas": int(pod.spec.get("replicas", 1)),
+                                           "availableReplicas": int(pod.spec.get("replicas", 1)) if pod.ready else 0}
+        failed = any("error" in p.extra for p in mine.values())
+        state = "Failed" if failed else ("Available" if mine and all(p.ready for p in mine.values()) else "Creating")
+        try:
+            await self.kube.patch_status(SELDON_GROUP, SELDON_VERSION, ns, SELDON_PLURAL, name,
+                                         {"status": {"state": state, "deploymentStatus": ds}})
+        except ApiError as e:
+            if e.status != 404:
+                raise
+
+    def backend(self, ns, sd, predictor):
+        pod = self.pods.get((ns, sd, predictor))
+        return pod.backend if pod else None
+
+
+class Router:
+    """Weighted request routing by the SD traffic split (smooth weighted round-robin)."""
+
+    def __init__(self, controller: FakeSeldonController):
+        self.ctl = controller
+        self._cw: dict = {}
+
+    def pick(self, ns: str, sd: str) -> Pod | None:
+        cands = [(k, w) for k, w in self.ctl.traffic.items() if k[0] == ns and k[1] == sd and w > 0
+                 and self.ctl.pods.get(k) is not None and self.ctl.pods[k].ready]
+        if not cands:
+            return None
+        total = sum(w for _, w in cands)
+        best = None
+        for k, w in cands:
+            self._cw[k] = self._cw.get(k, 0) + w
+            if best is None or self._cw[k] > self._cw[best]:
+                best = k
+        self._cw[best] -= total
+        return self.ctl.pods[best]
+
+    async def post(self, ns: str, sd: str, path: str, payload: dict, session=None) -> tuple[int, dict, str]:
+        import aiohttp
+
+        pod = self.pick(ns, sd)
+        if pod is None or pod.endpoint is None:
+            return 503, {}, ""
+        own = session is None
+        session = session or aiohttp.ClientSession()
+        try:
+            async with session.post(pod.endpoint + path, json=payload) as r:
+                return r.status, await r.json(content_type=None), pod.predictor
+        finally:
+            if own:
+                await session.close()
+
+
+def mlflow_model_cr(name: str, namespace: str, model_name: str, alias: str, interval: int = 60,
+                    secret: str | None = "minio-secret", **extra_spec) -> dict:
+    spec = {"modelName": model_name, "modelAlias": alias, "monitoringInterval": interval}
+    if secret:
+        spec["minioSecret"] = secret
+    spec.update(extra_spec)
+    return {"apiVersion": API_VERSION, "kind": KIND, "metadata": {"name": name, "namespace": namespace},
+            "spec": spec}
+
+
+async def wait_for(pred, timeout_s: float = 60.0, poll_s: float = 0.01):
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout_s:
+        v = await pred()
+        if v:
+            return v
+        await asyncio.sleep(poll_s)
+    raise TimeoutError("condition not met")
+
+
+# ---------------------------------------------------------------- bench --
+
+def deploy_and_wait(model: str = "llama3-8b", device="cuda", seed: int = 0, engine_kwargs: dict | None = None,
+                    namespace: str = "serving", timeout_s: float = 900.0):
+    """Run the full control-plane path in-process: MLflow registry (sqlite) holds
+    the model version with its architecture tag, an MlflowModel CR is created,
+    the operator reconciles it into a SeldonDeployment whose predictor is our
+    LLM runtime, the fake Seldon controller brings that predictor up on THIS
+    process's GPU, and the CR reports ready.  Returns (engine, info)."""
+    from ..runtime.deploy import build_engine
+    from .app import OperatorMetrics, make_operator
+    from .crd import OperatorSettings
+    from .mlflow import LocalMlflowClient, SqliteRegistry
+    from .prometheus import LocalProm, MetricStore
+
+    engine_kwargs = dict(engine_kwargs or {})
+
+    async def main():
+        kube = FakeKube()
+        reg = SqliteRegistry()
+        reg.create_model_version(model, f"mlflow-artifacts:/1/{model}/artifacts/model",
+                                 tags={"mlop.architecture": model, "mlop.runtime": seldon.RUNTIME_LLM})
+        reg.set_alias(model, "champion", 1)
+        clock = RealClock()
+        metrics = OperatorMetrics()
+        op, rec = make_operator(kube, LocalMlflowClient(reg), LocalProm(MetricStore()), clock,
+                                OperatorSettings(), metrics=metrics)
+        built = {}
+
+        def factory(pod, env):
+            import torch
+
+            if torch.device(device).type == "cuda":
+                torch.cuda.set_device(device)  # worker thread: HIP's current device is per-thread
+            eng = build_engine(env.get("MLOP_ARCHITECTURE", model), device=device, seed=seed, **engine_kwargs)
+            built["engine"] = eng
+            return eng
+
+        ctl = FakeSeldonController(kube, InProcessLauncher(factory), clock).start()
+        await op.start()
+        t0 = time.perf_counter()
+        cr = mlflow_model_cr(model, namespace, model, "champion", interval=60,
+                             maxNumSeqs=engine_kwargs.get("max_num_seqs", 256),
+                             maxModelLen=engine_kwargs.get("max_model_len", 4096))
+        await kube.create(GROUP, VERSION, namespace, PLURAL, cr)
+
+        async def ready():
+            o = await kube.get(GROUP, VERSION, namespace, PLURAL, model)
+            return (o.get("status") or {}).get("ready") == "True" and o
+
+        obj = await wait_for(ready, timeout_s)
+        ready_s = time.perf_counter() - t0
+        sd = await kube.get(SELDON_GROUP, SELDON_VERSION, namespace, SELDON_PLURAL, model)
+        pred = sd["spec"]["predictors"][0]
+        info = {"cr_ready_s": round(ready_s, 3), "phase": obj["status"].get("phase"),
+                "predictor": pred["name"], "runtime": pred.get("annotations", {}).get("mlop.amd.com/runtime"),
+                "placement": {k.split("/")[-1]: v for k, v in pred.get("annotations", {}).items()
+                              if k != "mlop.amd.com/runtime"},
+                "events": [e["reason"] for e in kube.events],
+                "weight_gb": round(built["engine"].model.weight_bytes() / 1e9, 2),
+                "kv_blocks": built["engine"].kv.num_blocks}
+        # hand the engine to the caller: stop the control loops, keep the engine
+        ctl.pods.clear()
+        await ctl.stop()
+        await op.stop()
+        return built["engine"], info
+
+    return asyncio.run(main())

@@ -80,12 +80,15 @@ class GateResult:
 
 
 def should_promote(new: dict, old: dict, thresholds: dict, error_rate_floor: float = 0.0,
-                   extra_max_ratio: dict | None = None, logger=None) -> GateResult:
+                   extra_max_ratio: dict | None = None, logger=None,
+                   latency_floor_s: float = 0.0) -> GateResult:
     """Reference gate (mlflow_operator.py:419-460): all of latency_95th, error_rate,
     latency_avg must exist for both; new <= old * (1 + threshold) for each.
     ``error_rate_floor``: also accept new error rate <= floor (the reference's
     relative test with a 0 baseline demands exactly 0 errors).  ``extra_max_ratio``:
-    {metric: ratio} extra guards (e.g. GPU HBM use), skipped if either side is None."""
+    {metric: ratio} extra guards (e.g. GPU HBM use), skipped if either side is None.
+    ``latency_floor_s``: latencies at or below this are always acceptable (relative
+    tests on sub-millisecond latencies are noise; 0 reproduces the reference)."""
     reasons = []
     for k in ("latency_95th", "error_rate", "latency_avg"):
         if new.get(k) is None or old.get(k) is None:
@@ -97,7 +100,7 @@ def should_promote(new: dict, old: dict, thresholds: dict, error_rate_floor: flo
     ok = True
     for k in ("latency_95th", "latency_avg"):
         lim = old[k] * (1 + thresholds.get(k, 0.05))
-        if new[k] > lim:
+        if new[k] > lim and new[k] > latency_floor_s:
             ok = False
             reasons.append(f"{k} {new[k]:.4g} > {lim:.4g}")
     lim = old["error_rate"] * (1 + thresholds.get("error_rate", 0.02))

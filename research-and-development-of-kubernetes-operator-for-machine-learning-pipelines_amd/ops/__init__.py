@@ -184,6 +184,8 @@ def _gemm_backend(M, N, K, epi, x2, w, o2) -> str:
     """Per-shape choice between the hand-written MFMA kernel and hipBLASLt,
     measured once per (M bucket, N, K, epilogue) on first eager use (never
     during graph capture).  ``gemm_choices()`` reports the table."""
+    if N % 8 or K % 64 or (epi != EPI_NONE and N % 32):
+        return "hipblaslt"  # shapes outside the MFMA kernel's tiling contract (e.g. tiny routers)
     if GEMM_BACKEND != "auto":
         return GEMM_BACKEND
     key = (_mbucket(M), N, K, epi)

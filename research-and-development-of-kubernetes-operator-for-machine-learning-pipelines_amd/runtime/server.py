@@ -1,0 +1,242 @@
+"""The predictor container: V2 ("kfserving") inference protocol server (G6).
+
+Endpoints (the SeldonDeployment's ``protocol: kfserving`` / Open Inference Protocol):
+  GET  /v2/health/live | /v2/health/ready | /v2 | /v2/models/{m} | /v2/models/{m}/ready
+  POST /v2/models/{m}/infer             tensors in / tensors out (sklearn or LLM)
+  POST /v2/models/{m}/generate          {"text_input" | "input_ids", "parameters": {...}}
+  POST /v2/models/{m}/generate_stream   server-sent events, one per token
+  POST /api/v1.0/feedback               Seldon feedback (counted as service="feedback")
+  GET  /metrics                         Prometheus exposition (runtime/metrics.py)
+
+Every request is timed into the Seldon-executor histograms with its HTTP
+code, which is what the operator's canary gate queries.
+
+``python -m mlopamd.runtime.server --runtime mlop-llm --architecture llama3-8b``
+starts it; configuration also comes from the env the SeldonDeployment sets
+(MLOP_RUNTIME, MLOP_MODEL_URI, MLOP_ARCHITECTURE, MLOP_ENGINE_*).
+Fault injection for canary tests: MLOP_INJECT_LATENCY_S, MLOP_INJECT_ERROR_RATE.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import time
+
+import numpy as np
+
+from .sampler import SamplingParams
+
+_DT = {"FP32": np.float32, "FP64": np.float64, "INT64": np.int64, "INT32": np.int32, "FP16": np.float16,
+       "BOOL": np.bool_, "UINT8": np.uint8}
+_DT_NAME = {np.dtype(v): k for k, v in _DT.items()}
+
+
+def _params(p: dict) -> SamplingParams:
+    return SamplingParams(max_tokens=int(p.get("max_tokens", 64)), temperature=float(p.get("temperature", 0.0)),
+                          top_k=int(p.get("top_k", 0)), top_p=float(p.get("top_p", 1.0)),
+                          ignore_eos=bool(p.get("ignore_eos", False)),
+                          stop_token_ids=list(p.get("stop_token_ids", [])))
+
+
+def make_app(backend, metrics, version: str = "1", inject_latency_s: float | None = None,
+             inject_error_rate: float | None = None):
+    from aiohttp import web
+
+    lat = float(os.environ.get("MLOP_INJECT_LATENCY_S", inject_latency_s or 0.0))
+    err_rate = float(os.environ.get("MLOP_INJECT_ERROR_RATE", inject_error_rate or 0.0))
+    state = {"ready": getattr(backend, "ready", True)}
+
+    @web.middleware
+    async def timing(request, handler):
+        t0 = time.perf_counter()
+        service = "feedback" if request.path.endswith("/feedback") else (
+            "generate" if "generate" in request.path else "predictions")
+        code = 500
+        try:
+            if request.method == "POST" and not request.path.endswith("/feedback"):
+                if lat:
+                    await asyncio.sleep(lat)
+                if err_rate and random.random() < err_rate:
+                    raise web.HTTPInternalServerError(text="injected failure")
+            resp = await handler(request)
+            code = resp.status
+            return resp
+        except web.HTTPException as e:
+            code = e.status
+            raise
+        finally:
+            if request.method == "POST" and metrics is not None:
+                metrics.observe_request(time.perf_counter() - t0, code=code, service=service)
+
+    app = web.Application(middlewares=[timing], client_max_size=64 * 2**20)
+
+    async def live(_):
+        return web.json_response({"live": True})
+
+    async def ready(_):
+        ok = bool(getattr(backend, "ready", True))
+        return web.json_response({"ready": ok}, status=200 if ok else 503)
+
+    async def server_meta(_):
+        return web.json_response({"name": "mlopamd-runtime", "version": "0.1.0",
+                                  "extensions": ["generate", "metrics"]})
+
+    async def model_meta(req):
+        md = backend.metadata()
+        md["versions"] = [version]
+        return web.json_response(md)
+
+    async def infer(req):
+        body = await req.json()
+        inputs = {i["name"]: i for i in body.get("inputs", [])}
+        if backend.kind == "sklearn":
+            first = next(iter(inputs.values()))
+            x = np.asarray(first["data"], dtype=_DT.get(first.get("datatype", "FP32"), np.float32))
+            x = x.reshape(first.get("shape", x.shape))
+            y = backend.predict(x)
+            y = np.asarray(y)
+            dt = _DT_NAME.get(y.dtype, "BYTES")
+            data = y.tolist() if dt != "BYTES" else [str(v) for v in y.tolist()]
+            return web.json_response({"model_name": backend.name, "model_version": version,
+                                      "id": body.get("id", ""), "outputs": [
+                                          {"name": "predict", "shape": list(y.shape), "datatype": dt, "data": data}]})
+        params = _params(body.get("parameters", {}))
+        if "input_ids" in inputs:
+            ids = [int(v) for v in inputs["input_ids"]["data"]]
+            res = await backend.generate(ids, params)
+            out = {"name": "output_ids", "shape": [len(res["output_ids"])], "datatype": "INT64",
+                   "data": res["output_ids"]}
+        else:
+            text = inputs["text_input"]["data"][0]
+            res = await backend.generate(backend.tokenizer.encode(text), params)
+            out = {"name": "text_output", "shape": [1], "datatype": "BYTES",
+                   "data": [backend.tokenizer.decode(res["output_ids"])]}
+        return web.json_response({"model_name": backend.name, "model_version": version, "id": body.get("id", ""),
+                                  "outputs": [out], "parameters": {"finish_reason": res["finish_reason"]}})
+
+    async def generate(req):
+        if backend.kind != "llm":
+            raise web.HTTPBadRequest(text="generate is only served by LLM predictors")
+        body = await req.json()
+        params = _params(body.get("parameters", body))
+        ids = body.get("input_ids") or backend.tokenizer.encode(body.get("text_input", ""))
+        res = await backend.generate(ids, params)
+        return web.json_response({"model_name": backend.name, "model_version": version,
+                                  "text_output": backend.tokenizer.decode(res["output_ids"]),
+                                  "output_ids": res["output_ids"], "finish_reason": res["finish_reason"],
+                                  "usage": {"prompt_tokens": res["prompt_tokens"],
+                                            "completion_tokens": len(res["output_ids"])},
+                                  "ttft_s": res["ttft"], "latency_s": res["latency"]})
+
+    async def generate_stream(req):
+        if backend.kind != "llm":
+            raise web.HTTPBadRequest(text="generate_stream is only served by LLM predictors")
+        body = await req.json()
+        params = _params(body.get("parameters", body))
+        ids = body.get("input_ids") or backend.tokenizer.encode(body.get("text_input", ""))
+        r = backend.submit(ids, params, stream=True)
+        resp = web.StreamResponse(headers={"Content-Type": "text/event-stream"})
+        await resp.prepare(req)
+        while True:
+            tok = await r.queue.get()
+            if tok is None:
+                break
+            await resp.write(f"data: {json.dumps({'token_id': tok, 'text_output': backend.tokenizer.decode([tok])})}\n\n".encode())
+        res = await r.future
+        await resp.write(f"data: {json.dumps({'finish_reason': res['finish_reason'], 'done': True})}\n\n".encode())
+        await resp.write_eof()
+        return resp
+
+    async def feedback(req):
+        await req.read()
+        return web.json_response({"status": "ok"})
+
+    async def prom(_):
+        if metrics is None:
+            return web.Response(text="")
+        try:
+            from .gpu_metrics import sample
+
+            metrics.update_gpu(sample())
+        except Exception:  # noqa: BLE001
+            pass
+        return web.Response(body=metrics.exposition(), content_type="text/plain", charset="utf-8")
+
+    r = app.router
+    r.add_get("/v2/health/live", live)
+    r.add_get("/v2/health/ready", ready)
+    r.add_get("/v2", server_meta)
+    r.add_get("/v2/models/{m}", model_meta)
+    r.add_get("/v2/models/{m}/ready", ready)
+    r.add_post("/v2/models/{m}/infer", infer)
+    r.add_post("/v2/models/{m}/generate", generate)
+    r.add_post("/v2/models/{m}/generate_stream", generate_stream)
+    r.add_post("/api/v1.0/feedback", feedback)
+    r.add_post("/api/v1.0/predictions", infer)
+    r.add_get("/metrics", prom)
+    return app
+
+
+def build_backend(runtime: str, model_uri: str | None, architecture: str | None, name: str, metrics,
+                  device: str = "cuda", engine_kwargs: dict | None = None, seed: int = 0, tp_state=None):
+    if runtime in ("mlop-sklearn", "sklearn"):
+        from .backends import SklearnBackend
+
+        return SklearnBackend(model_uri, name=name)
+    from .backends import LLMBackend
+    from .deploy import build_engine
+
+    t0 = time.perf_counter()
+    eng = build_engine(architecture or "llama3-8b", device=device, seed=seed, tp_state=tp_state,
+                       **(engine_kwargs or {}))
+    if metrics is not None:
+        metrics.load_seconds.labels(**metrics.labels).set(time.perf_counter() - t0)
+        metrics.ready.labels(**metrics.labels).set(1)
+    return LLMBackend(eng, metrics, name=name).start()
+
+
+def engine_kwargs_from_env() -> dict:
+    out = {}
+    for k, v in os.environ.items():
+        if k.startswith("MLOP_ENGINE_"):
+            key = k[len("MLOP_ENGINE_"):].lower()
+            try:
+                out[key] = json.loads(v)
+            except ValueError:
+                out[key] = v
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="mlopamd V2 inference server")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=int(os.environ.get("MLOP_PORT", 9000)))
+    ap.add_argument("--runtime", default=os.environ.get("MLOP_RUNTIME", "mlop-llm"))
+    ap.add_argument("--model-uri", default=os.environ.get("MLOP_MODEL_URI"))
+    ap.add_argument("--architecture", default=os.environ.get("MLOP_ARCHITECTURE"))
+    ap.add_argument("--name", default=os.environ.get("MLOP_MODEL_NAME", "model"))
+    ap.add_argument("--version", default=os.environ.get("MLOP_MODEL_VERSION", "1"))
+    ap.add_argument("--device", default=os.environ.get("MLOP_DEVICE", "cuda"))
+    ap.add_argument("--tp", type=int, default=1)
+    a = ap.parse_args(argv)
+
+    from aiohttp import web
+
+    from .metrics import RuntimeMetrics
+
+    metrics = RuntimeMetrics(model_name=a.name)
+    tp_state = None
+    if a.tp > 1 or int(os.environ.get("WORLD_SIZE", 1)) > 1:
+        from .tp_worker import serve_tp
+
+        return serve_tp(a, metrics)
+    backend = build_backend(a.runtime, a.model_uri, a.architecture, a.name, metrics, a.device,
+                            engine_kwargs_from_env(), tp_state=tp_state)
+    web.run_app(make_app(backend, metrics, version=a.version), host=a.host, port=a.port, print=None)
+
+
+if __name__ == "__main__":
+    main()
