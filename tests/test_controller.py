@@ -1,0 +1,349 @@
+"""Control-plane integration tests on the in-memory fakes with a VIRTUAL clock:
+the reference's 540 s canary and 60 s polls run in milliseconds.
+
+Covers SURVEY.md §3.2-3.6 / Appendix A: first deploy, canary promotion,
+canary failure -> rollback (+ anti-flap), reference no-rollback mode, alias
+removal, registry outage (no delete), operator restart mid-canary, 409 retry,
+CR deletion GC, spec update restarting the daemon, readiness gating.
+"""
+import asyncio
+
+import pytest
+
+from mlopamd.controller import seldon
+from mlopamd.controller.app import OperatorMetrics, make_operator
+from mlopamd.controller.clock import VirtualClock
+from mlopamd.controller.crd import (GROUP, PLURAL, SELDON_GROUP, SELDON_PLURAL, SELDON_VERSION, VERSION,
+                                    OperatorSettings)
+from mlopamd.controller.kube import FakeKube
+from mlopamd.controller.local import FakeSeldonController, SimLauncher, mlflow_model_cr
+from mlopamd.controller.mlflow import LocalMlflowClient, SqliteRegistry
+from mlopamd.controller.prometheus import LocalProm, MetricStore
+
+NS = "models"
+
+
+class Env:
+    def __init__(self, profiles=None, rollback=True, startup=None):
+        self.kube = FakeKube()
+        self.reg = SqliteRegistry()
+        self.clock = VirtualClock()
+        self.store = MetricStore()
+        self.metrics = OperatorMetrics()
+        self.profiles = profiles or {}
+        self.launcher = SimLauncher(self.store, self.clock, self.profiles, rps=100, period=5)
+        self.rollback = rollback
+
+    async def start(self):
+        self.op, self.rec = make_operator(self.kube, LocalMlflowClient(self.reg), LocalProm(self.store, self.clock),
+                                          self.clock, OperatorSettings(), metrics=self.metrics)
+        self.ctl = FakeSeldonController(self.kube, self.launcher, self.clock).start()
+        await self.op.start()
+
+    async def stop(self):
+        await self.op.stop()
+        await self.ctl.stop()
+
+    def version(self, tags=None):
+        mv = self.reg.create_model_version("m", f"mlflow-artifacts:/7/abc{len(self.profiles)}/artifacts/model",
+                                           tags=tags or {})
+        return mv.version
+
+    async def create_cr(self, **spec):
+        canary = spec.pop("canary", {})
+        canary.setdefault("rollback", self.rollback)
+        await self.kube.create(GROUP, VERSION, NS, PLURAL,
+                               mlflow_model_cr("m", NS, "m", "champion", interval=60, canary=canary, **spec))
+
+    async def status(self):
+        return (await self.kube.get(GROUP, VERSION, NS, PLURAL, "m")).get("status") or {}
+
+    async def sd(self):
+        try:
+            return await self.kube.get(SELDON_GROUP, SELDON_VERSION, NS, SELDON_PLURAL, "m")
+        except Exception:  # noqa: BLE001
+            return None
+
+    async def run_until(self, cond, max_virtual_s=5000.0):
+        start = self.clock.now()
+        while self.clock.now() - start < max_virtual_s:
+            if await cond():
+                return True
+            await self.clock.sleep(1.0)
+        return False
+
+    def reasons(self):
+        return [e["reason"] for e in self.kube.events]
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 60))
+
+
+def test_first_deploy_reference_contract():
+    async def go():
+        env = Env()
+        v1 = env.version()
+        env.reg.set_alias("m", "champion", v1)
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        st = await env.status()
+        assert st["currentModelVersion"] == "1" and st.get("previousModelVersion") is None and "error" not in st
+        sd = await env.sd()
+        assert sd["apiVersion"] == "machinelearning.seldon.io/v1" and sd["spec"]["protocol"] == "kfserving"
+        owner = sd["metadata"]["ownerReferences"][0]
+        assert owner["kind"] == "MlflowModel" and owner["controller"] and owner["blockOwnerDeletion"]
+        (p,) = sd["spec"]["predictors"]
+        assert p["name"] == "v1" and p["traffic"] == 100 and p["replicas"] == 1
+        assert p["graph"] == {"name": "classifier-1", "implementation": "MLFLOW_SERVER",
+                              "modelUri": "s3://mlflow/7/abc0/artifacts/model",
+                              "envSecretRefName": "minio-secret", "children": []}
+        assert env.reasons()[:2] == ["NewModelVersionDetected", "PredictorReady"]
+        await env.stop()
+    run(go())
+
+
+async def _ready(env):
+    return (await env.status()).get("ready") == "True"
+
+
+async def _phase(env, *phases):
+    return (await env.status()).get("phase") in phases
+
+
+def test_canary_promotes_in_reference_steps():
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"latency": 0.05}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        seen = []
+
+        async def track():
+            sd = await env.sd()
+            seen.append(seldon.traffic_of(sd))
+            return await _phase(env, "Promoted")
+        t0 = env.clock.now()
+        assert await env.run_until(track, 3000)
+        elapsed = env.clock.now() - t0
+        # 10 -> 100 in +10 steps, >= 60 s apart (reference: >= 9 x 60 s)
+        news = sorted({t.get("v2") for t in seen if t.get("v2")})
+        assert news[0] == 10 and 100 in news and len(news) >= 9
+        assert elapsed >= 8 * 60
+        assert env.reasons().count("TrafficIncrease") == 8
+        assert env.reasons()[-1] == "PromotionComplete"
+        sd = await env.sd()
+        assert [p["name"] for p in sd["spec"]["predictors"]] == ["v2"]
+        st = await env.status()
+        assert st["currentModelVersion"] == "2" and st["previousModelVersion"] == "1"
+        await env.stop()
+    run(go())
+
+
+def test_canary_regression_rolls_back_and_does_not_flap():
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"latency": 0.5}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "RolledBack"), 3000)
+        st = await env.status()
+        assert st["currentModelVersion"] == "1" and st["rolledBackVersion"] == "2"
+        assert "PromotionFailed" in env.reasons() and env.reasons()[-1] == "RollbackComplete"
+        sd = await env.sd()
+        assert seldon.traffic_of(sd) == {"v1": 100}
+        # the alias still points at v2: it must NOT be redeployed (no flapping)
+        n_new = env.reasons().count("NewModelVersionDetected")
+        await env.clock.sleep(600)
+        assert env.reasons().count("NewModelVersionDetected") == n_new
+        assert seldon.traffic_of(await env.sd()) == {"v1": 100}
+        # a NEW version is still picked up
+        env.profiles["3"] = {"latency": 0.05}
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "Promoted"), 3000)
+        await env.stop()
+    run(go())
+
+
+def test_reference_mode_no_rollback_leaves_split():
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"error_rate": 0.5, "latency": 0.05}}, rollback=False)
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "PromotionFailed"), 3000)
+        assert seldon.traffic_of(await env.sd()) == {"v1": 90, "v2": 10}
+        assert "RollbackComplete" not in env.reasons()
+        await env.stop()
+    run(go())
+
+
+def test_alias_removed_deletes_deployment():
+    async def go():
+        env = Env()
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.delete_alias("m", "champion")
+        assert await env.run_until(lambda: _phase(env, "AliasNotFound"), 200)
+        st = await env.status()
+        assert st["error"] == "Alias 'champion' does not exist"
+        assert st.get("currentModelVersion") is None and st.get("previousModelVersion") is None
+        assert await env.sd() is None
+        assert "AliasNotFound" in env.reasons()
+        # alias back -> redeployed
+        env.reg.set_alias("m", "champion", 1)
+        assert await env.run_until(lambda: _ready(env), 200)
+        await env.stop()
+    run(go())
+
+
+def test_registry_outage_keeps_serving():
+    async def go():
+        env = Env()
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.fail_mode = "unavailable"
+        await env.clock.sleep(300)
+        assert await env.sd() is not None  # the reference deleted it here
+        assert "RegistryUnavailable" in env.reasons() and "AliasNotFound" not in env.reasons()
+        env.reg.fail_mode = None
+        await env.clock.sleep(120)
+        assert "registryUnavailable" not in await env.status()
+        await env.stop()
+    run(go())
+
+
+def test_operator_restart_resumes_canary():
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"latency": 0.05}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+
+        async def at_30():
+            return (await env.status()).get("canaryTraffic", 0) >= 30
+        assert await env.run_until(at_30, 2000)
+        await env.op.stop()  # operator pod dies mid-canary
+        await env.clock.sleep(30)
+        env.op, env.rec = make_operator(env.kube, LocalMlflowClient(env.reg), LocalProm(env.store, env.clock),
+                                        env.clock, OperatorSettings())
+        await env.op.start()
+        assert await env.run_until(lambda: _phase(env, "Promoted"), 3000)
+        assert seldon.traffic_of(await env.sd()) == {"v2": 100}
+        await env.stop()
+    run(go())
+
+
+def test_conflict_on_apply_is_retried():
+    async def go():
+        env = Env(profiles={"1": {}, "2": {}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.kube.fail_next("replace", 409, times=2)
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "Canary"), 300)
+        assert await env.run_until(lambda: _has_two(env), 300)
+        await env.stop()
+    run(go())
+
+
+async def _has_two(env):
+    sd = await env.sd()
+    return sd and len(sd["spec"]["predictors"]) == 2
+
+
+def test_cr_delete_garbage_collects_sd():
+    async def go():
+        env = Env()
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        await env.kube.delete(GROUP, VERSION, NS, PLURAL, "m")
+        await env.clock.sleep(5)
+        assert await env.sd() is None and not env.ctl.pods
+        await env.stop()
+    run(go())
+
+
+def test_spec_update_switches_alias():
+    async def go():
+        env = Env()
+        v1, v2 = env.version(), env.version()
+        env.reg.set_alias("m", "champion", v1)
+        env.reg.set_alias("m", "challenger", v2)
+        await env.start()
+        await env.create_cr(canary={"initialTraffic": 50, "step": 50})
+        assert await env.run_until(lambda: _ready(env))
+        await env.kube.patch(GROUP, VERSION, NS, PLURAL, "m", {"spec": {"modelAlias": "challenger"}})
+
+        async def on_v2():
+            return (await env.status()).get("currentModelVersion") == "2"
+        assert await env.run_until(on_v2, 300)
+        await env.stop()
+    run(go())
+
+
+def test_slow_predictor_gates_after_readiness():
+    async def go():
+        env = Env(profiles={"1": {}, "2": {"startup_s": 400}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        await env.clock.sleep(350)  # the reference would have failed the canary by now (90 s budget)
+        st = await env.status()
+        assert st["phase"] == "Canary" and st.get("canaryAttempts", 0) == 0
+        assert await env.run_until(lambda: _phase(env, "Promoted"), 3000)
+        await env.stop()
+    run(go())
+
+
+def test_llm_runtime_predictor_gets_gpus_and_placement():
+    async def go():
+        env = Env()
+        v = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v)
+        await env.start()
+        await env.create_cr(tensorParallel=8, maxModelLen=8192, maxNumSeqs=128)
+        assert await env.run_until(lambda: _ready(env))
+        (p,) = (await env.sd())["spec"]["predictors"]
+        c = p["componentSpecs"][0]["spec"]["containers"][0]
+        assert c["resources"]["limits"]["amd.com/gpu"] == "8"
+        assert p["annotations"]["mlop.amd.com/runtime"] == "mlop-llm"
+        assert p["annotations"]["mlop.amd.com/tensorParallel"] == "8"
+        env_names = {e["name"]: e["value"] for e in c["env"]}
+        assert env_names["PREDICTOR_ID"] == "v1" and env_names["SELDON_DEPLOYMENT_ID"] == "m"
+        assert env_names["MLOP_ARCHITECTURE"] == "llama3-70b"
+        await env.stop()
+    run(go())
+
+
+def test_invalid_spec_reports_error():
+    async def go():
+        env = Env()
+        await env.start()
+        await env.kube.create(GROUP, VERSION, NS, PLURAL,
+                              {"apiVersion": "mlflow.nizepart.com/v1alpha1", "kind": "MlflowModel",
+                               "metadata": {"name": "m"}, "spec": {"modelAlias": "x"}})
+        await env.clock.sleep(5)
+        st = await env.status()
+        assert st["phase"] == "Invalid" and "modelName" in st["error"]
+        await env.stop()
+    run(go())

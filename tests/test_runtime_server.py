@@ -1,0 +1,116 @@
+"""The V2 runtime server (in-process, CPU): sklearn + LLM backends, executor
+metrics, streaming, fault injection; and the config-1 end-to-end demo."""
+import asyncio
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from mlopamd.runtime.backends import ByteTokenizer, LLMBackend, SklearnBackend, save_linear_model
+from mlopamd.runtime.metrics import RuntimeMetrics
+from mlopamd.runtime.server import make_app
+
+
+def _client(app):
+    from aiohttp.test_utils import TestClient, TestServer
+
+    return TestClient(TestServer(app))
+
+
+def test_sklearn_iris_v2_infer(tmp_path):
+    from mlopamd.controller.demo import train_iris
+
+    path, acc = train_iris(tmp_path / "m")
+    b = SklearnBackend(f"file://{path}", name="iris")
+    m = RuntimeMetrics("iris", "v1", "ns", "iris")
+    from sklearn.datasets import load_iris
+
+    X, y = load_iris(return_X_y=True)
+
+    async def go():
+        async with _client(make_app(b, m)) as c:
+            r = await c.get("/v2/health/ready")
+            assert r.status == 200
+            r = await c.post("/v2/models/iris/infer", json={"inputs": [
+                {"name": "input-0", "shape": [150, 4], "datatype": "FP64", "data": X.ravel().tolist()}]})
+            body = await r.json()
+            pred = np.asarray(body["outputs"][0]["data"])
+            assert (pred == y).mean() == pytest.approx(acc)
+            await c.post("/api/v1.0/feedback", json={"reward": 1})
+            txt = await (await c.get("/metrics")).text()
+            assert 'seldon_api_executor_client_requests_seconds_count{code="200",deployment_name="iris"' in txt
+            assert 'service="feedback"' in txt
+    asyncio.run(go())
+
+
+def test_linear_model_binary_and_regression(tmp_path):
+    p = save_linear_model(tmp_path / "b", [[1.0, -1.0]], [0.0], [0, 1])
+    b = SklearnBackend(str(p))
+    assert b.predict(np.array([[2.0, 1.0], [0.0, 3.0]])).tolist() == [1, 0]
+
+
+@pytest.fixture(scope="module")
+def llm_backend():
+    from mlopamd.models import build_model
+    from mlopamd.models.config import TINY_LLAMA
+    from mlopamd.runtime.engine import Engine, EngineConfig
+
+    torch.manual_seed(0)
+    m = build_model(TINY_LLAMA, device="cpu", dtype=torch.float32)
+    eng = Engine(m, EngineConfig(max_num_seqs=4, max_model_len=256, num_kv_blocks=64, use_graphs=False))
+    b = LLMBackend(eng, RuntimeMetrics("llm", "v1", "ns", "tiny"), name="tiny").start()
+    yield b
+    b.stop()
+
+
+def test_llm_generate_infer_stream(llm_backend):
+    async def go():
+        async with _client(make_app(llm_backend, llm_backend.metrics)) as c:
+            r = await c.post("/v2/models/tiny/generate", json={"text_input": "hello", "parameters": {
+                "max_tokens": 5, "ignore_eos": True}})
+            body = await r.json()
+            assert r.status == 200 and len(body["output_ids"]) == 5 and body["finish_reason"] == "length"
+            ids = ByteTokenizer().encode("hello")
+            r = await c.post("/v2/models/tiny/infer", json={"inputs": [
+                {"name": "input_ids", "shape": [len(ids)], "datatype": "INT64", "data": ids}],
+                "parameters": {"max_tokens": 5, "ignore_eos": True}})
+            body2 = await r.json()
+            assert body2["outputs"][0]["data"] == body["output_ids"]  # greedy: deterministic
+            r = await c.post("/v2/models/tiny/generate_stream", json={"input_ids": ids, "parameters": {
+                "max_tokens": 4, "ignore_eos": True}})
+            events = [json.loads(line[6:]) for line in (await r.text()).split("\n\n") if line.startswith("data: ")]
+            assert [e["token_id"] for e in events[:-1]] == body["output_ids"][:4] and events[-1]["done"]
+            # concurrent requests batch together
+            outs = await asyncio.gather(*(c.post("/v2/models/tiny/generate", json={
+                "input_ids": [5 + i, 6, 7], "parameters": {"max_tokens": 3, "ignore_eos": True}}) for i in range(4)))
+            assert all(o.status == 200 for o in outs)
+            txt = await (await c.get("/metrics")).text()
+            assert "mlop_time_to_first_token_seconds_count" in txt and "mlop_generated_tokens_total" in txt
+    asyncio.run(go())
+
+
+def test_fault_injection_counts_errors(tmp_path):
+    p = save_linear_model(tmp_path / "b", [[1.0, -1.0]], [0.0], [0, 1])
+    b = SklearnBackend(str(p))
+    m = RuntimeMetrics("d", "v2", "ns", "m")
+
+    async def go():
+        async with _client(make_app(b, m, inject_error_rate=1.0)) as c:
+            r = await c.post("/v2/models/m/infer", json={"inputs": [{"name": "x", "shape": [1, 2],
+                                                                      "datatype": "FP32", "data": [1, 2]}]})
+            assert r.status == 500
+            txt = await (await c.get("/metrics")).text()
+            assert 'code="500"' in txt
+    asyncio.run(go())
+
+
+@pytest.mark.slow
+def test_config1_demo_end_to_end():
+    from mlopamd.controller.demo import run_demo
+
+    out = asyncio.run(asyncio.wait_for(run_demo(60), 240))
+    assert out["accuracy"] > 0.9 and out["canary_phase"] == "Promoted"
+    assert out["final_predictors"] == {"v2": 100}
+    assert out["events"][:2] == ["NewModelVersionDetected", "PredictorReady"]
+    assert "PromotionComplete" in out["events"]
