@@ -57,6 +57,40 @@ class LlamaModel:
         self.lm_head = self.embed if cfg.tie_embeddings else w(self.vocab_local, H)
         self.cos_sin = rope_table(D, cfg.max_position, cfg.rope_theta, cfg.rope_scaling, self.device)
 
+    # ---------------------------------------------------------- sharding --
+    @torch.no_grad()
+    def load_shard_from(self, full: "LlamaModel") -> "LlamaModel":
+        """Copy this rank's TP shard out of a full (TP=1) model with the same config
+        (checkpoint-style loading; also how the TP tests compare against TP=1)."""
+        cfg, tp, r = self.cfg, self.ps.tp_size, self.ps.tp_rank
+        D = cfg.head_dim
+        kv_r = r * self.n_kv if tp <= cfg.num_kv_heads else (r * cfg.num_kv_heads) // tp
+        qs = slice(r * self.n_q * D, (r + 1) * self.n_q * D)
+        ks = slice(kv_r * D, (kv_r + self.n_kv) * D)
+        vs = self.vocab_start, self.vocab_start + self.vocab_local
+        dev = self.device
+
+        def cp(dst, src):
+            dst.copy_(src.to(dev, dst.dtype))
+
+        cp(self.embed, full.embed[vs[0]:vs[1]])
+        for L, F in zip(self.layers, full.layers):
+            q, k, v = F["qkv"].split([cfg.q_size, cfg.kv_size, cfg.kv_size], 0)
+            cp(L["qkv"], torch.cat([q[qs], k[ks], v[ks]], 0))
+            cp(L["o"], F["o"][:, qs])
+            cp(L["in_norm"], F["in_norm"])
+            cp(L["post_norm"], F["post_norm"])
+            self._shard_mlp(L, F)
+        cp(self.final_norm, full.final_norm)
+        if self.lm_head is not self.embed:
+            cp(self.lm_head, full.lm_head[vs[0]:vs[1]])
+        return self
+
+    def _shard_mlp(self, L, F):
+        r, I = self.ps.tp_rank, self.inter
+        L["gate_up"].copy_(F["gate_up"][2 * r * I:2 * (r + 1) * I].to(self.device, self.dtype))
+        L["down"].copy_(F["down"][:, r * I:(r + 1) * I].to(self.device, self.dtype))
+
     # ---------------------------------------------------------------- MLP --
     def _init_mlp(self, w):
         # gate_up rows interleaved in groups of 16 (gate, up, gate, up, ...): the

@@ -32,12 +32,21 @@ class MixtralModel(LlamaModel):
             "w2": w(self.n_local_experts, H, I),
         }
 
+    def _shard_mlp(self, L, F):
+        e0, n = self.expert_start, self.n_local_experts
+        L["router"].copy_(F["router"].to(self.device, self.dtype))
+        L["w13"].copy_(F["w13"][e0:e0 + n].to(self.device, self.dtype))
+        L["w2"].copy_(F["w2"][e0:e0 + n].to(self.device, self.dtype))
+
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         from ..parallel.moe import moe_forward
 
         L = self.layers[i]
+        # TP attention (tokens replicated on the EP group): partial sums, summed by the
+        # layer's TP all-reduce.  DP attention (tp == 1, ep > 1): all-to-all dispatch.
+        mode = "alltoall" if (self.ps.ep.size > 1 and self.ps.tp.size == 1) else "allreduce"
         return moe_forward(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.ps.ep,
-                           self.expert_start, self.n_local_experts)
+                           self.expert_start, self.n_local_experts, mode=mode)
 
     def forward(self, ids, meta, kv):
         # MoE output is already complete per token (EP combine) -> no TP all-reduce

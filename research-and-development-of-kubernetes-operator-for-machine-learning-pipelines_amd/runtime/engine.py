@@ -33,6 +33,45 @@ from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, bl
 from .sampler import Sampler, SamplingParams
 
 
+KIND_STOP, KIND_EAGER, KIND_GRAPH = 0, 1, 2
+
+
+class StepSync:
+    """Lock-step execution across a tensor-parallel group: rank 0 broadcasts
+    [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket] and the
+    already-uploaded metadata / ids / logits-index device buffers (over RCCL
+    on GPU, gloo on CPU); every rank then runs the identical forward."""
+
+    def __init__(self, group):
+        self.g = group
+        self.is_leader = group.rank == 0
+
+    def send(self, eng, kind, T, nt, nl, part, nparts, bucket):
+        hdr = torch.tensor([kind, T, nt, nl, part, nparts, bucket, 0], dtype=torch.int64, device=eng.device)
+        self.g.broadcast(hdr, 0)
+        if kind == KIND_STOP:
+            return
+        m = eng.meta
+        self.g.broadcast(m.d, 0)
+        if T:
+            self.g.broadcast(m.ids_d[:T], 0)
+        if nl:
+            self.g.broadcast(m.lidx_d[:nl], 0)
+
+    def recv(self, eng):
+        hdr = torch.zeros(8, dtype=torch.int64, device=eng.device)
+        self.g.broadcast(hdr, 0)
+        kind, T, nt, nl, part, nparts, bucket, _ = hdr.tolist()
+        if kind != KIND_STOP:
+            m = eng.meta
+            self.g.broadcast(m.d, 0)
+            if T:
+                self.g.broadcast(m.ids_d[:T], 0)
+            if nl:
+                self.g.broadcast(m.lidx_d[:nl], 0)
+        return kind, T, nt, nl, part, nparts, bucket
+
+
 class Status(Enum):
     WAITING = 0
     PREFILL = 1
@@ -103,6 +142,14 @@ class Engine:
         mc = model.cfg
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         nb = cfg.num_kv_blocks or self._auto_blocks()
+        tp = model.ps.tp
+        self.step_sync = StepSync(tp) if tp.size > 1 else None
+        if tp.size > 1:  # every rank must address the same page ids: agree on the minimum
+            t = torch.tensor([nb], dtype=torch.int64, device=self.device)
+            import torch.distributed as dist
+
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=tp.handle)
+            nb = int(t.item())
         self.kv = KVCache(mc.num_layers, nb, model.n_kv, mc.head_dim, self.device, model.dtype)
         self.alloc = BlockAllocator(nb)
         self.max_blocks_per_seq = blocks_needed(self.max_model_len)
@@ -124,7 +171,10 @@ class Engine:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.stats = collections.Counter()
-        if cfg.use_graphs and self.device.type == "cuda":
+        import os
+
+        tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS") == "1"
+        if cfg.use_graphs and self.device.type == "cuda" and tp_graphs:
             self.capture_graphs()
 
     # ----------------------------------------------------------- sizing --
@@ -269,12 +319,9 @@ class Engine:
         done = [c == s.length for s, c in zip(batch, ctx)]
         T, nt, nl = self.meta.fill(rows, chunks, ctx, toks, want_logits=done)
         part, nparts = plan_partitions(nt, self.model.n_kv, max(ctx))
-        self.meta.upload(T, nl)
-        meta = self.meta.meta(T, nt, nl, part, nparts)
-        hidden = self.model.forward(self.meta.ids_d[:T], meta, self.kv)
+        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0)
         tokens = None
         if nl:
-            logits = self.model.logits(hidden[meta.logits_idx])
             done_seqs = [s for s, d in zip(batch, done) if d]
             tokens = self.sampler(logits, [s.params for s in done_seqs]).tolist()
         else:
@@ -317,18 +364,12 @@ class Engine:
         g = self.graphs.get(bucket) if bucket is not None else None
         if g is not None:
             self.meta.fill_decode(rows, ctx, last, pad_to=bucket)
-            self.meta.upload(bucket, bucket)
-            graph, logits_buf = g
-            graph.replay()
-            logits = logits_buf[:B]
+            logits = self._launch(KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket)[:B]
             self.stats["graph_steps"] += 1
         else:
             self.meta.fill_decode(rows, ctx, last, pad_to=B)
             part, nparts = plan_partitions(B, self.model.n_kv, int(ctx.max()))
-            self.meta.upload(B, B)
-            meta = self.meta.meta(B, B, B, part, nparts)
-            hidden = self.model.forward(self.meta.ids_d[:B], meta, self.kv)
-            logits = self.model.logits(hidden[meta.logits_idx])
+            logits = self._launch(KIND_EAGER, B, B, B, part, nparts, 0)
             self.stats["eager_decode_steps"] += 1
         tokens = self.sampler(logits, [s.params for s in self.running]).tolist()
         self.stats["decode_steps"] += 1
@@ -356,6 +397,42 @@ class Engine:
                 self.running.remove(s)
             self._finish(s, reason)
         return StepOutput(s.seq_id, int(tok), reason is not None, reason)
+
+    # --------------------------------------------------------- execution --
+    def _launch(self, kind: int, T: int, nt: int, nl: int, part: int, nparts: int, bucket: int):
+        """Ship this step's metadata to the device and run it.  With tensor
+        parallelism, rank 0 (the only rank that schedules) first broadcasts a
+        small header + the metadata buffers to the TP group (SURVEY §2.5 CL5);
+        the other ranks run the same ``_execute`` from ``worker_loop``."""
+        self.meta.upload(T, nl)
+        if self.step_sync is not None:
+            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket)
+        return self._execute(kind, T, nt, nl, part, nparts, bucket)
+
+    def _execute(self, kind, T, nt, nl, part, nparts, bucket):
+        if kind == KIND_GRAPH:
+            graph, logits_buf = self.graphs[bucket]
+            graph.replay()
+            return logits_buf
+        meta = self.meta.meta(T, nt, nl, part, nparts)
+        hidden = self.model.forward(self.meta.ids_d[:T], meta, self.kv)
+        if nl == 0:
+            return None
+        return self.model.logits(hidden[meta.logits_idx])
+
+    def worker_loop(self):
+        """Non-zero TP ranks: replay rank 0's steps until it sends STOP."""
+        assert self.step_sync is not None
+        while True:
+            hdr = self.step_sync.recv(self)
+            if hdr[0] == KIND_STOP:
+                return
+            self._execute(*hdr)
+            self.stats["worker_steps"] += 1
+
+    def shutdown(self):
+        if self.step_sync is not None and self.step_sync.is_leader:
+            self.step_sync.send(self, KIND_STOP, 0, 0, 0, 0, 0, 0)
 
     # ----------------------------------------------------------- graphs --
     def capture_graphs(self):

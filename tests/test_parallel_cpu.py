@@ -1,0 +1,124 @@
+"""Multi-process (gloo, world_size 2) tests of the parallel paths on CPU:
+TP lock-step engine == TP=1 engine (Llama and Mixtral TP+EP), expert-parallel
+all-to-all MoE == single-rank MoE, process-group helpers."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(rank, world, port, fn_name, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = globals()[fn_name](rank, world)
+        torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_ranks(fn_name, world=2):
+    d = tempfile.mkdtemp()
+    mp.start_processes(_entry, args=(world, _free_port(), fn_name, d), nprocs=world, join=True,
+                       start_method="spawn")
+    return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+
+
+PROMPTS = [[5, 9, 11, 40, 2, 7], list(range(20, 61)), [100, 3]]
+
+
+def _tp_engine(cfg_name):
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    cfg = get_config(cfg_name)
+    full = build_model(cfg, device="cpu", dtype=torch.float32, seed=4)
+    ps = make_parallel_state(tp_size=2, ep_size=2)
+    shard = build_model(cfg, device="cpu", dtype=torch.float32, pstate=ps, seed=4).load_shard_from(full)
+    ec = EngineConfig(max_num_seqs=4, max_num_batched_tokens=32, max_model_len=128, num_kv_blocks=40, use_graphs=False)
+    eng = Engine(shard, ec)
+    params = SamplingParams(max_tokens=6, ignore_eos=True)
+    if ps.tp_rank == 0:
+        outs = eng.generate(PROMPTS, params)
+        eng.shutdown()
+        ref = Engine(full, ec).generate(PROMPTS, params)
+        return {"tp": outs, "ref": ref}
+    eng.worker_loop()
+    return {"worker_steps": eng.stats["worker_steps"]}
+
+
+def tp_llama(rank, world):
+    return _tp_engine("tiny-llama")
+
+
+def tp_mixtral(rank, world):
+    return _tp_engine("tiny-mixtral")
+
+
+@pytest.mark.parametrize("fn", ["tp_llama", "tp_mixtral"])
+def test_tp2_engine_matches_tp1(fn):
+    r0, r1 = run_ranks(fn)
+    assert r0["tp"] == r0["ref"]
+    assert r1["worker_steps"] > 0
+
+
+def ep_alltoall(rank, world):
+    from mlopamd import ops
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.parallel.moe import local_experts, moe_forward
+
+    torch.manual_seed(0)
+    E, H, I, k = 4, 64, 32, 2
+    router = torch.randn(E, H)
+    w13 = 0.1 * torch.randn(E, 2 * I, H)
+    w2 = 0.1 * torch.randn(E, H, I)
+    xs = [torch.randn(7, H), torch.randn(5, H)]  # different token counts per rank
+    ps = make_parallel_state(tp_size=1, ep_size=1)
+    from mlopamd.parallel.comm import Group
+    import torch.distributed as dist
+
+    ep = Group(rank=rank, size=world, handle=None)
+    nl = E // world
+    out = moe_forward(xs[rank], router, w13[rank * nl:(rank + 1) * nl], w2[rank * nl:(rank + 1) * nl], k, ep,
+                      rank * nl, nl, mode="alltoall")
+    # single-rank reference with all experts
+    topw, topi = ops.moe_route(torch.nn.functional.linear(xs[rank], router), k)
+    ref = local_experts(xs[rank], topw, topi, w13, w2, 0, E)
+    return {"err": float((out - ref).abs().max())}
+
+
+def test_ep_alltoall_matches_single_rank():
+    for r in run_ranks("ep_alltoall"):
+        assert r["err"] < 1e-4
+
+
+def collectives(rank, world):
+    from mlopamd.parallel.comm import make_parallel_state
+
+    ps = make_parallel_state(tp_size=2)
+    x = torch.full((2, 3), float(rank + 1))
+    ps.tp.all_reduce(x)
+    g = ps.tp.all_gather(torch.tensor([[rank]]), dim=-1)
+    b = torch.tensor([rank * 10.0])
+    ps.tp.broadcast(b, 0)
+    return {"ar": x.tolist(), "ag": g.tolist(), "b": b.item()}
+
+
+def test_group_collectives():
+    for r in run_ranks("collectives"):
+        assert r["ar"] == [[3.0] * 3] * 2 and r["ag"] == [[0, 1]] and r["b"] == 0.0
