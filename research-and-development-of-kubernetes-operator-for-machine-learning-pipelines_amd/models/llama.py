@@ -103,6 +103,12 @@ class LlamaModel:
         act = ops.gemm(x, L["gate_up"], epi=ops.EPI_SILU_MUL)  # K1/K2 + fused K8
         return linear(act, L["down"])
 
+    def mlp_add_norm(self, i, x, residual, next_norm, eps):
+        """TP=1: MLP whose down projection also does residual += and the next norm."""
+        L = self.layers[i]
+        act = ops.gemm(x, L["gate_up"], epi=ops.EPI_SILU_MUL)
+        return ops.gemm_add_rmsnorm(act, L["down"], residual, next_norm, eps)
+
     # ------------------------------------------------------------ forward --
     def weight_tensors(self):
         yield self.embed
@@ -128,12 +134,17 @@ class LlamaModel:
             qkv = linear(x, L["qkv"])
             q = ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i], self.n_q)
             a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
+            nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
+            if tp.size == 1:
+                # O projection with the residual add + post-attention norm in its reduce pass
+                x = ops.gemm_add_rmsnorm(a.view(a.shape[0], -1), L["o"], residual, L["post_norm"], eps)
+                x = self.mlp_add_norm(i, x, residual, nxt, eps)
+                continue
             o = linear(a.view(a.shape[0], -1), L["o"])
             tp.all_reduce(o)
             x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
             m = self.mlp(i, x)
             tp.all_reduce(m)
-            nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
             x = ops.add_rmsnorm(m, residual, nxt, eps)
         return x
 

@@ -48,6 +48,9 @@ class MixtralModel(LlamaModel):
         return moe_forward(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.ps.ep,
                            self.expert_start, self.n_local_experts, mode=mode)
 
+    def mlp_add_norm(self, i, x, residual, next_norm, eps):
+        return ops.add_rmsnorm(self.mlp(i, x), residual, next_norm, eps)
+
     def forward(self, ids, meta, kv):
         # MoE output is already complete per token (EP combine) -> no TP all-reduce
         # when attention runs TP=1 inside an EP group; the base forward all-reduces

@@ -170,6 +170,24 @@ void gemm(Tensor out, Tensor a, Tensor w, Tensor ws, int64_t epi) {
                     (int)out.stride(0), wsp, wsn, (int)M, (int)N, (int)K, (int)epi, cur_stream());
 }
 
+// out = rmsnorm(residual += a . w^T) * norm_w through the split-K path; false = not taken
+bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor norm_w, Tensor ws,
+                      double eps) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(out, "out"); check_bf16(residual, "residual");
+  check_bf16(norm_w, "norm_w");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && N % 8 == 0, "w [N, K], K % 64");
+  TORCH_CHECK(out.numel() == M * N && residual.numel() == M * N && norm_w.numel() == N, "shapes");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat, "ws f32");
+  c10::DeviceGuard g(a.device());
+  return mlop::launch_gemm_add_rmsnorm(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(),
+                                       residual.data_ptr(), norm_w.data_ptr(), (float)eps,
+                                       ws.data_ptr<float>(), ws.numel(), (int)M, (int)N, (int)K,
+                                       cur_stream());
+}
+
 // grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
 void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi) {
   check_bf16(out, "out"); check_bf16(a, "a"); check_bf16(w, "w"); check_i32(offsets, "offsets");
@@ -260,6 +278,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
   m.def("grouped_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int max_rows, "
         "int epi) -> ()");
+  m.def("gemm_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor a, Tensor w, Tensor norm_w, "
+        "Tensor(c!) ws, float eps) -> bool");
   m.def("moe_route(Tensor(a!) topw, Tensor(b!) topi, Tensor logits) -> ()");
   m.def("moe_permute(Tensor(a!) xp, Tensor(b!) offsets, Tensor(c!) src, Tensor(d!) inv, Tensor x, "
         "Tensor topi, int e0, int n_local) -> ()");
@@ -288,6 +308,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("paged_attention", &paged_attention);
   m.impl("gemm", &gemm);
   m.impl("grouped_gemm", &grouped_gemm);
+  m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);
   m.impl("moe_route", &moe_route);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);

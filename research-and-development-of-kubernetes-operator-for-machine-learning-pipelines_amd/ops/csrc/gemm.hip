@@ -2,31 +2,35 @@
 //
 //   C[M, N] = A[M, K] . B[N, K]^T        (A: activations row-major, B: weights [out, in])
 //
-// Tiling: a workgroup owns a BM x BN output tile, K is walked in BK = 64 steps
-// through a double-buffered, XOR-swizzled LDS image (16-B chunk c of row r at
-// chunk c ^ (r & 7): the 16 rows a ds_read_b128 lane group reads land on 8
-// different 16-B bank slots, cdna_hip_programming.md §5.5 T2).  Staging is
-// register-based and split (T14): the next tile's global loads are issued
-// before the current tile's MFMAs and written to LDS after them.
-// Waves are arranged WM x WN; each wave owns (BM/WM) x (BN/WN) as a grid of
-// 16x16 accumulators fed by v_mfma_f32_16x16x32_bf16.
+// Structure (cdna_hip_programming.md §5 "glds vs register staging", "Pipelining
+// across barriers"):
+//   * a workgroup owns a BM x BN tile; K is walked in BK = 64 steps;
+//   * BOTH operands stream global -> LDS with global_load_lds_dwordx4 (LDS-DMA,
+//     no VGPR staging) into a 3-deep ring: two k-steps stay in flight while the
+//     MFMAs consume the third;
+//   * one raw s_barrier per k-step, preceded by a COUNTED vmcnt (never 0 in the
+//     steady state) — __syncthreads() would drain the DMA queue (its fence emits
+//     vmcnt(0));
+//   * the LDS image is lane-linear per 1 KiB piece (8 rows x 128 B), XOR-swizzled
+//     through the SOURCE address: 16-B chunk c of row r sits at slot c ^ (r & 7),
+//     so the 16 rows a ds_read_b128 lane group reads hit 8 different bank slots
+//     (T2, rule 21: swizzle the source and the read, never the LDS destination);
+//   * all LDS lives in ONE extern __shared__ array (a second object can make hipcc
+//     emit vmcnt(0) before every ds_read: §5 item 4(a));
+//   * waves WM x WN, each owning (BM/WM) x (BN/WN) as 16x16 accumulators fed by
+//     v_mfma_f32_16x16x32_bf16.
 //
-// Decode (M <= 256) is weight-streaming: BM covers the whole batch so every
-// weight byte is read from HBM once; when the N tiles cannot fill 256 CUs the
-// K range is split over blockIdx.z and fp32 partial slabs are combined by a
-// second (reduce) kernel that also applies the epilogue (launch-boundary
-// reduce, cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2).
+// Decode (M <= 256) is weight-streaming: BM covers the batch so each weight byte
+// is fetched from HBM once; when the N tiles cannot fill 256 CUs, K is split over
+// blockIdx.z and fp32 slabs are combined by a reduce kernel that also applies
+// the epilogue — optionally fused with the decoder's residual add + RMSNorm
+// (launch-boundary reduce, §5 "Projection GEMM at M = 256" item 2).
 //
-// Epilogues (applied from an fp32 LDS copy of the tile, 16-B coalesced stores):
+// Epilogues (fp32 LDS copy of the tile, 16-B coalesced stores):
 //   EPI_NONE      C = bf16(acc)
-//   EPI_SILU_MUL  B rows are gate/up interleaved in groups of 16
-//                 ([g0..g15, u0..u15, g16..g31, u16..u31, ...]) so a tile holds
-//                 matching gate and up columns: C[:, j] = silu(gate_j) * up_j
-//                 (C has N/2 columns) — fuses K8 into the gate_up projection.
-//
-// Grouped mode (MoE K13): A rows are sorted by expert, offsets[e]..offsets[e+1]
-// are expert e's rows, B = W[e] ([E, N, K]); blockIdx.y enumerates
-// (expert, m-tile) pairs (a block past the last pair exits immediately).
+//   EPI_SILU_MUL  B rows gate/up interleaved in groups of 16, C[:, j] = silu(g_j) * u_j (N/2 cols)
+// Grouped mode (MoE K13): A rows sorted by expert, offsets[e]..offsets[e+1];
+// B = W[e] ([E, N, K]); blockIdx.y enumerates (expert, m-tile) pairs on device.
 #include "common.h"
 #include "launch.h"
 
@@ -34,28 +38,46 @@ namespace mlop {
 
 enum { EPI_NONE = 0, EPI_SILU_MUL = 1 };
 constexpr int kBK = 64;
+constexpr int kStages = 3;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ float silu_bf(float g) {
+  const float gb = bf2f(f2bf(g));
+  return bf2f(f2bf(gb / (1.f + __expf(-gb))));
+}
 
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, float* __restrict__ ws, int M, int N, int K, int k_chunk,
     const int* __restrict__ offsets, int n_groups) {
-  constexpr int T = WM * WN * 64;
+  constexpr int NW = WM * WN, T = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int CH = (BM + BN) * (kBK / 8);  // 16-B chunks per stage
-  static_assert(CH % T == 0, "stage chunks must divide the thread count");
-  constexpr int CPT = CH / T;
+  constexpr int NP = (BM + BN) / 8;  // 1-KiB pieces (8 rows x 128 B) per stage
+  static_assert(NP % NW == 0, "pieces must divide the waves");
+  constexpr int PPW = NP / NW;        // LDS-DMA instructions per wave per stage
   constexpr int STAGE = (BM + BN) * kBK;  // bf16 elements per stage
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int n0 = blockIdx.x * BN;
   int m0 = blockIdx.y * BM, m_end = M;
   const uint16_t* Bg = B;
   if constexpr (GROUPED) {
-    // find (expert, m-tile) of this block
     int t = blockIdx.y, e = 0;
     for (; e < n_groups; ++e) {
       const int rows = offsets[e + 1] - offsets[e];
@@ -68,33 +90,33 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     m_end = offsets[e + 1];
     Bg = B + (size_t)e * N * ldb;
   }
-  const int kz = blockIdx.z;
-  const int kbeg = kz * k_chunk;
+  const int kbeg = blockIdx.z * k_chunk;
   const int kend = min(K, kbeg + k_chunk);
   const int nk = (kend - kbeg) / kBK;
 
-  u32x4 stage[CPT];
-  auto gload = [&](int k) {
+  // per-lane source row / chunk of each piece this wave issues (k advances by kBK)
+  const int prow = lane >> 3;                  // row inside the 8-row piece
+  const int pchunk = (lane & 7) ^ prow;        // source chunk for LDS slot (lane & 7)
+  const uint16_t* src[PPW];
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * T;
-      const int r = c >> 3, ch = c & 7;
-      if (r < BM) {
-        const int gr = min(m0 + r, m_end - 1);
-        stage[i] = *reinterpret_cast<const u32x4*>(A + (size_t)gr * lda + k + ch * 8);
-      } else {
-        const int gn = min(n0 + r - BM, N - 1);
-        stage[i] = *reinterpret_cast<const u32x4*>(Bg + (size_t)gn * ldb + k + ch * 8);
-      }
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wid + i * NW;
+    const int r = p * 8 + prow;
+    if (r < BM) {
+      const int gr = min(m0 + r, m_end - 1);
+      src[i] = A + (size_t)gr * lda + kbeg + pchunk * 8;
+    } else {
+      const int gn = min(n0 + r - BM, N - 1);
+      src[i] = Bg + (size_t)gn * ldb + kbeg + pchunk * 8;
     }
-  };
-  auto sstore = [&](int buf) {
+  }
+  auto issue = [&](int buf, int kt) {
     uint16_t* base = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * T;
-      const int r = c >> 3, ch = c & 7;
-      *reinterpret_cast<u32x4*>(base + r * kBK + ((ch ^ (r & 7)) << 3)) = stage[i];
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wid + i * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * kBK),
+                                       (lds_void_t*)(base + p * 512), 16, 0, 0);
     }
   };
 
@@ -104,15 +126,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(0);
-  }
-  __syncthreads();
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kbeg + (kt + 1) * kBK);
-    const uint16_t* sA = smem + buf * STAGE;
+    if (kt + 1 < nk) wait_vmcnt<PPW>(); else wait_vmcnt<0>();
+    raw_barrier();  // stage kt visible to all waves; stage kt-1's buffer free
+    if (kt + 2 < nk) issue((kt + 2) % kStages, kt + 2);
+    const uint16_t* sA = smem + (kt % kStages) * STAGE;
     const uint16_t* sB = sA + BM * kBK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -133,14 +153,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
   }
 
   const int rows_here = min(BM, m_end - m0);
   if (gridDim.z > 1) {
     // split-K: fp32 partial slab [kz][M][N] (plain stores; reduce kernel in the next launch)
-    float* P = ws + (size_t)kz * M * N;
+    float* P = ws + (size_t)blockIdx.z * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -154,7 +172,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
       }
     return;
   }
-  // epilogue through LDS: fp32 tile [BM][BN + 4]
+  raw_barrier();  // every wave is done reading the ring before it becomes the C tile
   float* sC = reinterpret_cast<float*>(smem);
   constexpr int LDC = BN + 4;
 #pragma unroll
@@ -187,13 +205,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
       const float* u = g + 16;
       u32x4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // HF order: silu in bf16, then the product
-        const float g0 = bf2f(f2bf(g[2 * j])), g1 = bf2f(f2bf(g[2 * j + 1]));
-        const float s0 = bf2f(f2bf(g0 / (1.f + __expf(-g0))));
-        const float s1 = bf2f(f2bf(g1 / (1.f + __expf(-g1))));
-        o[j] = pack2(s0 * bf2f(f2bf(u[2 * j])), s1 * bf2f(f2bf(u[2 * j + 1])));
-      }
+      for (int j = 0; j < 4; ++j)
+        o[j] = pack2(silu_bf(g[2 * j]) * bf2f(f2bf(u[2 * j])),
+                     silu_bf(g[2 * j + 1]) * bf2f(f2bf(u[2 * j + 1])));
       *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + n0 / 2 + j0) = o;
     }
   }
@@ -227,17 +241,75 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(uint16_t* __restrict
     u32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (EPI == EPI_NONE) {
+      if (EPI == EPI_NONE)
         o[j] = pack2(a[2 * j], a[2 * j + 1]);
-      } else {
-        const float g0 = bf2f(f2bf(a[2 * j])), g1 = bf2f(f2bf(a[2 * j + 1]));
-        const float s0 = bf2f(f2bf(g0 / (1.f + __expf(-g0))));
-        const float s1 = bf2f(f2bf(g1 / (1.f + __expf(-g1))));
-        o[j] = pack2(s0 * bf2f(f2bf(b[2 * j])), s1 * bf2f(f2bf(b[2 * j + 1])));
-      }
+      else
+        o[j] = pack2(silu_bf(a[2 * j]) * bf2f(f2bf(b[2 * j])),
+                     silu_bf(a[2 * j + 1]) * bf2f(f2bf(b[2 * j + 1])));
     }
     *reinterpret_cast<u32x4*>(C + (size_t)r * ldc + j0) = o;
   }
+}
+
+// split-K reduce fused with the decoder's residual add + RMSNorm (one row per block):
+//   y = bf16(sum_s slab[s][r]);  residual[r] = bf16(residual[r] + y);  out[r] = rmsnorm(residual[r]) * w
+template <int VPT>
+__global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
+    uint16_t* __restrict__ out, uint16_t* __restrict__ residual, const float* __restrict__ ws,
+    const uint16_t* __restrict__ w, float eps, int M, int N, int splits) {
+  __shared__ float scratch[16];
+  const int r = blockIdx.x;
+  const int nvec = N >> 3;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int s = 0; s < splits; ++s) {
+        const float4* p = reinterpret_cast<const float4*>(ws + ((size_t)s * M + r) * N + vi * 8);
+        float4 x = p[0], y = p[1];
+        a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
+        a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
+      }
+      u32x4 res = *reinterpret_cast<const u32x4*>(residual + (size_t)r * N + vi * 8);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float s0 = bf2f(f2bf(a[2 * j])) + lo_bf(res[j]);
+        const float s1 = bf2f(f2bf(a[2 * j + 1])) + hi_bf(res[j]);
+        o[j] = pack2(s0, s1);
+        v[i][2 * j] = lo_bf(o[j]);
+        v[i][2 * j + 1] = hi_bf(o[j]);
+      }
+      *reinterpret_cast<u32x4*>(residual + (size_t)r * N + vi * 8) = o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)N + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      u32x4 wv = *reinterpret_cast<const u32x4*>(w + vi * 8);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = pack2(bf2f(f2bf(v[i][2 * j] * inv)) * lo_bf(wv[j]),
+                     bf2f(f2bf(v[i][2 * j + 1] * inv)) * hi_bf(wv[j]));
+      *reinterpret_cast<u32x4*>(out + (size_t)r * N + vi * 8) = o;
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+constexpr size_t lds_bytes() {
+  constexpr size_t ring = (size_t)kStages * (BM + BN) * kBK * 2;
+  constexpr size_t epi = (size_t)BM * (BN + 4) * 4;
+  return ring > epi ? ring : epi;
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED>
@@ -245,9 +317,8 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
                     float* ws, int M, int N, int K, int splits, int k_chunk, const int* offsets,
                     int n_groups, int m_tiles, hipStream_t st) {
   constexpr int T = WM * WN * 64;
-  const size_t lds_stage = 2 * (size_t)(BM + BN) * kBK * 2;
-  const size_t lds_epi = (size_t)BM * (BN + 4) * 4;
-  const size_t lds = lds_stage > lds_epi ? lds_stage : lds_epi;
+  constexpr size_t lds = lds_bytes<BM, BN, WM, WN>();
+  static_assert(lds <= 163840, "LDS budget");
   auto kern = gemm_kernel<BM, BN, WM, WN, EPI, GROUPED>;
   static bool attr = false;
   if (!attr) {
@@ -256,78 +327,113 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
   }
   dim3 grid((N + BN - 1) / BN, m_tiles, splits);
   kern<<<grid, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups);
-  if (splits > 1) {
-    const int outw = EPI == EPI_NONE ? N : N / 2;
-    const long total = (long)M * (outw / 8);
-    const int g = (int)std::min<long>((total + 255) / 256, 4096);
-    splitk_reduce_kernel<EPI><<<g, 256, 0, st>>>(C, ldc, ws, M, N, splits);
-  }
 }
 
-// Host-side config choice.  Returns the workspace floats needed (0 if none) when
-// ws == nullptr && query, else launches.
-template <int EPI, bool GROUPED>
-static long dispatch(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc,
-                     float* ws, long ws_floats, int M, int N, int K, const int* offsets,
-                     int n_groups, int max_rows_per_group, hipStream_t st, bool query) {
-  // pick the tile by the (per-group) row count
-  const int mrows = GROUPED ? max_rows_per_group : M;
-  int BM, BN;
-  if (mrows <= 64) { BM = 64; BN = 64; }
-  else if (mrows <= 128) { BM = 128; BN = 64; }
-  else if (mrows <= 256 || GROUPED) { BM = 256; BN = 64; }
-  else { BM = 256; BN = 128; }
-  const int n_tiles = (N + BN - 1) / BN;
-  int m_tiles = GROUPED ? (M + BM - 1) / BM + n_groups : (M + BM - 1) / BM;
-  int splits = 1, k_chunk = K;
-  const long tiles = (long)n_tiles * (GROUPED ? (M + BM - 1) / BM : m_tiles);
-  if (!GROUPED && tiles < 160 && K >= 1024) {
-    splits = (int)std::min<long>(8, std::max<long>(1, 256 / tiles));
-    k_chunk = ((K / splits + kBK - 1) / kBK) * kBK;
-    splits = (K + k_chunk - 1) / k_chunk;
+struct Plan {
+  int BM, BN, splits, k_chunk, m_tiles;
+};
+
+static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {
+  Plan p{};
+  const int mrows = grouped ? rows_per_group : M;
+  if (mrows <= 64) { p.BM = 64; p.BN = 64; }
+  else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
+  else if (mrows <= 256) { p.BM = 256; p.BN = ((N + 127) / 128 >= 192) ? 128 : 64; }
+  else { p.BM = 256; p.BN = 128; }
+  const int n_tiles = (N + p.BN - 1) / p.BN;
+  const int real_m_tiles = (M + p.BM - 1) / p.BM;
+  p.m_tiles = grouped ? real_m_tiles + n_groups : real_m_tiles;
+  p.splits = 1;
+  p.k_chunk = K;
+  const long tiles = (long)n_tiles * real_m_tiles;
+  if (!grouped && tiles < 160 && K >= 1024) {
+    int s = (int)std::min<long>(8, std::max<long>(1, 320 / tiles));
+    int kc = ((K / s + kBK - 1) / kBK) * kBK;
+    p.splits = (K + kc - 1) / kc;
+    p.k_chunk = kc;
   }
-  const long need = splits > 1 ? (long)splits * M * N : 0;
-  if (query) return need;
-  if (need > ws_floats) { splits = 1; k_chunk = K; }  // no workspace: single pass
+  return p;
+}
+
+template <int EPI, bool GROUPED>
+static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_t* B, int ldb,
+                        uint16_t* C, int ldc, float* ws, int M, int N, int K, const int* offsets,
+                        int n_groups, hipStream_t st) {
 #define MLOP_GEMM(bm, bn, wm, wn)                                                                   \
-  run_cfg<bm, bn, wm, wn, EPI, GROUPED>(A, lda, B, ldb, C, ldc, ws, M, N, K, splits, k_chunk,      \
-                                        offsets, n_groups, m_tiles, st)
-  if (BM == 64) MLOP_GEMM(64, 64, 1, 4);
-  else if (BM == 128) MLOP_GEMM(128, 64, 2, 2);
-  else if (BN == 64) MLOP_GEMM(256, 64, 4, 1);
+  run_cfg<bm, bn, wm, wn, EPI, GROUPED>(A, lda, B, ldb, C, ldc, ws, M, N, K, p.splits, p.k_chunk,  \
+                                        offsets, n_groups, p.m_tiles, st)
+  if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4);
+  else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2);
+  else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2);
   else MLOP_GEMM(256, 128, 4, 2);
 #undef MLOP_GEMM
-  return need;
 }
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {
-  return epi == EPI_NONE
-             ? dispatch<EPI_NONE, false>(nullptr, 0, nullptr, 0, nullptr, 0, nullptr, 0, M, N, K,
-                                         nullptr, 0, 0, nullptr, true)
-             : dispatch<EPI_SILU_MUL, false>(nullptr, 0, nullptr, 0, nullptr, 0, nullptr, 0, M, N,
-                                             K, nullptr, 0, 0, nullptr, true);
+  (void)epi;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  return p.splits > 1 ? (long)p.splits * M * N : 0;
 }
 
 void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws,
                  long ws_floats, int M, int N, int K, int epi, hipStream_t st) {
   if (M == 0) return;
+  Plan p = plan(M, N, K, false, 0, 0);
+  if (p.splits > 1 && (long)p.splits * M * N > ws_floats) { p.splits = 1; p.k_chunk = K; }
   if (epi == EPI_NONE)
-    dispatch<EPI_NONE, false>((const uint16_t*)A, lda, (const uint16_t*)B, ldb, (uint16_t*)C, ldc,
-                              ws, ws_floats, M, N, K, nullptr, 0, 0, st, false);
+    launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, ldb, (uint16_t*)C,
+                                 ldc, ws, M, N, K, nullptr, 0, st);
   else
-    dispatch<EPI_SILU_MUL, false>((const uint16_t*)A, lda, (const uint16_t*)B, ldb, (uint16_t*)C,
-                                  ldc, ws, ws_floats, M, N, K, nullptr, 0, 0, st, false);
+    launch_plan<EPI_SILU_MUL, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, ldb,
+                                     (uint16_t*)C, ldc, ws, M, N, K, nullptr, 0, st);
+  if (p.splits > 1) {
+    const int outw = epi == EPI_NONE ? N : N / 2;
+    const long total = (long)M * (outw / 8);
+    const int g = (int)std::min<long>((total + 255) / 256, 4096);
+    if (epi == EPI_NONE)
+      splitk_reduce_kernel<EPI_NONE><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, p.splits);
+    else
+      splitk_reduce_kernel<EPI_SILU_MUL><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, p.splits);
+  }
+}
+
+// y = A.B^T; residual += y; out = rmsnorm(residual) * w.  Returns false (nothing
+// launched) when the shape does not take the split-K path: the caller then runs
+// gemm + add_rmsnorm.
+bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, void* residual,
+                             const void* w, float eps, float* ws, long ws_floats, int M, int N,
+                             int K, hipStream_t st) {
+  if (M == 0) return true;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
+  launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
+                               M, N, K, nullptr, 0, st);
+  const int nvec = N / 8;
+  int vpt = 1;
+  while (vpt < 8 && nvec / vpt > 512) vpt <<= 1;
+  const int threads = ((nvec / vpt + 63) / 64) * 64;
+  auto* o = (uint16_t*)out;
+  auto* r = (uint16_t*)residual;
+  auto* wv = (const uint16_t*)w;
+  switch (vpt) {
+    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
+    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
+    case 4: splitk_add_rmsnorm_kernel<4><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
+    default: splitk_add_rmsnorm_kernel<8><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
+  }
+  return true;
 }
 
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
                          int M, int N, int K, int max_rows, int epi, hipStream_t st) {
   if (M == 0) return;
+  const Plan p = plan(M, N, K, true, n_groups, max_rows);
   if (epi == EPI_NONE)
-    dispatch<EPI_NONE, true>((const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N,
-                             nullptr, 0, M, N, K, offsets, n_groups, max_rows, st, false);
+    launch_plan<EPI_NONE, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N,
+                                nullptr, M, N, K, offsets, n_groups, st);
   else
-    dispatch<EPI_SILU_MUL, true>((const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N / 2,
-                                 nullptr, 0, M, N, K, offsets, n_groups, max_rows, st, false);
+    launch_plan<EPI_SILU_MUL, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C,
+                                    N / 2, nullptr, M, N, K, offsets, n_groups, st);
 }
 
 }  // namespace mlop

@@ -26,6 +26,9 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
 long gemm_workspace_floats(int M, int N, int K, int epi);
 void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws,
                  long ws_floats, int M, int N, int K, int epi, hipStream_t st);
+bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, void* residual,
+                             const void* w, float eps, float* ws, long ws_floats, int M, int N,
+                             int K, hipStream_t st);
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
                          int M, int N, int K, int max_rows, int epi, hipStream_t st);
 void launch_moe_route(float* topw, int* topi, const void* logits, int T, int E, int k,

@@ -191,6 +191,26 @@ def test_gemm(gpu, M, N, K):
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (64, 4096, 14336), (256, 4096, 4096), (256, 4096, 14336)])
+def test_gemm_add_rmsnorm(gpu, M, N, K):
+    torch.manual_seed(K)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    res = torch.randn(M, N, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
+    y = (x.float() @ w.float().t()).to(bf)
+    exp_out, exp_res = ref.add_rmsnorm(y, res, nw, 1e-5)
+    for backend in ("mlop", "hipblaslt"):
+        ops.GEMM_BACKEND = backend
+        try:
+            r2 = res.clone()
+            out = ops.gemm_add_rmsnorm(x, w, r2, nw, 1e-5)
+        finally:
+            ops.GEMM_BACKEND = "auto"
+        close(r2, exp_res, atol=3e-2, rtol=2e-2)
+        close(out, exp_out, atol=5e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M,I,K", [(1, 14336, 4096), (37, 3584, 4096), (256, 14336, 4096), (900, 512, 256)])
 def test_gemm_silu_mul(gpu, M, I, K):
     torch.manual_seed(I)
