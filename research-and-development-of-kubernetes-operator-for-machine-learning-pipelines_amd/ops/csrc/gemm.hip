@@ -338,7 +338,14 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   const int mrows = grouped ? rows_per_group : M;
   if (mrows <= 64) { p.BM = 64; p.BN = 64; }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
-  else if (mrows <= 256) { p.BM = 256; p.BN = ((N + 127) / 128 >= 192) ? 128 : 64; }
+  else if (mrows <= 256) {
+    static const int bn_min_tiles = [] {
+      const char* e = getenv("MLOP_GEMM_BN128_MIN_TILES");
+      return e ? atoi(e) : 192;
+    }();
+    p.BM = 256;
+    p.BN = ((N + 127) / 128 >= bn_min_tiles) ? 128 : 64;
+  }
   else { p.BM = 256; p.BN = 128; }
   const int n_tiles = (N + p.BN - 1) / p.BN;
   const int real_m_tiles = (M + p.BM - 1) / p.BM;
@@ -346,8 +353,13 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.splits = 1;
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
+  // experiment knobs (microbench sweeps): MLOP_GEMM_SPLIT_TARGET = WGs aimed for when splitting
+  static const int split_target = [] {
+    const char* e = getenv("MLOP_GEMM_SPLIT_TARGET");
+    return e ? atoi(e) : 320;
+  }();
   if (!grouped && tiles < 160 && K >= 1024) {
-    int s = (int)std::min<long>(8, std::max<long>(1, 320 / tiles));
+    int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
     p.k_chunk = kc;

@@ -1,9 +1,10 @@
-"""GEMM microbench on the decode / prefill projection shapes of Llama-3-8B:
-hand-written MFMA GEMM (ops.gemm) vs torch.matmul (hipBLASLt).  One process,
-interleaved rounds (cdna_hip_programming.md §5.4 rule 24), random data."""
+"""GEMM microbench on the Llama-3-8B projection shapes: the hand-written MFMA
+GEMM (forced, ``ops.GEMM_BACKEND = "mlop"``) vs torch.matmul (hipBLASLt).
+One process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), random data.
+Env knobs of the C++ planner are swept by re-running with MLOP_GEMM_* set."""
 import json
-import sys
 import os
+import sys
 
 import torch
 
@@ -12,11 +13,12 @@ from mlopamd import ops  # noqa: E402
 
 ops.load()
 dev = torch.device("cuda")
+Ms = [int(m) for m in os.environ.get("BENCH_MS", "1,64,128,256,512,8192").split(",")]
 shapes = []
-for M in (1, 16, 64, 128, 256, 2048, 8192):
+for M in Ms:
     for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
                        ("down", 4096, 14336), ("lm_head", 128256, 4096)):
-        if name == "lm_head" and M > 256:
+        if name == "lm_head" and M > 512:
             continue
         shapes.append((name, M, N, K))
 
@@ -34,20 +36,26 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3  # us
 
 
-res = []
+def mlop(x, w, epi):
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        return ops.gemm(x, w, epi=epi)
+    finally:
+        ops.GEMM_BACKEND = "auto"
+
+
+tag = os.environ.get("BENCH_TAG", "")
 for name, M, N, K in shapes:
     x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     w = (0.02 * torch.randn(N, K, device=dev)).to(torch.bfloat16)
     epi = ops.EPI_SILU_MUL if name == "gate_up" else ops.EPI_NONE
     ts_m, ts_t = [], []
     for _ in range(3):
-        ts_m.append(timeit(lambda: ops.gemm(x, w, epi=epi)))
+        ts_m.append(timeit(lambda: mlop(x, w, epi)))
         ts_t.append(timeit(lambda: torch.matmul(x, w.t())))
     tm, tt = min(ts_m), min(ts_t)
     flops = 2 * M * N * K
     byts = 2 * (N * K + M * K + M * N)
-    r = dict(shape=name, M=M, N=N, K=K, mlop_us=round(tm, 1), hipblaslt_us=round(tt, 1),
-             mlop_tflops=round(flops / tm / 1e6, 1), mlop_tbps=round(byts / tm / 1e6, 2),
-             speedup=round(tt / tm, 2))
-    res.append(r)
-    print(json.dumps(r), flush=True)
+    print(json.dumps(dict(tag=tag, shape=name, M=M, N=N, K=K, mlop_us=round(tm, 1), hipblaslt_us=round(tt, 1),
+                          mlop_tflops=round(flops / tm / 1e6, 1), mlop_tbps=round(byts / tm / 1e6, 2),
+                          speedup=round(tt / tm, 2))), flush=True)
