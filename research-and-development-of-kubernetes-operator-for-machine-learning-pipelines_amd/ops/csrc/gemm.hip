@@ -61,7 +61,7 @@ template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, float* __restrict__ ws, int M, int N, int K, int k_chunk,
-    const int* __restrict__ offsets, int n_groups) {
+    const int* __restrict__ offsets, int n_groups, int n_tiles_x, int m_tiles_y, int n_splits) {
   constexpr int NW = WM * WN, T = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -74,11 +74,20 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const int n0 = blockIdx.x * BN;
-  int m0 = blockIdx.y * BM, m_end = M;
+  // XCD-aware remap (T1, bijective form): the 1-D grid is dealt round-robin over
+  // the 8 XCDs, so give each XCD a CONTIGUOUS range of logical tiles ordered
+  // (split, m-tile, n-tile): tiles sharing an A panel / K-chunk share an L2.
+  // Speed only — correctness never depends on placement.
+  const int G = gridDim.x, L = blockIdx.x;
+  const int q = G >> 3, rr = G & 7, xcd = L & 7, slot = L >> 3;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+  const int gx = n_tiles_x;
+  const int bx = lid % gx, by = (lid / gx) % m_tiles_y, bz = lid / (gx * m_tiles_y);
+  const int n0 = bx * BN;
+  int m0 = by * BM, m_end = M;
   const uint16_t* Bg = B;
   if constexpr (GROUPED) {
-    int t = blockIdx.y, e = 0;
+    int t = by, e = 0;
     for (; e < n_groups; ++e) {
       const int rows = offsets[e + 1] - offsets[e];
       const int tiles = (rows + BM - 1) / BM;
@@ -90,9 +99,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     m_end = offsets[e + 1];
     Bg = B + (size_t)e * N * ldb;
   }
-  const int kbeg = blockIdx.z * k_chunk;
+  const int kbeg = bz * k_chunk;
   const int kend = min(K, kbeg + k_chunk);
   const int nk = (kend - kbeg) / kBK;
+  const bool split = n_splits > 1;
 
   // per-lane source row / chunk of each piece this wave issues (k advances by kBK)
   const int prow = lane >> 3;                  // row inside the 8-row piece
@@ -156,9 +166,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
   }
 
   const int rows_here = min(BM, m_end - m0);
-  if (gridDim.z > 1) {
+  if (split) {
     // split-K: fp32 partial slab [kz][M][N] (plain stores; reduce kernel in the next launch)
-    float* P = ws + (size_t)blockIdx.z * M * N;
+    float* P = ws + (size_t)bz * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -325,8 +335,10 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  dim3 grid((N + BN - 1) / BN, m_tiles, splits);
-  kern<<<grid, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups);
+  const int gx = (N + BN - 1) / BN;
+  const int blocks = gx * m_tiles * splits;
+  kern<<<blocks, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups, gx,
+                               m_tiles, splits);
 }
 
 struct Plan {
