@@ -96,9 +96,8 @@ def main(argv=None):
         for _ in range(n):
             outs = engine.step()
             gen += len(outs)
-            for o in outs:
-                if o.finished:
-                    new_request(O)
+            for _ in outs.finished:
+                new_request(O)
         return gen
 
     run_steps(a.warmup)

@@ -134,6 +134,51 @@ class StepOutput:
     finish_reason: str | None = None
 
 
+class _ParamsList(list):
+    pass
+
+
+class _AllGreedy:
+    """Stands in for a list of greedy SamplingParams of any length."""
+
+    all_greedy = True
+
+    def __getitem__(self, k):
+        return self
+
+
+_ALL_GREEDY = _AllGreedy()
+
+
+class StepBatch:
+    """One step's outputs as arrays (no per-token Python objects on the hot path);
+    iterating yields ``StepOutput`` lazily."""
+
+    __slots__ = ("seq_ids", "tokens", "fin", "reasons")
+
+    def __init__(self, seq_ids, tokens, fin, reasons: dict):
+        self.seq_ids, self.tokens, self.fin, self.reasons = seq_ids, tokens, fin, reasons
+
+    @classmethod
+    def from_list(cls, outs: list):
+        return cls(np.array([o.seq_id for o in outs], dtype=np.int64),
+                   np.array([o.token for o in outs], dtype=np.int64),
+                   np.array([o.finished for o in outs], dtype=bool),
+                   {o.seq_id: o.finish_reason for o in outs if o.finished})
+
+    def __len__(self):
+        return len(self.seq_ids)
+
+    def __iter__(self):
+        for sid, tok, f in zip(self.seq_ids.tolist(), self.tokens.tolist(), self.fin.tolist()):
+            yield StepOutput(sid, tok, f, self.reasons.get(sid) if f else None)
+
+    @property
+    def finished(self) -> list:
+        return [StepOutput(int(self.seq_ids[i]), int(self.tokens[i]), True, self.reasons.get(int(self.seq_ids[i])))
+                for i in np.nonzero(self.fin)[0]]
+
+
 class Engine:
     def __init__(self, model, cfg: EngineConfig | None = None):
         self.model = model
@@ -161,6 +206,19 @@ class Engine:
                                 cfg.max_num_seqs + self.buckets[-1], self.max_blocks_per_seq,
                                 self.G, model.n_kv, self.max_model_len, self.device)
         self.free_rows = list(range(cfg.max_num_seqs - 1, -1, -1))
+        # struct-of-arrays state of running rows: the decode hot path is vectorised
+        R = cfg.max_num_seqs
+        self.r_len = np.zeros(R, np.int64)      # tokens in the sequence (prompt + output)
+        self.r_gen = np.zeros(R, np.int64)      # generated tokens
+        self.r_maxgen = np.zeros(R, np.int64)
+        self.r_last = np.zeros(R, np.int64)     # last token (next decode input)
+        self.r_ignore = np.zeros(R, bool)       # ignore_eos
+        self.r_hasstop = np.zeros(R, bool)      # has stop_token_ids (checked in Python)
+        self.r_nblk = np.zeros(R, np.int64)     # KV pages held
+        self.r_sid = np.zeros(R, np.int64)
+        self.r_random = np.zeros(R, bool)       # non-greedy sampling
+        self._rows = np.zeros(0, np.int32)
+        self._rows_dirty = True
         self.sampler = Sampler(self.device, cfg.seed)
         self.waiting: collections.deque[Sequence] = collections.deque()
         self.prefilling: list[Sequence] = []
@@ -238,6 +296,7 @@ class Engine:
         start = len(seq.blocks)
         seq.blocks.extend(new)
         self.meta.bt_h[seq.row, start:start + need] = new
+        self.r_nblk[seq.row] = len(seq.blocks)
         return True
 
     def _release(self, seq: Sequence):
@@ -245,9 +304,25 @@ class Engine:
             self.alloc.free(seq.blocks)
             seq.blocks = []
         if seq.row >= 0:
+            self.r_nblk[seq.row] = 0
             self.free_rows.append(seq.row)
             seq.row = -1
         seq.num_cached = 0
+        self._rows_dirty = True
+
+    def _params_of_running(self):
+        """Sampling params of the decode batch; a falsy ``any_random`` lets the sampler
+        take the all-greedy fast path without a per-sequence Python scan."""
+        lst = _ParamsList(s.params for s in self.running) if self.r_random[self._rows].any() else _ALL_GREEDY
+        return lst
+
+    def _register_running(self, s: Sequence):
+        r, p = s.row, s.params
+        self.r_random[r] = not p.greedy
+        self.r_len[r], self.r_gen[r], self.r_maxgen[r] = s.length, len(s.output), p.max_tokens
+        self.r_last[r] = s.output[-1] if s.output else s.prompt[-1]
+        self.r_ignore[r], self.r_hasstop[r], self.r_sid[r] = p.ignore_eos, bool(p.stop_token_ids), s.seq_id
+        self._rows_dirty = True
 
     def _finish(self, seq: Sequence, reason: str):
         seq.status = Status.FINISHED
@@ -336,48 +411,87 @@ class Engine:
                 self.prefilling.remove(s)
                 s.status = Status.RUNNING
                 self.running.append(s)
-                outs.append(self._append(s, tokens[ti]))
+                o = self._append(s, tokens[ti])
+                if not o.finished:
+                    self._register_running(s)
+                outs.append(o)
                 ti += 1
-        return outs
+        return StepBatch.from_list(outs)
 
     # ----------------------------------------------------------- decode --
     def _decode_step(self):
-        # every running seq needs a slot for its last token's KV
-        i = 0
-        while i < len(self.running):
-            s = self.running[i]
-            if self._ensure_blocks(s, s.length):
-                i += 1
-                continue
-            victim = self.running.pop()  # newest
-            self._preempt(victim)
-            if victim is s:
-                continue
-        B = len(self.running)
+        t0 = time.perf_counter()
+        # every running seq needs a KV slot for its last token: only rows crossing a
+        # page boundary allocate (vectorised test, Python only for those few rows)
+        while True:
+            if self._rows_dirty:
+                self._rows = np.fromiter((s.row for s in self.running), dtype=np.int32, count=len(self.running))
+                self._rows_dirty = False
+            rows = self._rows
+            ctx = self.r_len[rows]
+            need = np.nonzero((ctx + BLOCK_SIZE - 1) // BLOCK_SIZE > self.r_nblk[rows])[0]
+            ok = True
+            for i in need.tolist():
+                s = self.running[i]
+                if not self._ensure_blocks(s, s.length):
+                    self._preempt(self.running.pop())  # newest goes back to the queue
+                    ok = False
+                    break
+            if ok:
+                break
+        B = len(rows)
         if B == 0:
-            return []
-        rows = np.fromiter((s.row for s in self.running), dtype=np.int32, count=B)
-        ctx = np.fromiter((s.length for s in self.running), dtype=np.int32, count=B)
-        last = np.fromiter((s.output[-1] if s.output else s.prompt[-1] for s in self.running),
-                           dtype=np.int64, count=B)
+            return StepBatch.from_list([])
+        ctx = ctx.astype(np.int32)
+        last = self.r_last[rows]
         bucket = next((b for b in self.buckets if b >= B), None)
         g = self.graphs.get(bucket) if bucket is not None else None
         if g is not None:
             self.meta.fill_decode(rows, ctx, last, pad_to=bucket)
+            t1 = time.perf_counter()
             logits = self._launch(KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket)[:B]
             self.stats["graph_steps"] += 1
         else:
             self.meta.fill_decode(rows, ctx, last, pad_to=B)
             part, nparts = plan_partitions(B, self.model.n_kv, int(ctx.max()))
+            t1 = time.perf_counter()
             logits = self._launch(KIND_EAGER, B, B, B, part, nparts, 0)
             self.stats["eager_decode_steps"] += 1
-        tokens = self.sampler(logits, [s.params for s in self.running]).tolist()
+        toks = self.sampler(logits, self._params_of_running()).cpu().numpy().astype(np.int64)
+        t2 = time.perf_counter()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += B
-        outs = []
-        for s, t in zip(list(self.running), tokens):
-            s.num_cached = s.length
-            outs.append(self._append(s, t))
+        # vectorised bookkeeping
+        self.r_len[rows] += 1
+        self.r_gen[rows] += 1
+        self.r_last[rows] = toks
+        fin_len = (self.r_gen[rows] >= self.r_maxgen[rows]) | (self.r_len[rows] >= self.max_model_len)
+        fin_stop = (~self.r_ignore[rows]) & (toks == self.model.cfg.eos_token_id)
+        run = self.running
+        hs = np.nonzero(self.r_hasstop[rows])[0]
+        for i in hs.tolist():
+            if int(toks[i]) in run[i].params.stop_token_ids:
+                fin_stop[i] = True
+        fin = fin_stop | fin_len
+        for s, t in zip(run, toks.tolist()):
+            s.output.append(t)
+        sids = self.r_sid[rows].copy()
+        reasons = {}
+        fi = np.nonzero(fin)[0]
+        if len(fi):
+            done = [run[i] for i in fi.tolist()]
+            for i, s in zip(fi.tolist(), done):
+                reasons[s.seq_id] = "stop" if fin_stop[i] else "length"
+            dset = set(id(s) for s in done)
+            self.running = [s for s in run if id(s) not in dset]
+            for s in done:
+                self._finish(s, reasons[s.seq_id])
+        outs = StepBatch(sids, toks, fin, reasons)
+        t3 = time.perf_counter()
+        # host-side cost accounting (us): prep before launch, device (launch..tokens), bookkeeping
+        self.stats["decode_host_prep_us"] += int(1e6 * (t1 - t0))
+        self.stats["decode_device_us"] += int(1e6 * (t2 - t1))
+        self.stats["decode_host_post_us"] += int(1e6 * (t3 - t2))
         return outs
 
     def _append(self, s: Sequence, tok: int) -> StepOutput:
@@ -386,7 +500,7 @@ class Engine:
             s.first_token_time = time.perf_counter()
         p = s.params
         reason = None
-        if not p.ignore_eos and (tok == self.model.cfg.eos_token_id or tok in p.stop_token_ids):
+        if (not p.ignore_eos and tok == self.model.cfg.eos_token_id) or tok in p.stop_token_ids:
             reason = "stop"
         elif len(s.output) >= p.max_tokens:
             reason = "length"

@@ -72,7 +72,7 @@ class Sampler:
 
     def __call__(self, logits: torch.Tensor, params: list[SamplingParams]) -> torch.Tensor:
         n = logits.shape[0]
-        if all(p.greedy for p in params[:n]):
+        if getattr(params, "all_greedy", False) or all(p.greedy for p in params[:n]):
             return ops.argmax(logits) if logits.is_cuda else logits.argmax(-1)
         dev = logits.device
         temps = torch.tensor([p.temperature for p in params[:n]], dtype=torch.float32)
