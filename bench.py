@@ -41,7 +41,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--batch", type=int, default=256, help="concurrent requests per GPU")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="concurrent requests per GPU (288 GB HBM holds their 64 GB of KV pages)")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=2048)

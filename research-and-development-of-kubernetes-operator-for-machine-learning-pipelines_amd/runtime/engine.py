@@ -120,7 +120,7 @@ class EngineConfig:
     kv_cache_bytes: int | None = None
     gpu_memory_utilization: float = 0.90
     use_graphs: bool = True
-    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024)
     prefill_min_batch: int = 1
     max_decode_gap: int = 0
     seed: int = 0
