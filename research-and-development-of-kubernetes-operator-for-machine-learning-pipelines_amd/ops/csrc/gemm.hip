@@ -57,7 +57,7 @@ __device__ __forceinline__ float silu_bf(float g) {
   return bf2f(f2bf(gb / (1.f + __expf(-gb))));
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED>
+template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES = 3, bool SETPRIO = false>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, float* __restrict__ ws, int M, int N, int K, int k_chunk,
@@ -136,14 +136,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vmcnt<PPW>(); else wait_vmcnt<0>();
+    // stage kt must have landed; the STAGES-2 younger stages may stay in flight
+    if (STAGES == 3 && kt + 1 < nk) wait_vmcnt<PPW>(); else wait_vmcnt<0>();
     raw_barrier();  // stage kt visible to all waves; stage kt-1's buffer free
-    if (kt + 2 < nk) issue((kt + 2) % kStages, kt + 2);
-    const uint16_t* sA = smem + (kt % kStages) * STAGE;
+    if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
+    const uint16_t* sA = smem + (kt % STAGES) * STAGE;
     const uint16_t* sB = sA + BM * kBK;
+    if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ch = kk * 4 + (lane >> 4);
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
+    if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   const int rows_here = min(BM, m_end - m0);
@@ -183,43 +187,51 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     return;
   }
   raw_barrier();  // every wave is done reading the ring before it becomes the C tile
+  // the C tile goes through LDS in column chunks of <= 128 (fp32 [BM][EW + 4])
   float* sC = reinterpret_cast<float*>(smem);
-  constexpr int LDC = BN + 4;
+  constexpr int EW = BN < 128 ? BN : 128;
+  constexpr int LDC = EW + 4;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int c0 = 0; c0 < BN; c0 += EW) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = wn * WTN + j * 16 + (lane & 15);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sC[(wm * WTM + i * 16 + 4 * (lane >> 4) + r) * LDC + n] = acc[i][j][r];
+      for (int j = 0; j < TN; ++j) {
+        const int n = wn * WTN + j * 16 + (lane & 15) - c0;
+        if (n >= 0 && n < EW) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sC[(wm * WTM + i * 16 + 4 * (lane >> 4) + r) * LDC + n] = acc[i][j][r];
+        }
+      }
+    __syncthreads();
+    if constexpr (EPI == EPI_NONE) {
+      constexpr int VPR = EW / 8;
+      for (int v = tid; v < BM * VPR; v += T) {
+        const int r = v / VPR, c = (v % VPR) * 8;
+        if (r >= rows_here || n0 + c0 + c >= N) continue;
+        const float* s = sC + r * LDC + c;
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack2(s[2 * j], s[2 * j + 1]);
+        *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + n0 + c0 + c) = o;
+      }
+    } else {
+      constexpr int OUTW = EW / 2, VPR = OUTW / 8;
+      for (int v = tid; v < BM * VPR; v += T) {
+        const int r = v / VPR, j0 = (v % VPR) * 8;
+        const int gcol = (j0 / 16) * 32 + (j0 % 16);
+        if (r >= rows_here || n0 + c0 + gcol >= N) continue;
+        const float* g = sC + r * LDC + gcol;
+        const float* u = g + 16;
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = pack2(silu_bf(g[2 * j]) * bf2f(f2bf(u[2 * j])),
+                       silu_bf(g[2 * j + 1]) * bf2f(f2bf(u[2 * j + 1])));
+        *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + (n0 + c0) / 2 + j0) = o;
+      }
     }
-  __syncthreads();
-  if constexpr (EPI == EPI_NONE) {
-    constexpr int VPR = BN / 8;
-    for (int v = tid; v < BM * VPR; v += T) {
-      const int r = v / VPR, c = (v % VPR) * 8;
-      if (r >= rows_here || n0 + c >= N) continue;
-      const float* s = sC + r * LDC + c;
-      u32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = pack2(s[2 * j], s[2 * j + 1]);
-      *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + n0 + c) = o;
-    }
-  } else {
-    constexpr int OUTW = BN / 2, VPR = OUTW / 8;
-    for (int v = tid; v < BM * VPR; v += T) {
-      const int r = v / VPR, j0 = (v % VPR) * 8;
-      const int gcol = (j0 / 16) * 32 + (j0 % 16);
-      if (r >= rows_here || n0 + gcol >= N) continue;
-      const float* g = sC + r * LDC + gcol;
-      const float* u = g + 16;
-      u32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = pack2(silu_bf(g[2 * j]) * bf2f(f2bf(u[2 * j])),
-                     silu_bf(g[2 * j + 1]) * bf2f(f2bf(u[2 * j + 1])));
-      *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + n0 / 2 + j0) = o;
-    }
+    if (c0 + EW < BN) __syncthreads();
   }
 }
 
@@ -315,21 +327,22 @@ __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int STAGES>
 constexpr size_t lds_bytes() {
-  constexpr size_t ring = (size_t)kStages * (BM + BN) * kBK * 2;
-  constexpr size_t epi = (size_t)BM * (BN + 4) * 4;
+  constexpr size_t ring = (size_t)STAGES * (BM + BN) * kBK * 2;
+  constexpr int EW = BN < 128 ? BN : 128;
+  constexpr size_t epi = (size_t)BM * (EW + 4) * 4;
   return ring > epi ? ring : epi;
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED>
+template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES, bool SETPRIO>
 static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc,
                     float* ws, int M, int N, int K, int splits, int k_chunk, const int* offsets,
                     int n_groups, int m_tiles, hipStream_t st) {
   constexpr int T = WM * WN * 64;
-  constexpr size_t lds = lds_bytes<BM, BN, WM, WN>();
+  constexpr size_t lds = lds_bytes<BM, BN, STAGES>();
   static_assert(lds <= 163840, "LDS budget");
-  auto kern = gemm_kernel<BM, BN, WM, WN, EPI, GROUPED>;
+  auto kern = gemm_kernel<BM, BN, WM, WN, EPI, GROUPED, STAGES, SETPRIO>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -342,34 +355,43 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
 }
 
 struct Plan {
-  int BM, BN, splits, k_chunk, m_tiles;
+  int BM, BN, splits, k_chunk, m_tiles, variant;
 };
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Tile choice by the (per-group) row count:
+//   M <= 64 / 128: narrow tiles, many WGs (weight streaming);  M <= 256: the whole
+//   batch in one tile (weights read once), BN by how many N tiles fill the chip;
+//   large M: variant 0 = 256x128 (3-stage ring), 1 = 256x256 (2-stage, 128x64 per
+//   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs.
 static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {
   Plan p{};
+  p.variant = 0;
   const int mrows = grouped ? rows_per_group : M;
   if (mrows <= 64) { p.BM = 64; p.BN = 64; }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
   else if (mrows <= 256) {
-    static const int bn_min_tiles = [] {
-      const char* e = getenv("MLOP_GEMM_BN128_MIN_TILES");
-      return e ? atoi(e) : 192;
-    }();
+    static const int bn_min_tiles = env_int("MLOP_GEMM_BN128_MIN_TILES", 192);
     p.BM = 256;
     p.BN = ((N + 127) / 128 >= bn_min_tiles) ? 128 : 64;
+  } else {
+    static const int big = env_int("MLOP_GEMM_BIG_VARIANT", 0);
+    static const int big_min_m = env_int("MLOP_GEMM_BIG_MIN_M", 1024);
+    p.BM = 256;
+    p.BN = 128;
+    if (big && mrows >= big_min_m && !grouped) { p.BN = 256; p.variant = big; }
   }
-  else { p.BM = 256; p.BN = 128; }
   const int n_tiles = (N + p.BN - 1) / p.BN;
   const int real_m_tiles = (M + p.BM - 1) / p.BM;
   p.m_tiles = grouped ? real_m_tiles + n_groups : real_m_tiles;
   p.splits = 1;
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
-  // experiment knobs (microbench sweeps): MLOP_GEMM_SPLIT_TARGET = WGs aimed for when splitting
-  static const int split_target = [] {
-    const char* e = getenv("MLOP_GEMM_SPLIT_TARGET");
-    return e ? atoi(e) : 320;
-  }();
+  static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 320);
   if (!grouped && tiles < 160 && K >= 1024) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
@@ -383,13 +405,16 @@ template <int EPI, bool GROUPED>
 static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                         uint16_t* C, int ldc, float* ws, int M, int N, int K, const int* offsets,
                         int n_groups, hipStream_t st) {
-#define MLOP_GEMM(bm, bn, wm, wn)                                                                   \
-  run_cfg<bm, bn, wm, wn, EPI, GROUPED>(A, lda, B, ldb, C, ldc, ws, M, N, K, p.splits, p.k_chunk,  \
-                                        offsets, n_groups, p.m_tiles, st)
-  if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4);
-  else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2);
-  else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2);
-  else MLOP_GEMM(256, 128, 4, 2);
+#define MLOP_GEMM(bm, bn, wm, wn, stages, prio)                                                   \
+  run_cfg<bm, bn, wm, wn, EPI, GROUPED, stages, prio>(A, lda, B, ldb, C, ldc, ws, M, N, K,        \
+                                                      p.splits, p.k_chunk, offsets, n_groups,     \
+                                                      p.m_tiles, st)
+  if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
+  else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
+  else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
+  else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
+  else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
+  else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
 #undef MLOP_GEMM
 }
 
