@@ -12,8 +12,8 @@
 //     steady state) — __syncthreads() would drain the DMA queue (its fence emits
 //     vmcnt(0));
 //   * the LDS image is lane-linear per 1 KiB piece (8 rows x 128 B), XOR-swizzled
-//     through the SOURCE address: 16-B chunk c of row r sits at slot c ^ (r & 7),
-//     so the 16 rows a ds_read_b128 lane group reads hit 8 different bank slots
+//     through the SOURCE address: 16-B chunk c of row r sits at slot c ^ ((r>>1)&7),
+//     so the 16 rows a ds_read_b128 lane group reads hit 16 different bank slots
 //     (T2, rule 21: swizzle the source and the read, never the LDS destination);
 //   * all LDS lives in ONE extern __shared__ array (a second object can make hipcc
 //     emit vmcnt(0) before every ds_read: §5 item 4(a));
@@ -46,6 +46,11 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+
+// 16-B slot of chunk c in image row r is c ^ swz(r).  Two 128-B rows share one
+// 256-B bank row, so (r>>1)&7 (not r&7) makes the 16 rows of a ds_read_b128 lane
+// group land on 16 distinct slots: (r&1) picks the half, swz the slot in it.
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -106,12 +111,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 
   // per-lane source row / chunk of each piece this wave issues (k advances by kBK)
   const int prow = lane >> 3;                  // row inside the 8-row piece
-  const int pchunk = (lane & 7) ^ prow;        // source chunk for LDS slot (lane & 7)
   const uint16_t* src[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int p = wid + i * NW;
     const int r = p * 8 + prow;
+    const int pchunk = (lane & 7) ^ swz(r);     // source chunk for LDS slot (lane & 7)
     if (r < BM) {
       const int gr = min(m0 + r, m_end - 1);
       src[i] = A + (size_t)gr * lda + kbeg + pchunk * 8;
@@ -154,12 +159,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WTM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(sA + r * kBK + ((ch ^ (r & 7)) << 3));
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + r * kBK + ((ch ^ swz(r)) << 3));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WTN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + r * kBK + ((ch ^ (r & 7)) << 3));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + r * kBK + ((ch ^ swz(r)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
