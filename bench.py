@@ -47,9 +47,12 @@ def parse(argv=None):
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
-    ap.add_argument("--prefill-min-batch", type=int, default=16)
+    ap.add_argument("--prefill-min-batch", type=int, default=4)
     ap.add_argument("--max-decode-gap", type=int, default=24)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-mixed", action="store_true",
+                    help="separate prefill steps instead of prompt chunks riding in the decode step")
+    ap.add_argument("--mixed-min-chunk", type=int, default=64)
     ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
@@ -76,7 +79,7 @@ def main(argv=None):
         engine_kwargs=dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
                            max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
                            prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
-                           ))
+                           mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk))
     from mlopamd.runtime.sampler import SamplingParams
 
     rng = np.random.default_rng(1234 + rank)
@@ -84,7 +87,8 @@ def main(argv=None):
     P, O = a.prompt_len, a.output_len
 
     def new_request(max_tokens):
-        prompt = rng.integers(1000, V - 1000, size=P).tolist()
+        lo = min(1000, V // 4)
+        prompt = rng.integers(lo, V - lo, size=P).tolist()
         engine.add_request(prompt, SamplingParams(max_tokens=int(max_tokens), temperature=a.temperature,
                                                   top_k=50 if a.temperature > 0 else 0, ignore_eos=True))
 
@@ -144,9 +148,10 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random prompt tokens, random-init weights)",
-            "config": {"model": "Llama-3-8B", "global_batch": a.batch * world, "seq_len": P + O,
+            "config": {"model": "Llama-3-8B" if a.model == "llama3-8b" else a.model, "global_batch": a.batch * world, "seq_len": P + O,
                        "prompt_len": P, "output_len": O, "parallelism": f"dp{world}",
-                       "graphs": not a.no_graphs},
+                       "graphs": not a.no_graphs, "mixed_prefill": not a.no_mixed,
+                       "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap},
             "p50_cr_ready_s": round(p50_ready, 3),
             "served_tokens_per_sec_per_gpu": round(value / world, 2),
             "prefill_tokens_per_sec": round(total_prefill / max_t, 2),

@@ -88,6 +88,7 @@ class ModelSpec:
     replicas: int = 1
     max_model_len: int | None = None
     max_num_seqs: int | None = None
+    kv_target_fraction: float | None = None
     canary: CanaryPolicy = field(default_factory=CanaryPolicy)
 
     @classmethod
@@ -101,6 +102,7 @@ class ModelSpec:
                    expert_parallel=spec.get("expertParallel"),
                    replicas=int(spec.get("replicas", 1)),
                    max_model_len=spec.get("maxModelLen"), max_num_seqs=spec.get("maxNumSeqs"),
+                   kv_target_fraction=spec.get("kvTargetFraction"),
                    canary=CanaryPolicy.from_spec(spec))
 
     def validate(self) -> list[str]:

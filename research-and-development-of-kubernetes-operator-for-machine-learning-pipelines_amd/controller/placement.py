@@ -4,7 +4,10 @@ Inputs: the model architecture (weights, KV bytes per token), the serving
 targets (max concurrent sequences x max context), and the node (HBM per GPU,
 GPUs per node).  Output: tensor-parallel / expert-parallel degree, GPUs to
 request (``amd.com/gpu``), per-GPU weight and KV budgets and the resulting KV
-token capacity.  Policy: the smallest power-of-two TP (dividing the head
+token capacity.  The KV target is ``kv_target_fraction`` (default 0.5: the mean context of a
+uniformly-aged batch) of max_num_seqs x max_model_len — the engine preempts
+(recompute) on the rare tail instead of every replica paying for the worst
+case.  Policy: the smallest power-of-two TP (dividing the head
 counts) that fits weights + activation reserve + the KV target in
 ``utilization x HBM`` — bigger shards and fewer ranks mean fewer, larger
 collectives over the point-to-point xGMI links.  An explicit TP request
@@ -43,7 +46,7 @@ def _valid_tp(cfg: ModelConfig, tp: int) -> bool:
 def plan(arch: str | ModelConfig, max_model_len: int = 4096, max_num_seqs: int = 256,
          hbm_gb: float = 288.0, gpus_per_node: int = 8, utilization: float = 0.90,
          reserve_gb: float = 8.0, requested_tp: int | None = None, requested_ep: int | None = None,
-         kv_target_fraction: float = 1.0) -> Placement:
+         kv_target_fraction: float = 0.5) -> Placement:
     cfg = arch if isinstance(arch, ModelConfig) else get_config(arch)
     usable = hbm_gb * utilization
     wbytes = cfg.weight_bytes()

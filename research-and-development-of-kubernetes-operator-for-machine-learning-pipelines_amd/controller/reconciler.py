@@ -122,7 +122,8 @@ class MlflowModelReconciler:
             if runtime == seldon.RUNTIME_LLM and arch:
                 p = plan(arch, max_model_len=spec.max_model_len or 4096, max_num_seqs=spec.max_num_seqs or 256,
                          hbm_gb=self.settings.hbm_per_gpu_gb, gpus_per_node=self.settings.gpus_per_node,
-                         requested_tp=spec.tensor_parallel, requested_ep=spec.expert_parallel)
+                         requested_tp=spec.tensor_parallel, requested_ep=spec.expert_parallel,
+                         kv_target_fraction=spec.kv_target_fraction or 0.5)
                 placement = {"tensorParallel": p.tensorParallel, "expertParallel": p.expertParallel,
                              "gpus": p.gpus, "weightGBPerGPU": p.weightGBPerGPU,
                              "kvTokenCapacity": p.kvTokenCapacity, "fits": p.fits}

@@ -127,12 +127,22 @@ class MetaBuffers:
         token_ids_per_seq[i]: the q_len input ids. Block tables must already
         hold the pages covering ctx_lens.  want_logits[i] (default all): emit a
         logits row for sequence i's last token.  Returns (T, num_tiles, n_logits)."""
-        nl = 0
+        return self._fill_ragged(0, 0, 0, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits)
+
+    def fill_mixed(self, d_rows: np.ndarray, d_ctx: np.ndarray, d_last: np.ndarray,
+                   rows, q_lens, ctx_lens, token_ids_per_seq, want_logits=None):
+        """One step that decodes ``d_rows`` (one token each, vectorised, first B
+        tokens / tiles / logits) and prefills chunks of other sequences after
+        them (Sarathi-style mixed batch: the decode rows ride in the prefill's
+        GEMMs).  Returns (T, num_tiles, n_logits)."""
+        B = len(d_rows)
+        self.fill_decode(d_rows, d_ctx, d_last, pad_to=B)
+        return self._fill_ragged(B, B, B, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits)
+
+    def _fill_ragged(self, t, nt, nl, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits):
         pos_h, slot_h = self.view_h("positions"), self.view_h("slots")
         ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
         qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")
-        t = 0
-        nt = 0
         qt = self.qt
         for i, row in enumerate(rows):
             ql, cl = int(q_lens[i]), int(ctx_lens[i])

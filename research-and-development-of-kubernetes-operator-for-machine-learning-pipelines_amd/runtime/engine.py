@@ -11,9 +11,13 @@ Step policy:
     hipGraph captured for the smallest batch bucket >= B (padded rows attend to
     nothing), so a decode step costs one graph launch + one metadata H2D + one
     token D2H;
-  * a prefill step is taken when requests wait and either nothing is decoding,
+  * prompt work is scheduled when requests wait and either nothing is decoding,
     enough requests are queued (``prefill_min_batch``) or the oldest has waited
     ``max_decode_gap`` decode steps (bounded TTFT without fragmenting decode);
+    while sequences decode it runs as a MIXED step (``mixed_prefill``): every
+    running row's decode token plus prompt chunks up to the token budget in one
+    eager ragged forward, so decode rides in the prefill's larger-M GEMMs
+    instead of stalling behind a separate prefill pass;
   * KV pages come from a free-list; on exhaustion the newest running sequence
     is preempted (pages freed, recomputed later).
 """
@@ -123,6 +127,8 @@ class EngineConfig:
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024)
     prefill_min_batch: int = 1
     max_decode_gap: int = 0
+    mixed_prefill: bool = True    # prefill chunks ride in the decode step (one forward)
+    mixed_min_chunk: int = 64     # below this many free token slots, decode alone
     seed: int = 0
 
 
@@ -350,7 +356,10 @@ class Engine:
 
     def step(self) -> list[StepOutput]:
         if self._want_prefill():
-            out = self._prefill_step()
+            if self.running and self.cfg.mixed_prefill:
+                out = self._mixed_step()
+            else:
+                out = self._prefill_step()
             if out is not None:
                 self._decode_since_prefill = 0
                 return out
@@ -360,8 +369,9 @@ class Engine:
         return []
 
     # ---------------------------------------------------------- prefill --
-    def _prefill_step(self):
-        budget = self.cfg.max_num_batched_tokens
+    def _collect_prefill(self, budget: int):
+        """Admit prompt chunks up to ``budget`` tokens: continuing chunked
+        prefills first, then waiting requests (each needs a free row + pages)."""
         batch, chunks = [], []
         for seq in list(self.prefilling):
             if budget <= 0:
@@ -386,6 +396,26 @@ class Engine:
             batch.append(seq)
             chunks.append(n)
             budget -= n
+        return batch, chunks
+
+    def _prefill_finish(self, batch, ctx, done, tokens) -> list:
+        outs = []
+        ti = 0
+        for s, c, d in zip(batch, ctx, done):
+            s.num_cached = c
+            if d:
+                self.prefilling.remove(s)
+                s.status = Status.RUNNING
+                self.running.append(s)
+                o = self._append(s, tokens[ti])
+                if not o.finished:
+                    self._register_running(s)
+                outs.append(o)
+                ti += 1
+        return outs
+
+    def _prefill_step(self):
+        batch, chunks = self._collect_prefill(self.cfg.max_num_batched_tokens)
         if not batch:
             return None
         rows = [s.row for s in batch]
@@ -403,26 +433,61 @@ class Engine:
             torch.cuda.synchronize() if self.device.type == "cuda" else None
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
-        outs = []
-        ti = 0
-        for s, c, d in zip(batch, ctx, done):
-            s.num_cached = c
-            if d:
-                self.prefilling.remove(s)
-                s.status = Status.RUNNING
-                self.running.append(s)
-                o = self._append(s, tokens[ti])
-                if not o.finished:
-                    self._register_running(s)
-                outs.append(o)
-                ti += 1
-        return StepBatch.from_list(outs)
+        return StepBatch.from_list(self._prefill_finish(batch, ctx, done, tokens))
+
+    # ------------------------------------------------------------ mixed --
+    def _mixed_step(self):
+        """Decode every running sequence AND prefill prompt chunks in ONE eager
+        forward (chunked-prefill piggybacking): the decode rows share the
+        prefill's weight reads and its larger-M GEMMs instead of paying a
+        separate M=B pass; the ragged paged-attention kernel takes both kinds
+        of tile.  Returns None (caller decodes alone) when nothing fits."""
+        t0 = time.perf_counter()
+        rows, ctx_d = self._decode_rows()
+        B = len(rows)
+        budget = self.cfg.max_num_batched_tokens - B
+        if B == 0 or budget < self.cfg.mixed_min_chunk:
+            return None
+        batch, chunks = self._collect_prefill(budget)
+        if not batch:
+            return None
+        p_rows = [s.row for s in batch]
+        p_ctx = [s.num_cached + n for s, n in zip(batch, chunks)]
+        p_toks = [s.tokens(s.num_cached, c) for s, c in zip(batch, p_ctx)]
+        done = [c == s.length for s, c in zip(batch, p_ctx)]
+        T, nt, nl = self.meta.fill_mixed(rows, ctx_d.astype(np.int32), self.r_last[rows],
+                                         p_rows, chunks, p_ctx, p_toks, want_logits=done)
+        part, nparts = plan_partitions(nt, self.model.n_kv, max(int(ctx_d.max()), max(p_ctx)))
+        t1 = time.perf_counter()
+        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0)
+        done_seqs = [s for s, d in zip(batch, done) if d]
+        dparams = self._params_of_running()
+        if getattr(dparams, "all_greedy", False) and all(s.params.greedy for s in done_seqs):
+            params = _ALL_GREEDY
+        else:
+            params = _ParamsList([s.params for s in self.running] + [s.params for s in done_seqs])
+        toks = self.sampler(logits, params).cpu().numpy().astype(np.int64)
+        t2 = time.perf_counter()
+        self.stats["mixed_steps"] += 1
+        self.stats["decode_tokens"] += B
+        self.stats["prefill_tokens"] += T - B
+        d_out = self._decode_finish(rows, toks[:B])
+        p_out = self._prefill_finish(batch, p_ctx, done, toks[B:].tolist())
+        self.stats["mixed_host_us"] += int(1e6 * (t1 - t0 + time.perf_counter() - t2))
+        self.stats["mixed_device_us"] += int(1e6 * (t2 - t1))
+        if not p_out:
+            return d_out
+        p = StepBatch.from_list(p_out)
+        reasons = dict(d_out.reasons)
+        reasons.update(p.reasons)
+        return StepBatch(np.concatenate([d_out.seq_ids, p.seq_ids]), np.concatenate([d_out.tokens, p.tokens]),
+                         np.concatenate([d_out.fin, p.fin]), reasons)
 
     # ----------------------------------------------------------- decode --
-    def _decode_step(self):
-        t0 = time.perf_counter()
-        # every running seq needs a KV slot for its last token: only rows crossing a
-        # page boundary allocate (vectorised test, Python only for those few rows)
+    def _decode_rows(self):
+        """Rows of the running batch with a KV slot for their next token: only rows
+        crossing a page boundary allocate (vectorised test, Python only for those
+        few); on exhaustion the newest sequence is preempted."""
         while True:
             if self._rows_dirty:
                 self._rows = np.fromiter((s.row for s in self.running), dtype=np.int32, count=len(self.running))
@@ -438,7 +503,11 @@ class Engine:
                     ok = False
                     break
             if ok:
-                break
+                return rows, ctx
+
+    def _decode_step(self):
+        t0 = time.perf_counter()
+        rows, ctx = self._decode_rows()
         B = len(rows)
         if B == 0:
             return StepBatch.from_list([])
@@ -461,7 +530,16 @@ class Engine:
         t2 = time.perf_counter()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += B
-        # vectorised bookkeeping
+        outs = self._decode_finish(rows, toks)
+        t3 = time.perf_counter()
+        # host-side cost accounting (us): prep before launch, device (launch..tokens), bookkeeping
+        self.stats["decode_host_prep_us"] += int(1e6 * (t1 - t0))
+        self.stats["decode_device_us"] += int(1e6 * (t2 - t1))
+        self.stats["decode_host_post_us"] += int(1e6 * (t3 - t2))
+        return outs
+
+    def _decode_finish(self, rows, toks) -> StepBatch:
+        """Vectorised bookkeeping of one decode token per running row."""
         self.r_len[rows] += 1
         self.r_gen[rows] += 1
         self.r_last[rows] = toks
@@ -484,15 +562,10 @@ class Engine:
                 reasons[s.seq_id] = "stop" if fin_stop[i] else "length"
             dset = set(id(s) for s in done)
             self.running = [s for s in run if id(s) not in dset]
+            self._rows_dirty = True
             for s in done:
                 self._finish(s, reasons[s.seq_id])
-        outs = StepBatch(sids, toks, fin, reasons)
-        t3 = time.perf_counter()
-        # host-side cost accounting (us): prep before launch, device (launch..tokens), bookkeeping
-        self.stats["decode_host_prep_us"] += int(1e6 * (t1 - t0))
-        self.stats["decode_device_us"] += int(1e6 * (t2 - t1))
-        self.stats["decode_host_post_us"] += int(1e6 * (t3 - t2))
-        return outs
+        return StepBatch(sids, toks, fin, reasons)
 
     def _append(self, s: Sequence, tok: int) -> StepOutput:
         s.output.append(int(tok))

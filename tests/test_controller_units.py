@@ -175,12 +175,20 @@ def test_placement_8b_fits_one_gpu():
 def test_placement_70b():
     p = placement.plan("llama3-70b", 8192, 16)
     assert p.fits and p.tensorParallel == 1  # 141 GB + 43 GB KV fits one 288 GB GPU
-    assert placement.plan("llama3-70b", 8192, 64).tensorParallel == 2  # 171 GB KV target does not
+    # worst-case KV (fraction 1.0): 171 GB for 64 x 8192 does not fit beside 141 GB of weights
+    assert placement.plan("llama3-70b", 8192, 64, kv_target_fraction=1.0).tensorParallel == 2
+    assert placement.plan("llama3-70b", 8192, 128).tensorParallel == 2  # mean-context target, 171 GB
     big = placement.plan("llama3-70b", 8192, 512)
     assert big.tensorParallel >= 2 and big.fits
     p8 = placement.plan("llama3-70b", 8192, 128, requested_tp=8)
     assert p8.tensorParallel == 8 and p8.gpus == 8 and p8.weightGBPerGPU < 18 and p8.fits
     assert not placement.plan("llama3-70b", requested_tp=3).fits
+
+
+def test_placement_bench_config_is_one_gpu():
+    """The headline bench (1024 concurrent x 2048 max len) is one 288 GB GPU per replica."""
+    p = placement.plan("llama3-8b", 2048, 1024)
+    assert p.tensorParallel == 1 and p.fits and p.kvTokenCapacity >= 1024 * 1024
 
 
 def test_placement_mixtral_ep():

@@ -41,6 +41,41 @@ def test_generate_matches_dense_with_chunking(tiny):
     assert eng.alloc.num_free == eng.alloc.num_blocks - 1  # everything released
 
 
+@pytest.mark.parametrize("mixed", [True, False])
+def test_mixed_prefill_decode_steps(tiny, mixed):
+    """Requests arriving while others decode: with mixing, their prompt chunks
+    ride in the decode step (one ragged forward); outputs stay exact."""
+    eng = Engine(tiny, EngineConfig(max_num_seqs=8, max_num_batched_tokens=48, max_model_len=256,
+                                    num_kv_blocks=96, use_graphs=False, mixed_prefill=mixed,
+                                    mixed_min_chunk=8))
+    prompts = [torch.randint(2, 500, (n,)).tolist() for n in (7, 40, 12, 65, 3)]
+    seqs = [eng.add_request(prompts[0], SamplingParams(max_tokens=12, ignore_eos=True))]
+    for p in prompts[1:]:
+        eng.step()
+        eng.step()
+        seqs.append(eng.add_request(p, SamplingParams(max_tokens=12, ignore_eos=True)))
+    while eng.has_work():
+        eng.step()
+    for p, s in zip(prompts, seqs):
+        assert s.output == greedy_ref(tiny, p, 12)
+    assert (eng.stats["mixed_steps"] > 0) == mixed
+    assert eng.alloc.num_free == eng.alloc.num_blocks - 1
+
+
+def test_mixed_step_sampling_params(tiny):
+    """A mixed step with non-greedy decode rows and a greedy prefill completes
+    through the general sampler path."""
+    eng = Engine(tiny, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, max_model_len=128,
+                                    num_kv_blocks=48, use_graphs=False, mixed_min_chunk=8))
+    a = eng.add_request([5, 6, 7, 8], SamplingParams(max_tokens=6, temperature=0.8, top_k=5, ignore_eos=True))
+    eng.step()
+    b = eng.add_request(list(range(10, 30)), SamplingParams(max_tokens=4, ignore_eos=True))
+    while eng.has_work():
+        eng.step()
+    assert eng.stats["mixed_steps"] >= 1
+    assert len(a.output) == 6 and b.output == greedy_ref(tiny, list(range(10, 30)), 4)
+
+
 def test_preemption_recompute(tiny):
     # 12 usable pages: two 60-token sequences cannot both grow to 100 tokens
     eng = Engine(tiny, EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, max_model_len=256,

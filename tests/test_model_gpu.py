@@ -48,3 +48,24 @@ def test_llama3_8b_layer_shapes_decode(gpu):
     assert all(len(o) == 4 for o in outs)
     assert eng.stats["graph_steps"] >= 3
     _check_greedy(model, prompts[:3], [o[:2] for o in outs[:3]], tol=0.1)
+
+
+@pytest.mark.parametrize("mixed", [True, False])
+def test_engine_staggered_arrivals(gpu, mixed):
+    """Requests arriving while others decode (the serving pattern): with mixing
+    their prompt chunks share the decode step's forward (ragged attention over
+    decode + prefill tiles); greedy outputs match the dense oracle either way."""
+    torch.manual_seed(0)
+    model = build_model(TINY_LLAMA, device=gpu, seed=5)
+    eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=96, max_model_len=512,
+                                     num_kv_blocks=128, graph_buckets=(1, 2, 4, 8), mixed_prefill=mixed,
+                                     mixed_min_chunk=8))
+    prompts = [torch.randint(2, 500, (n,)).tolist() for n in (9, 70, 21, 150, 4, 33)]
+    seqs = [eng.add_request(prompts[0], SamplingParams(max_tokens=12, ignore_eos=True))]
+    for p in prompts[1:]:
+        eng.step()
+        seqs.append(eng.add_request(p, SamplingParams(max_tokens=12, ignore_eos=True)))
+    while eng.has_work():
+        eng.step()
+    assert (eng.stats["mixed_steps"] > 0) == mixed
+    _check_greedy(model, prompts, [s.output for s in seqs])
