@@ -55,6 +55,10 @@ class CanaryPolicy:
     latency_floor_s: float = 0.0    # latencies below this always pass (0 = reference)
     window_s: int = 60              # PromQL range (mlflow_operator.py:363)
     ready_timeout_s: float = 1800.0  # wait for the new predictor's readiness before gating
+    # GPU-side guards {metric: max new/old ratio} over prometheus.gpu_guard_queries;
+    # skipped for predictors that do not export the series (reference runtimes)
+    gpu_guards: dict = field(default_factory=lambda: {
+        "tpot_avg": 1.10, "gpu_memory_used": 1.30, "gpu_power": 1.25})
 
     @classmethod
     def from_spec(cls, spec: dict) -> "CanaryPolicy":
@@ -72,7 +76,8 @@ class CanaryPolicy:
                    error_rate_floor=float(c.get("errorRateFloor", base.error_rate_floor)),
                    latency_floor_s=float(c.get("latencyFloorSeconds", base.latency_floor_s)),
                    window_s=int(c.get("windowSeconds", base.window_s)),
-                   ready_timeout_s=float(c.get("readyTimeoutSeconds", base.ready_timeout_s)))
+                   ready_timeout_s=float(c.get("readyTimeoutSeconds", base.ready_timeout_s)),
+                   gpu_guards=dict(base.gpu_guards if c.get("gpuGuards") is None else c["gpuGuards"]))
 
 
 @dataclass(frozen=True)

@@ -145,7 +145,9 @@ class SimLauncher:
     """Simulated predictors: every ``period`` (virtual) seconds each ready pod
     records ``rps * period * traffic%`` requests into the MetricStore as the
     Seldon executor would (cumulative histogram buckets, counts per code).
-    ``profiles[version] = {"latency": s, "error_rate": f, "startup_s": s}``."""
+    ``profiles[version] = {"latency": s, "error_rate": f, "startup_s": s}``; an LLM
+    predictor profile may add ``tpot`` (s per output token), ``gpu_mem`` (bytes)
+    and ``gpu_power`` (W): the runtime's TPOT histogram and amd-smi gauges."""
 
     BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0)
 
@@ -165,7 +167,7 @@ class SimLauncher:
     async def _emit(self, pod: Pod, prof: dict):
         lbl = {"deployment_name": pod.sd, "predictor_name": pod.predictor, "namespace": pod.namespace}
         counts = {b: 0.0 for b in self.BUCKETS}
-        inf = lsum = ok = err = 0.0
+        inf = lsum = ok = err = toks = 0.0
         lat = float(prof.get("latency", 0.05))
         er = float(prof.get("error_rate", 0.0))
         while True:
@@ -187,6 +189,14 @@ class SimLauncher:
             self.store.add("seldon_api_executor_client_requests_seconds_count", lbl, inf, t)
             self.store.add("seldon_api_executor_server_requests_seconds_count", dict(lbl, code="200", service="predictions"), ok, t)
             self.store.add("seldon_api_executor_server_requests_seconds_count", dict(lbl, code="500", service="predictions"), err, t)
+            if "tpot" in prof:
+                toks += n * 32  # 32 output tokens per request
+                self.store.add("mlop_time_per_output_token_seconds_sum", lbl, toks * float(prof["tpot"]), t)
+                self.store.add("mlop_time_per_output_token_seconds_count", lbl, toks, t)
+            if "gpu_mem" in prof:
+                self.store.add("mlop_gpu_memory_used_bytes", dict(lbl, gpu="0"), float(prof["gpu_mem"]), t)
+            if "gpu_power" in prof:
+                self.store.add("mlop_gpu_power_watts", dict(lbl, gpu="0"), float(prof["gpu_power"]), t)
             await self.clock.sleep(self.period)
 
     async def stop(self, pod: Pod):

@@ -44,6 +44,26 @@ def model_queries(deployment_name: str, predictor_name: str, namespace: str, win
     }
 
 
+TPOT_HIST = "mlop_time_per_output_token_seconds"
+GPU_MEM = "mlop_gpu_memory_used_bytes"
+GPU_POWER = "mlop_gpu_power_watts"
+
+
+def gpu_guard_queries(deployment_name: str, predictor_name: str, namespace: str, window: int = 60) -> dict:
+    """Extra per-predictor series for the canary gate ("plus amd-smi /
+    rocprof series"): mean time per output token from the LLM runtime's TPOT
+    histogram, peak HBM use and mean socket power from its amd-smi gauges.
+    A predictor that exports none of them (e.g. MLFLOW_SERVER / sklearn) yields
+    None and the gate skips the guard."""
+    sel = f'deployment_name="{deployment_name}", predictor_name="{predictor_name}", namespace="{namespace}"'
+    w = f"[{window}s]"
+    return {
+        "tpot_avg": f"sum(increase({TPOT_HIST}_sum{{{sel}}}{w})) / sum(increase({TPOT_HIST}_count{{{sel}}}{w}))",
+        "gpu_memory_used": f"max(max_over_time({GPU_MEM}{{{sel}}}{w}))",
+        "gpu_power": f"avg(avg_over_time({GPU_POWER}{{{sel}}}{w}))",
+    }
+
+
 def _first(result):
     if not result:
         return None
@@ -418,6 +438,14 @@ def _eval(node, store, t, lookback):
                 key = frozenset((k, x) for k, x in lbl.items() if k not in ("le", "__name__"))
                 groups[key].append((float(lbl["le"]), v))
             return [(dict(k), _hq(phi, b)) for k, b in groups.items()]
+        if fn in ("max_over_time", "min_over_time", "avg_over_time", "last_over_time", "sum_over_time",
+                  "count_over_time"):
+            rv = _eval(args[0], store, t, lookback)
+            assert isinstance(rv, tuple) and rv[0] == "range", f"{fn} needs a range vector"
+            agg = {"max_over_time": max, "min_over_time": min, "sum_over_time": sum, "count_over_time": len,
+                   "avg_over_time": lambda xs: sum(xs) / len(xs), "last_over_time": lambda xs: xs[-1]}[fn]
+            return [({k: x for k, x in lbl.items() if k != "__name__"}, float(agg([v for _, v in w])))
+                    for lbl, w, _ in rv[1] if w]
         if fn in ("abs", "ceil", "floor", "sqrt", "exp", "ln"):
             f = {"abs": abs, "ceil": math.ceil, "floor": math.floor, "sqrt": math.sqrt,
                  "exp": math.exp, "ln": math.log}[fn]

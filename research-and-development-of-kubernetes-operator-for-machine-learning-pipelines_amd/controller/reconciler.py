@@ -33,7 +33,7 @@ from .crd import (EV_ALIAS_NOT_FOUND, EV_NEW_VERSION, EV_PREDICTOR_READY, EV_PRO
 from .kube import ApiError
 from .mlflow import NotFound, RegistryError, RegistryUnavailable
 from .placement import plan
-from .prometheus import get_model_metrics, should_promote
+from .prometheus import get_model_metrics, gpu_guard_queries, should_promote
 
 PH_DEPLOYING, PH_READY, PH_CANARY = "Deploying", "Ready", "Canary"
 PH_PROMOTED, PH_ROLLED_BACK, PH_FAILED, PH_NO_ALIAS = "Promoted", "RolledBack", "PromotionFailed", "AliasNotFound"
@@ -281,12 +281,15 @@ class MlflowModelReconciler:
         next_at = float(status.get("canaryNextAttempt", now))
         if now < next_at:
             return next_at - now
-        new_m = await get_model_metrics(self.prom, name, pc, ns, pol.window_s)
-        old_m = await get_model_metrics(self.prom, name, pp, ns, pol.window_s)
+        guards = pol.gpu_guards or {}
+        new_m = await get_model_metrics(self.prom, name, pc, ns, pol.window_s,
+                                        extra_queries=guards and gpu_guard_queries(name, pc, ns, pol.window_s))
+        old_m = await get_model_metrics(self.prom, name, pp, ns, pol.window_s,
+                                        extra_queries=guards and gpu_guard_queries(name, pp, ns, pol.window_s))
         logger.info("[%s/%s] Metrics for new model (version %s): %s", ns, name, cur, new_m)
         logger.info("[%s/%s] Metrics for old model (version %s): %s", ns, name, prev, old_m)
         gate = should_promote(new_m, old_m, pol.thresholds, pol.error_rate_floor, logger=logger,
-                              latency_floor_s=pol.latency_floor_s)
+                              latency_floor_s=pol.latency_floor_s, extra_max_ratio=guards)
         if gate.promote:
             traffic = min(100, int(status.get("canaryTraffic", 0)) + pol.step)
             if traffic >= 100:

@@ -170,6 +170,41 @@ def test_canary_regression_rolls_back_and_does_not_flap():
     run(go())
 
 
+@pytest.mark.parametrize("guards,expect", [(None, "RolledBack"), ({}, "Promoted")])
+def test_gpu_guard_tpot_regression(guards, expect):
+    """Same request latency, but the new LLM predictor's time per output token is
+    40% worse: the default GPU-side guard (tpot_avg <= 1.10x) rolls it back;
+    gpuGuards: {} restores the reference gate, which promotes."""
+    async def go():
+        base = {"latency": 0.05, "gpu_mem": 40e9, "gpu_power": 700.0}
+        env = Env(profiles={"1": dict(base, tpot=0.010), "2": dict(base, tpot=0.014)})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        canary = {} if guards is None else {"gpuGuards": guards}
+        await env.create_cr(canary=canary)
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, expect), 3000)
+        if expect == "RolledBack":
+            assert seldon.traffic_of(await env.sd()) == {"v1": 100}
+            assert "tpot_avg" in (await env.status())["error"]
+        await env.stop()
+    run(go())
+
+
+def test_gpu_guard_hbm_regression_rolls_back():
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05, "gpu_mem": 40e9}, "2": {"latency": 0.05, "gpu_mem": 80e9}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "RolledBack"), 3000)
+        await env.stop()
+    run(go())
+
+
 def test_reference_mode_no_rollback_leaves_split():
     async def go():
         env = Env(profiles={"1": {"latency": 0.05}, "2": {"error_rate": 0.5, "latency": 0.05}}, rollback=False)

@@ -7,7 +7,7 @@ import pytest
 import yaml
 from hypothesis import given, settings, strategies as st
 
-from mlopamd.controller import crd, placement, seldon
+from mlopamd.controller import crd, placement, prometheus, seldon
 from mlopamd.controller.kube import ApiError, FakeKube, merge_patch
 from mlopamd.controller.mlflow import (MlflowRestClient, NotFound, RegistryUnavailable, SqliteRegistry,
                                        serve_registry)
@@ -312,3 +312,31 @@ def test_mlflow_rest_against_sqlite_registry(tmp_path):
             await dead.get_model_version("m", 1)
         await dead.close()
     asyncio.run(go())
+
+
+def test_over_time_functions_and_gpu_guard_queries():
+    st = prometheus.MetricStore()
+    lbl = {"deployment_name": "d", "predictor_name": "v1", "namespace": "n"}
+    for i, v in enumerate((10.0, 30.0, 20.0)):
+        st.add("mlop_gpu_memory_used_bytes", dict(lbl, gpu="0"), v, 100.0 + 10 * i)
+        st.add("mlop_gpu_power_watts", dict(lbl, gpu="0"), 100.0 * (i + 1), 100.0 + 10 * i)
+        st.add("mlop_time_per_output_token_seconds_sum", lbl, 0.02 * 100 * i, 100.0 + 10 * i)
+        st.add("mlop_time_per_output_token_seconds_count", lbl, 100.0 * i, 100.0 + 10 * i)
+    q = prometheus.gpu_guard_queries("d", "v1", "n", 60)
+    ev = lambda s: prometheus.evaluate(s, st, 121.0)  # noqa: E731
+    assert ev(q["gpu_memory_used"])[0][1] == 30.0
+    assert ev(q["gpu_power"])[0][1] == pytest.approx(200.0)
+    assert ev(q["tpot_avg"])[0][1] == pytest.approx(0.02)
+    assert ev('last_over_time(mlop_gpu_memory_used_bytes{predictor_name="v1"}[60s])')[0][1] == 20.0
+    other = prometheus.gpu_guard_queries("d", "v9", "n", 60)
+    assert ev(other["tpot_avg"]) == [] and ev(other["gpu_memory_used"]) == []
+
+
+def test_gate_gpu_guards_skip_missing_series():
+    base = {"latency_95th": 0.1, "error_rate": 0.0, "latency_avg": 0.05}
+    g = prometheus.should_promote(dict(base, tpot_avg=0.02), dict(base, tpot_avg=0.01), {}, 0.0,
+                                  extra_max_ratio={"tpot_avg": 1.1})
+    assert not g.promote and "tpot_avg" in g.reasons[0]
+    g = prometheus.should_promote(dict(base, tpot_avg=None), dict(base, tpot_avg=0.01), {}, 0.0,
+                                  extra_max_ratio={"tpot_avg": 1.1})
+    assert g.promote
