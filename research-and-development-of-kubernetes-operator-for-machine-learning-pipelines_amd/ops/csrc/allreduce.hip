@@ -1,0 +1,229 @@
+// K15: one-shot all-reduce over xGMI peer memory (tensor-parallel decode).
+//
+// Why: a TP decode step all-reduces [B, hidden] bf16 twice per layer (8-16 KiB
+// per token row); at these sizes RCCL's ring is latency-bound (2(N-1) hops).
+// xGMI on MI355X is point-to-point (7 links per GPU), so ONE hop in which every
+// rank reads all peers' inputs at once uses all links in parallel
+// (SURVEY.md §2.5 K15 / §5 "distributed communication backend").
+//
+// Protocol (per rank: one IPC-exported buffer = flags | data[2]):
+//   * every block b copies its slice of the input into its OWN buffer, then
+//     (one lane, after every wave's vmcnt(0) + a block barrier) a SYSTEM-scope
+//     release (L2 write-back) and a relaxed system-scope store of the epoch into
+//     flag[rank][b] of EVERY peer's buffer;
+//   * lanes 0..N-1 of wave 0 poll flag[p][b] of the local buffer until it
+//     reaches the epoch (>=: a fast peer may already be one call ahead), then a
+//     system-scope acquire, vmcnt(0) and a block barrier before any peer load
+//     (MI355X_MICROARCH.md "Valid forms"; cdna_hip_programming.md Guideline 16);
+//   * the block sums its slice over ranks 0..N-1 IN RANK ORDER in fp32 (every
+//     rank produces bitwise-identical output) and stores bf16.
+//   * epochs live in device memory, one counter per block, so the kernel is
+//     hipGraph-capturable (no host-side state per call); data is double
+//     buffered by epoch parity: a peer can run at most one call ahead (it
+//     needs this rank's flag of the call in between), so the parity it
+//     overwrites is never the one still being read.  The grid is FIXED
+//     (kBlocks) so every block advances its epoch on every call.
+//   * every poll is bounded: on timeout the block sets an error word (read by
+//     car_error) and finishes — a wedged peer never hangs the GPU.
+#include "common.h"
+#include "launch.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace mlop {
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kBlocks = 64;
+constexpr int kThreads = 512;
+constexpr int kFlagStride = 16;  // u32 per flag slot: one 64-B line per (source rank, block)
+constexpr size_t kFlagsBytes = (size_t)kMaxRanks * kBlocks * kFlagStride * 4;
+constexpr long kMaxSpins = 1L << 26;
+
+struct Peers {
+  uint8_t* base[kMaxRanks];
+};
+
+struct CarState {
+  int rank = 0, world = 1, device = 0;
+  size_t max_bytes = 0;  // per parity
+  uint8_t* buf = nullptr;
+  uint32_t* epochs = nullptr;
+  int* err = nullptr;
+  Peers peers{};
+};
+
+#define CAR_CHECK(x)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      throw std::runtime_error(std::string("custom all-reduce: ") + #x + ": " +        \
+                               hipGetErrorString(e_));                                 \
+  } while (0)
+
+__device__ __forceinline__ void add_bf16x8(float (&acc)[8], const uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[2 * j] += __uint_as_float(w[j] << 16);
+    acc[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+  }
+}
+
+template <int NR>
+__global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restrict__ out,
+                                                               const uint16_t* __restrict__ in,
+                                                               long n16, Peers peers, int rank,
+                                                               uint32_t* epochs, int* err,
+                                                               size_t max_bytes) {
+  __shared__ uint32_t s_e;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) s_e = epochs[b] + 1;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const long per = (n16 + kBlocks - 1) / kBlocks;
+  const long lo = min(n16, (long)b * per), hi = min(n16, lo + per);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+
+  // 1. publish my slice
+  uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+  for (long i = lo + tid; i < hi; i += kThreads) mine[i] = src[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back dirty L2 lines
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NR; ++p) {
+      uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[p]) + (size_t)(rank * kBlocks + b) * kFlagStride;
+      __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // 2. wait for every peer's slice b
+  if (tid < 64) {
+    if (tid < NR) {
+      const uint32_t* f =
+          reinterpret_cast<const uint32_t*>(peers.base[rank]) + (size_t)(tid * kBlocks + b) * kFlagStride;
+      long spins = 0;
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+        if (++spins > kMaxSpins) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  // 3. reduce in rank order (bitwise identical on every rank)
+  uint4* o = reinterpret_cast<uint4*>(out);
+  for (long i = lo + tid; i < hi; i += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NR; ++p) {
+      const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.base[p] + doff)[i];
+      add_bf16x8(acc, v);
+    }
+    uint4 r;
+    r.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
+    r.y = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
+    r.z = (uint32_t)f2bf(acc[4]) | ((uint32_t)f2bf(acc[5]) << 16);
+    r.w = (uint32_t)f2bf(acc[6]) | ((uint32_t)f2bf(acc[7]) << 16);
+    o[i] = r;
+  }
+  if (tid == 0) epochs[b] = e;
+}
+
+CarState* get(long h) {
+  if (h == 0) throw std::runtime_error("custom all-reduce: null handle");
+  return reinterpret_cast<CarState*>(h);
+}
+
+}  // namespace
+
+long car_create(int rank, int world, long max_bytes, int device) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world)
+    throw std::runtime_error("custom all-reduce: bad rank/world");
+  if (max_bytes <= 0 || max_bytes % 16) throw std::runtime_error("custom all-reduce: max_bytes % 16");
+  auto* s = new CarState;
+  s->rank = rank, s->world = world, s->device = device, s->max_bytes = (size_t)max_bytes;
+  CAR_CHECK(hipSetDevice(device));
+  CAR_CHECK(hipMalloc(&s->buf, kFlagsBytes + 2 * (size_t)max_bytes));
+  CAR_CHECK(hipMemset(s->buf, 0, kFlagsBytes));
+  CAR_CHECK(hipMalloc(&s->epochs, kBlocks * sizeof(uint32_t)));
+  CAR_CHECK(hipMemset(s->epochs, 0, kBlocks * sizeof(uint32_t)));
+  CAR_CHECK(hipMalloc(&s->err, sizeof(int)));
+  CAR_CHECK(hipMemset(s->err, 0, sizeof(int)));
+  CAR_CHECK(hipDeviceSynchronize());
+  s->peers.base[rank] = s->buf;
+  return reinterpret_cast<long>(s);
+}
+
+void car_ipc_handle(long h, void* out64) {
+  CarState* s = get(h);
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+  CAR_CHECK(hipSetDevice(s->device));
+  CAR_CHECK(hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(out64), s->buf));
+}
+
+void car_open(long h, const void* handles) {
+  CarState* s = get(h);
+  CAR_CHECK(hipSetDevice(s->device));
+  const auto* hs = reinterpret_cast<const hipIpcMemHandle_t*>(handles);
+  for (int p = 0; p < s->world; ++p) {
+    if (p == s->rank || s->peers.base[p]) continue;
+    void* ptr = nullptr;
+    CAR_CHECK(hipIpcOpenMemHandle(&ptr, hs[p], hipIpcMemLazyEnablePeerAccess));
+    s->peers.base[p] = reinterpret_cast<uint8_t*>(ptr);
+  }
+}
+
+long car_max_bytes(long h) { return (long)get(h)->max_bytes; }
+
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st) {
+  CarState* s = get(h);
+  if (numel % 8) throw std::runtime_error("custom all-reduce: numel must be a multiple of 8");
+  if ((size_t)numel * 2 > s->max_bytes) throw std::runtime_error("custom all-reduce: message too large");
+  for (int p = 0; p < s->world; ++p)
+    if (!s->peers.base[p]) throw std::runtime_error("custom all-reduce: peers not opened");
+  const long n16 = numel / 8;
+  dim3 g(kBlocks), blk(kThreads);
+  auto* o = static_cast<uint16_t*>(out);
+  auto* i = static_cast<const uint16_t*>(in);
+  switch (s->world) {
+    case 1: car_oneshot_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 2: car_oneshot_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 4: car_oneshot_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 8: car_oneshot_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    default: throw std::runtime_error("custom all-reduce: world must be 1, 2, 4 or 8");
+  }
+  CAR_CHECK(hipGetLastError());
+}
+
+int car_error(long h) {
+  CarState* s = get(h);
+  int v = 0;
+  CAR_CHECK(hipSetDevice(s->device));
+  CAR_CHECK(hipMemcpy(&v, s->err, sizeof(int), hipMemcpyDeviceToHost));
+  return v;
+}
+
+void car_destroy(long h) {
+  CarState* s = get(h);
+  hipSetDevice(s->device);
+  hipDeviceSynchronize();
+  for (int p = 0; p < s->world; ++p)
+    if (p != s->rank && s->peers.base[p]) hipIpcCloseMemHandle(s->peers.base[p]);
+  hipFree(s->buf);
+  hipFree(s->epochs);
+  hipFree(s->err);
+  delete s;
+}
+
+}  // namespace mlop

@@ -271,9 +271,41 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
                       cur_stream());
 }
 
+
+// ---- K15 custom all-reduce: host-side state, int handles -------------------
+int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes, int64_t device) {
+  return mlop::car_create((int)rank, (int)world, (long)max_bytes, (int)device);
+}
+Tensor car_ipc_handle(int64_t h) {
+  Tensor t = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  mlop::car_ipc_handle((long)h, t.data_ptr());
+  return t;
+}
+void car_open(int64_t h, Tensor handles) {
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
+              handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
+  mlop::car_open((long)h, handles.data_ptr());
+}
+void car_all_reduce(int64_t h, Tensor out, Tensor inp) {
+  check_bf16(out, "out"); check_bf16(inp, "inp");
+  TORCH_CHECK(out.numel() == inp.numel(), "all_reduce: out/inp size mismatch");
+  TORCH_CHECK(inp.numel() % 8 == 0, "all_reduce: numel must be a multiple of 8");
+  TORCH_CHECK(inp.numel() * 2 <= mlop::car_max_bytes((long)h), "all_reduce: message exceeds the registered buffer");
+  c10::DeviceGuard g(inp.device());
+  mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream());
+}
+int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
+void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
+
 }  // namespace
 
 TORCH_LIBRARY(mlop, m) {
+  m.def("car_create(int rank, int world, int max_bytes, int device) -> int", &car_create);
+  m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
+  m.def("car_open(int h, Tensor handles) -> ()", &car_open);
+  m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp) -> ()");
+  m.def("car_error(int h) -> int", &car_error);
+  m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
   m.def("grouped_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int max_rows, "
@@ -314,4 +346,5 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("moe_combine", &moe_combine);
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
+  m.impl("car_all_reduce", &car_all_reduce);
 }

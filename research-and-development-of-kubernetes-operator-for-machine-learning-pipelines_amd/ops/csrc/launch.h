@@ -41,4 +41,13 @@ void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStr
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
                    const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);
 
+// K15 custom one-shot all-reduce (allreduce.hip); handles are opaque state pointers
+long car_create(int rank, int world, long max_bytes, int device);
+void car_ipc_handle(long h, void* out64);
+void car_open(long h, const void* handles);
+long car_max_bytes(long h);
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st);
+int car_error(long h);
+void car_destroy(long h);
+
 }  // namespace mlop

@@ -47,9 +47,12 @@ class Group:
     rank: int = 0
     size: int = 1
     handle: object = None
+    car: object = None  # CustomAllReduce (K15) for small bf16 messages on GPU
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            if self.car is not None and self.car.eligible(x):
+                return self.car.all_reduce(x)
             dist.all_reduce(x, group=self.handle)
         return x
 
@@ -96,9 +99,11 @@ def single() -> ParallelState:
     return ParallelState(tp=Group(), ep=Group())
 
 
-def make_parallel_state(tp_size: int = 1, ep_size: int = 1) -> ParallelState:
+def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = True) -> ParallelState:
     """Split the world into consecutive TP groups (TP inside a node: xGMI is point-to-point,
-    keep TP degree <= 8).  EP reuses the TP ranks (experts sharded over the same GPUs)."""
+    keep TP degree <= 8).  EP reuses the TP ranks (experts sharded over the same GPUs).
+    On GPU the TP group gets the K15 one-shot all-reduce for decode-size messages
+    (``MLOP_CUSTOM_AR=0`` keeps everything on RCCL)."""
     if not dist.is_initialized():
         assert tp_size == 1 and ep_size == 1, "TP/EP > 1 needs torch.distributed"
         return single()
@@ -112,4 +117,10 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1) -> ParallelState:
             tp_handle = h
     tp = Group(rank=rank % tp_size, size=tp_size, handle=tp_handle)
     ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=tp_handle)
+    if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() \
+            and dist.get_backend(tp_handle) == "nccl" and os.environ.get("MLOP_CUSTOM_AR", "1") != "0":
+        from .custom_ar import CustomAllReduce
+
+        tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
+                                 group=tp_handle)
     return ParallelState(tp=tp, ep=ep)

@@ -1,0 +1,63 @@
+"""K15 custom one-shot all-reduce over xGMI peer memory (``ops/csrc/allreduce.hip``).
+
+Tensor-parallel decode all-reduces small [B, hidden] bf16 tensors twice per
+layer; RCCL's ring pays 2(N-1) latency-bound hops for them.  Here every rank
+exports one device buffer through HIP IPC, the ranks exchange the 64-byte
+handles once over the (RCCL or gloo) process group, and each call is ONE
+kernel in which every rank reads all peers' inputs in a single hop across the
+point-to-point xGMI links, with an epoch-flag handshake (system-scope
+release / acquire) instead of a collective library call.  The kernel keeps its
+epochs on the device, so it is captured into the decode hipGraphs like any
+other op.  Messages above ``max_bytes`` (prefill) stay on RCCL.
+
+Parity with the reference: the reference has no collective at all (SURVEY.md
+§2.2-2.3); this implements the north-star row K15 / CL1.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_MAX_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_MAX_BYTES", 4 << 20))
+
+
+class CustomAllReduce:
+    def __init__(self, rank: int, world: int, device, group=None, max_bytes: int = DEFAULT_MAX_BYTES):
+        from .. import ops
+
+        ops.load()
+        self.rank, self.world, self.group = rank, world, group
+        self.device = torch.device(device)
+        self.max_bytes = int(max_bytes)
+        self.h = torch.ops.mlop.car_create(rank, world, self.max_bytes, self.device.index or 0)
+        mine = torch.ops.mlop.car_ipc_handle(self.h)
+        if world > 1:
+            allh = [None] * world
+            dist.all_gather_object(allh, bytes(mine.numpy().tobytes()), group=group)
+        else:
+            allh = [bytes(mine.numpy().tobytes())]
+        table = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(world, 64).clone()
+        torch.ops.mlop.car_open(self.h, table)
+        if world > 1:
+            dist.barrier(group=group)
+
+    def eligible(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % 8 == 0 and 2 * x.numel() <= self.max_bytes)
+
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum over ranks (rank order, fp32 accumulation: identical on every rank)."""
+        out = x if out is None else out
+        torch.ops.mlop.car_all_reduce(self.h, out, x)
+        return out
+
+    def error(self) -> int:
+        """Non-zero if any call timed out waiting for a peer (the result is then invalid)."""
+        return int(torch.ops.mlop.car_error(self.h))
+
+    def close(self):
+        if self.h:
+            torch.ops.mlop.car_destroy(self.h)
+            self.h = 0

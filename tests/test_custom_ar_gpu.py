@@ -1,0 +1,106 @@
+"""K15 one-shot all-reduce (ops/csrc/allreduce.hip) on ONE MI355X: two processes
+share cuda:0 and map each other's buffers through HIP IPC, so the epoch-flag
+handshake, the parity double-buffering, in-place use and hipGraph capture are
+exercised exactly as across xGMI peers (the fabric path itself needs a
+multi-GPU node).  Oracle: fp32 sum in rank order of the known per-rank inputs,
+rounded once to bf16 — the kernel must match it bit for bit on every rank."""
+import os
+import socket
+import tempfile
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [8, 4096, 3 * 4096, 64 * 1024, 8000, 4096, 200 * 1024]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(it, n, world):
+    return [torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + p)).to(torch.bfloat16)
+            for p in range(world)]
+
+
+def _oracle(xs):
+    acc = torch.zeros(xs[0].numel(), dtype=torch.float32)
+    for x in xs:
+        acc += x.float()
+    return acc.to(torch.bfloat16)
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mlopamd.parallel.custom_ar import CustomAllReduce
+
+    car = CustomAllReduce(rank, world, torch.device("cuda", 0), group=None, max_bytes=1 << 20)
+    res = {"eager": [], "inplace": [], "graph": []}
+    try:
+        for it, n in enumerate(SIZES):
+            xs = _inputs(it, n, world)
+            x = xs[rank].cuda()
+            if rank == 1 and it % 2:
+                time.sleep(0.05)  # uneven arrival: rank 0 spins on the flags meanwhile
+            out = torch.empty_like(x)
+            car.all_reduce(x, out)
+            torch.cuda.synchronize()
+            res["eager"].append(torch.equal(out.cpu(), _oracle(xs)))
+        # in place, back to back (parity reuse every second call)
+        for it in range(6):
+            xs = _inputs(50 + it, 4096, world)
+            x = xs[rank].cuda()
+            car.all_reduce(x)
+            torch.cuda.synchronize()
+            res["inplace"].append(torch.equal(x.cpu(), _oracle(xs)))
+        # hipGraph: capture two calls, replay with fresh inputs
+        static = torch.zeros(2, 8192, dtype=torch.bfloat16, device="cuda")
+        outs = torch.zeros_like(static)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            car.all_reduce(static[0], outs[0])
+            car.all_reduce(static[1], outs[1])
+        dist.barrier()
+        for it in range(4):
+            xs0, xs1 = _inputs(80 + it, 8192, world), _inputs(90 + it, 8192, world)
+            static[0].copy_(xs0[rank].cuda())
+            static[1].copy_(xs1[rank].cuda())
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            res["graph"].append(torch.equal(outs[0].cpu(), _oracle(xs0)) and
+                                torch.equal(outs[1].cpu(), _oracle(xs1)))
+        res["error"] = car.error()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+
+
+def test_custom_all_reduce_two_processes_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = tempfile.mkdtemp()
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
+        assert res["error"] == 0, f"rank {r}: a flag wait timed out"
+        assert all(res["eager"]), (r, res["eager"])
+        assert all(res["inplace"]), (r, res["inplace"])
+        assert all(res["graph"]), (r, res["graph"])
