@@ -117,8 +117,9 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
             tp_handle = h
     tp = Group(rank=rank % tp_size, size=tp_size, handle=tp_handle)
     ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=tp_handle)
-    if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() \
-            and dist.get_backend(tp_handle) == "nccl" and os.environ.get("MLOP_CUSTOM_AR", "1") != "0":
+    car_env = os.environ.get("MLOP_CUSTOM_AR", "1")
+    backend_ok = dist.get_backend(tp_handle) == "nccl" or car_env == "force"  # force: gloo + GPU tests
+    if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() and backend_ok and car_env != "0":
         from .custom_ar import CustomAllReduce
 
         tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),

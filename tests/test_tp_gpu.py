@@ -1,0 +1,80 @@
+"""Tensor-parallel serving on the GPU path with ONE MI355X: two TP ranks share
+cuda:0 (gloo carries the step-metadata broadcast and the logits gather, the
+K15 one-shot all-reduce carries the row-parallel sums through HIP IPC), so the
+sharded HIP-kernel model, the lock-step scheduler and the custom all-reduce
+run together.  Oracle: the unsharded model's dense fp32 recompute (greedy
+tokens must be the argmax or within a small logit gap of it: TP changes the
+bf16 summation order)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+PROMPTS = [[5, 9, 11, 40, 2, 7], list(range(20, 61)), [100, 3], list(range(300, 390))]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir, cfg_name):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MLOP_CUSTOM_AR="force")
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    dev = torch.device("cuda", 0)
+    cfg = get_config(cfg_name)
+    full = build_model(cfg, device=dev, seed=4)
+    ps = make_parallel_state(tp_size=2, ep_size=1)
+    assert ps.tp.car is not None
+    shard = build_model(cfg, device=dev, pstate=ps, seed=4).load_shard_from(full)
+    ec = EngineConfig(max_num_seqs=4, max_num_batched_tokens=48, max_model_len=256, num_kv_blocks=64,
+                      use_graphs=False)
+    eng = Engine(shard, ec)
+    res = {}
+    try:
+        if ps.tp_rank == 0:
+            res["tp"] = eng.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
+            eng.shutdown()
+            res["car_error"] = ps.tp.car.error()
+        else:
+            eng.worker_loop()
+            res["worker_steps"] = eng.stats["worker_steps"]
+            res["car_error"] = ps.tp.car.error()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        ps.tp.car.close()
+        dist.destroy_process_group()
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+
+
+@pytest.mark.parametrize("cfg_name", ["tiny-llama"])
+def test_tp2_engine_on_gpu_with_custom_all_reduce(cfg_name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = tempfile.mkdtemp()
+    mp.start_processes(_worker, args=(2, _free_port(), d, cfg_name), nprocs=2, join=True, start_method="spawn")
+    r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=False)
+    r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=False)
+    assert r0["car_error"] == 0 and r1["car_error"] == 0 and r1["worker_steps"] > 0
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from test_model_gpu import _check_greedy
+
+    full = build_model(get_config(cfg_name), device=torch.device("cuda", 0), seed=4)
+    _check_greedy(full, PROMPTS, r0["tp"])
