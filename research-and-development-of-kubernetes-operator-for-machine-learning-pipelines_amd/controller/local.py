@@ -94,8 +94,9 @@ class ProcessLauncher:
     """One OS process per predictor replica running the V2 runtime server."""
 
     def __init__(self, scraper=None, extra_env: dict | None = None, python: str = sys.executable,
-                 ready_timeout_s: float = 600.0):
+                 ready_timeout_s: float = 600.0, per_predictor_env: dict | None = None):
         self.scraper, self.extra_env, self.python = scraper, extra_env or {}, python
+        self.per_predictor_env = per_predictor_env or {}  # predictor name -> env (fault injection)
         self.ready_timeout_s = ready_timeout_s
 
     async def start(self, pod: Pod):
@@ -105,6 +106,7 @@ class ProcessLauncher:
         env = dict(os.environ)
         env.update(_env_of(pod.spec))
         env.update(self.extra_env)
+        env.update(self.per_predictor_env.get(pod.predictor, {}))
         env["SELDON_DEPLOYMENT_ID"] = pod.sd
         env["SELDON_NAMESPACE"] = pod.namespace
         repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
