@@ -112,15 +112,23 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0,
 
 
 def paged_attention(q, k_cache, v_cache, meta, out: torch.Tensor | None = None):
-    """Ragged paged attention; ``meta`` is a ``mlopamd.runtime.attn_meta.AttnMeta``."""
+    """Ragged paged attention; ``meta`` is a ``mlopamd.runtime.attn_meta.AttnMeta``.
+    Decode / short rows run on the 16-q-row tiles (``tile_*``), prompt chunks on
+    the flash-prefill tiles (``ptile_*``); both write disjoint rows of ``out``."""
     if not q.is_cuda:
         return ref.paged_attention(q, k_cache, v_cache, meta)
     _need_gpu()
     out = torch.empty_like(q) if out is None else out
     scale = 1.0 / math.sqrt(q.shape[-1])
-    torch.ops.mlop.paged_attention(out, meta.part_o, meta.part_ml, q, k_cache, v_cache,
-                                   meta.block_tables, meta.tile_seq, meta.tile_q0, meta.q_start,
-                                   meta.q_len, meta.ctx_len, scale, meta.part_tokens, meta.nparts)
+    if meta.tile_seq.numel():
+        torch.ops.mlop.paged_attention(out, meta.part_o, meta.part_ml, q, k_cache, v_cache,
+                                       meta.block_tables, meta.tile_seq, meta.tile_q0, meta.q_start,
+                                       meta.q_len, meta.ctx_len, scale, meta.part_tokens, meta.nparts)
+    pts = getattr(meta, "ptile_seq", None)
+    if pts is not None and pts.numel():
+        # prompt chunks: K7 flash prefill (128 q-rows per workgroup, K/V via LDS-DMA)
+        torch.ops.mlop.flash_prefill(out, q, k_cache, v_cache, meta.block_tables, pts, meta.ptile_q0,
+                                     meta.q_start, meta.q_len, meta.ctx_len, scale)
     return out
 
 

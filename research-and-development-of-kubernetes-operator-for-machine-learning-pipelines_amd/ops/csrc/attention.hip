@@ -275,4 +275,186 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
 #undef MLOP_ATTN_CASE
 }
 
+// ---------------------------------------------------------------------------
+// K7 flash prefill: the same S^T / O^T formulation, re-blocked for prompt
+// chunks.  One workgroup = 128 MFMA q-rows (128/G query tokens x the G heads of
+// one kv head) against EVERY key of its causal range; each wave owns 2 column
+// tiles (32 q-rows), so every K/V fragment read from LDS feeds 2 MFMAs and
+// every K/V byte fetched from HBM/L2 feeds all 128 q-rows (vs 16 in the decode
+// tile above: 8x the arithmetic intensity).  K/V page pairs (32 keys, 16 KB)
+// stream through a 3-deep LDS ring by LDS-DMA (global_load_lds, counted vmcnt,
+// one raw barrier per pair), swizzled through the SOURCE address:
+//   K page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ k        (ds_read_b128, 16 keys/group)
+//   V page [128 dims][4 x 8 B]:  chunk c of dim d at c ^ ((d>>3&1)<<1) (ds_read_b64, dims d, d+8)
+// both conflict-free for the fragment reads below.
+template <int G>
+__global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
+    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
+    const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int num_blocks) {
+  constexpr int QB = 128 / G;            // query tokens per workgroup
+  constexpr int STAGES = 3;
+  constexpr int STAGE = 4 * kBS * kD;    // bf16 per stage: K page A | K page B | V page A | V page B
+  constexpr int PAGE = kBS * kD;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[STAGES * STAGE];
+
+  const int tile = blockIdx.x, kvh = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int s = ptile_seq[tile], q0 = ptile_q0[tile];
+  const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
+  const int last_q = min(q0 + QB, ql) - 1;
+  const int kv_end = ctx - ql + last_q + 1;  // exclusive causal limit of the workgroup
+  const int n_pairs = (kv_end + 31) >> 5;
+  const int n_pages = (kv_end + kBS - 1) / kBS;
+  const int r = lane & 15, g4 = lane >> 4;
+
+  bf16x8 qf[2][4];
+  int pos_r[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int R = 32 * wid + 16 * c + r;
+    const int qi = q0 + R / G;
+    const bool ok = qi < ql;
+    pos_r[c] = ok ? ctx - ql + qi : -1;
+    const uint16_t* qrow = q + ((size_t)(qs + (ok ? qi : 0)) * Hq + kvh * G + R % G) * kD;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + g4 * 8);
+      qf[c][kk] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f32x4 o[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int d = 0; d < 8; ++d) o[c][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {kNegBig, kNegBig}, l[2] = {0.f, 0.f};
+
+  const int* bt = block_tables + (size_t)s * bt_stride;
+  const size_t page_stride = (size_t)Hkv * PAGE;
+  // this lane's DMA source offsets inside a page (wave w moves piece w of each page)
+  const int kkey = wid * 4 + (lane >> 4);
+  const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
+  const int vdim = wid * 32 + (lane >> 1);
+  const int v_off = kvh * PAGE + vdim * kBS + ((((lane & 1) ^ ((vdim >> 3) & 1))) << 3);
+  auto issue = [&](int buf, int pp) {
+    const int pgA = min(max(bt[2 * pp], 0), num_blocks - 1);
+    const int pgB = (2 * pp + 1 < n_pages) ? min(max(bt[2 * pp + 1], 0), num_blocks - 1) : pgA;
+    uint16_t* base = smem + buf * STAGE + wid * 512;
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pgA * page_stride + k_off), (lds_void_t*)(base), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_off), (lds_void_t*)(base + PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vc + pgA * page_stride + v_off), (lds_void_t*)(base + 2 * PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vc + pgB * page_stride + v_off), (lds_void_t*)(base + 3 * PAGE), 16, 0, 0);
+  };
+
+  issue(0, 0);
+  if (n_pairs > 1) issue(1, 1);
+  for (int pp = 0; pp < n_pairs; ++pp) {
+    if (pp + 1 < n_pairs) wait_vmcnt<4>(); else wait_vmcnt<0>();
+    raw_barrier();  // pair pp visible to every wave; buffer (pp-1)%3 free
+    if (pp + 2 < n_pairs) issue((pp + 2) % STAGES, pp + 2);
+    const uint16_t* sK = smem + (pp % STAGES) * STAGE;
+    const uint16_t* sV = sK + 2 * PAGE;
+    bf16x8 ka[4], kb[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int slot = ((kk * 4 + g4) ^ r) << 3;
+      ka[kk] = *reinterpret_cast<const bf16x8*>(sK + r * kD + slot);
+      kb[kk] = *reinterpret_cast<const bf16x8*>(sK + PAGE + r * kD + slot);
+    }
+    bf16x4 va[8], vb[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int dim = d * 16 + r;
+      const int c8 = (g4 ^ (((dim >> 3) & 1) << 1)) << 2;
+      va[d] = *reinterpret_cast<const bf16x4*>(sV + dim * kBS + c8);
+      vb[d] = *reinterpret_cast<const bf16x4*>(sV + PAGE + dim * kBS + c8);
+    }
+    const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        sa = mfma16(ka[kk], qf[c][kk], sa);
+        sb = mfma16(kb[kk], qf[c][kk], sb);
+      }
+      float pa[4], pb[4];
+      float mx = kNegBig;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pa[i] = (tokA + i <= pos_r[c]) ? sa[i] * scale_log2 : -INFINITY;
+        pb[i] = (tokB + i <= pos_r[c]) ? sb[i] * scale_log2 : -INFINITY;
+        mx = fmaxf(mx, fmaxf(pa[i], pb[i]));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m[c], mx);
+      const float alpha = exp2f(m[c] - m_new);
+      m[c] = m_new;
+      float rs = 0.f;
+      bf16x8 pf;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pa[i] = exp2f(pa[i] - m_new);
+        pb[i] = exp2f(pb[i] - m_new);
+        rs += pa[i] + pb[i];
+        pf[i] = (short)f2bf(pa[i]);
+        pf[4 + i] = (short)f2bf(pb[i]);
+      }
+      l[c] = l[c] * alpha + rs;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        o[c][d] *= alpha;
+        bf16x8 vf = {va[d][0], va[d][1], va[d][2], va[d][3], vb[d][0], vb[d][1], vb[d][2], vb[d][3]};
+        o[c][d] = mfma16(vf, pf, o[c][d]);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float L = l[c];
+    L += __shfl_xor(L, 16, 64);
+    L += __shfl_xor(L, 32, 64);
+    const int R = 32 * wid + 16 * c + r;
+    const int qi = q0 + R / G;
+    if (qi >= ql) continue;
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    uint16_t* orow = out + ((size_t)(qs + qi) * Hq + kvh * G + R % G) * kD + g4 * 4;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      u32x2 v;
+      v[0] = pack2(o[c][d][0] * inv, o[c][d][1] * inv);
+      v[1] = pack2(o[c][d][2] * inv, o[c][d][3] * inv);
+      *reinterpret_cast<u32x2*>(orow + d * 16) = v;
+    }
+  }
+}
+
+void launch_flash_prefill(void* out, const void* q, const void* kc, const void* vc, const int* bt,
+                          int bt_stride, const int* ptile_seq, const int* ptile_q0,
+                          const int* q_start, const int* q_len, const int* ctx_len, int num_ptiles,
+                          int Hq, int Hkv, float scale_log2, int num_blocks, hipStream_t st) {
+  if (num_ptiles == 0) return;
+  dim3 grid(num_ptiles, Hkv);
+#define MLOP_FLASH_CASE(GG)                                                                       \
+  case GG:                                                                                        \
+    flash_prefill_kernel<GG><<<grid, 256, 0, st>>>(                                              \
+        (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt,        \
+        bt_stride, ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks); \
+    break;
+  switch (Hq / Hkv) {
+    MLOP_FLASH_CASE(1)
+    MLOP_FLASH_CASE(2)
+    MLOP_FLASH_CASE(4)
+    MLOP_FLASH_CASE(8)
+    default: break;
+  }
+#undef MLOP_FLASH_CASE
+}
+
 }  // namespace mlop

@@ -95,6 +95,37 @@ void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_start) {
                          cur_stream());
 }
 
+void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
+                   Tensor ptile_seq, Tensor ptile_q0, Tensor q_start, Tensor q_len, Tensor ctx_len,
+                   double scale) {
+  check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables"); check_i32(ptile_seq, "ptile_seq");
+  check_i32(ptile_q0, "ptile_q0"); check_i32(q_start, "q_start"); check_i32(q_len, "q_len");
+  check_i32(ctx_len, "ctx_len");
+  TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
+              "k_cache must be [NB, Hkv, 16, 128]");
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 128, 16}),
+              "v_cache must be [NB, Hkv, 128, 16]");
+  const int Hq = (int)q.size(1), Hkv = (int)k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "flash prefill: GQA group must be 1, 2, 4 or 8");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(ptile_seq.numel() == ptile_q0.numel(), "tile arrays");
+  TORCH_CHECK(q_start.numel() == q_len.numel() && q_len.numel() == ctx_len.numel() &&
+                  block_tables.size(0) >= q_len.numel(),
+              "per-sequence arrays");
+  c10::DeviceGuard g(q.device());
+  mlop::launch_flash_prefill(out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                             block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                             ptile_seq.data_ptr<int>(), ptile_q0.data_ptr<int>(),
+                             q_start.data_ptr<int>(), q_len.data_ptr<int>(), ctx_len.data_ptr<int>(),
+                             (int)ptile_seq.numel(), Hq, Hkv, (float)(scale * 1.4426950408889634),
+                             (int)k_cache.size(0), cur_stream());
+}
+
 void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_cache,
                      Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0,
                      Tensor q_start, Tensor q_len, Tensor ctx_len, double scale,
@@ -325,6 +356,8 @@ TORCH_LIBRARY(mlop, m) {
         "Tensor pos, Tensor cos_sin, Tensor slots) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor x, int interleaved=0) -> ()");
   m.def("embedding(Tensor(a!) out, Tensor table, Tensor ids, int vocab_start) -> ()");
+  m.def("flash_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor ptile_seq, Tensor ptile_q0, Tensor q_start, Tensor q_len, Tensor ctx_len, float scale) -> ()");
   m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor q, "
         "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, float scale, int part_tokens, "
@@ -338,6 +371,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("embedding", &embedding);
   m.impl("paged_attention", &paged_attention);
+  m.impl("flash_prefill", &flash_prefill);
   m.impl("gemm", &gemm);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);

@@ -19,6 +19,21 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;    // 16x16 MFMA accumu
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 using u32x2 = __attribute__((ext_vector_type(2))) uint32_t;
 
+typedef __attribute__((address_space(3))) void lds_void_t;  // LDS-DMA destination
+
+// s_barrier without __syncthreads' fence (whose vmcnt(0) would drain in-flight
+// LDS-DMA; cdna_hip_programming.md "Pipelining across barriers")
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ float bf2f_s(short v) { return bf2f((uint16_t)v); }
 

@@ -39,23 +39,12 @@ namespace mlop {
 enum { EPI_NONE = 0, EPI_SILU_MUL = 1 };
 constexpr int kBK = 64;
 constexpr int kStages = 3;
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // 16-B slot of chunk c in image row r is c ^ swz(r).  Two 128-B rows share one
 // 256-B bank row, so (r>>1)&7 (not r&7) makes the 16 rows of a ds_read_b128 lane
 // group land on 16 distinct slots: (r&1) picks the half, swz the slot in it.
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 __device__ __forceinline__ float silu_bf(float g) {
   const float gb = bf2f(f2bf(g));

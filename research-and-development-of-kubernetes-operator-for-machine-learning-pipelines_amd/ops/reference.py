@@ -88,7 +88,10 @@ def paged_attention(q, k_cache, v_cache, meta):
     qs, ql, cl = (meta.q_start.cpu().tolist(), meta.q_len.cpu().tolist(), meta.ctx_len.cpu().tolist())
     bt = meta.block_tables.cpu()
     # only rows referenced by this launch's tiles are live (other rows hold stale values)
-    for s in sorted(set(meta.tile_seq.cpu().tolist())):
+    live = set(meta.tile_seq.cpu().tolist())
+    if getattr(meta, "ptile_seq", None) is not None:
+        live |= set(meta.ptile_seq.cpu().tolist())
+    for s in sorted(live):
         if ql[s] == 0 or cl[s] == 0:
             continue
         k, v = gather_kv(k_cache, v_cache, bt[s], cl[s])

@@ -8,7 +8,9 @@ see new values on every replay without re-capture.
 Sequence-indexed arrays (q_start, q_len, ctx_len, block_tables) are indexed by
 a stable *row* (the sequence's slot in [0, max_seqs)), so the host only
 touches the rows that changed; tiles (16 MFMA q-rows = 16/G query tokens)
-point at rows.
+point at rows.  Rows with a prompt chunk of at least ``flash_min_q`` tokens
+get flash-prefill tiles instead (128 q-rows = 128/G tokens each, emitted
+latest-first so the longest causal ranges start first).
 """
 from __future__ import annotations
 
@@ -25,8 +27,10 @@ class AttnMeta:
     positions: torch.Tensor   # int32 [T]
     slots: torch.Tensor       # int32 [T]
     block_tables: torch.Tensor  # int32 [max_seqs, max_blocks]
-    tile_seq: torch.Tensor    # int32 [num_tiles]
+    tile_seq: torch.Tensor    # int32 [num_tiles]   decode-kernel tiles (16 q-rows)
     tile_q0: torch.Tensor     # int32 [num_tiles]
+    ptile_seq: torch.Tensor   # int32 [num_ptiles]  flash-prefill tiles (128 q-rows)
+    ptile_q0: torch.Tensor    # int32 [num_ptiles]
     q_start: torch.Tensor     # int32 [max_seqs]
     q_len: torch.Tensor       # int32 [max_seqs]
     ctx_len: torch.Tensor     # int32 [max_seqs]
@@ -59,14 +63,18 @@ class MetaBuffers:
     and ``max_seqs`` concurrent sequences."""
 
     def __init__(self, max_tokens: int, max_seqs: int, max_blocks_per_seq: int, group: int,
-                 n_kv: int, max_model_len: int, device):
+                 n_kv: int, max_model_len: int, device, flash_min_q: int = 17):
         self.device = torch.device(device)
         self.max_tokens, self.max_seqs, self.mb = max_tokens, max_seqs, max_blocks_per_seq
         self.G, self.n_kv, self.max_model_len = group, n_kv, max_model_len
         self.qt = 16 // group
+        self.pqt = 128 // group if group <= 8 else 0  # flash tile tokens (0: no flash kernel for G > 8)
+        self.flash_min_q = flash_min_q if self.pqt else 1 << 30
         self.max_tiles = max_tokens  # worst case: one tile per token
+        self.npt = 0                 # flash tiles of the last fill
         sizes = [("positions", max_tokens), ("slots", max_tokens), ("tile_seq", self.max_tiles),
-                 ("tile_q0", self.max_tiles), ("q_start", max_seqs), ("q_len", max_seqs),
+                 ("tile_q0", self.max_tiles), ("ptile_seq", self.max_tiles), ("ptile_q0", self.max_tiles),
+                 ("q_start", max_seqs), ("q_len", max_seqs),
                  ("ctx_len", max_seqs), ("block_tables", max_seqs * max_blocks_per_seq)]
         self.off = {}
         o = 0
@@ -108,13 +116,15 @@ class MetaBuffers:
         if n_logits:
             self.lidx_d[:n_logits].copy_(self.lidx_h[:n_logits], non_blocking=True)
 
-    def meta(self, num_tokens: int, num_tiles: int, n_logits: int, part_tokens: int, nparts: int) -> AttnMeta:
+    def meta(self, num_tokens: int, num_tiles: int, n_logits: int, part_tokens: int, nparts: int,
+             num_ptiles: int = 0) -> AttnMeta:
         if nparts > 1:
             assert num_tiles * self.n_kv * nparts <= self.wp_capacity, "partial workspace too small"
         return AttnMeta(
             positions=self.view_d("positions", num_tokens), slots=self.view_d("slots", num_tokens),
             block_tables=self.view_d("block_tables").view(self.max_seqs, self.mb),
             tile_seq=self.view_d("tile_seq", num_tiles), tile_q0=self.view_d("tile_q0", num_tiles),
+            ptile_seq=self.view_d("ptile_seq", num_ptiles), ptile_q0=self.view_d("ptile_q0", num_ptiles),
             q_start=self.view_d("q_start"), q_len=self.view_d("q_len"), ctx_len=self.view_d("ctx_len"),
             part_tokens=part_tokens, nparts=nparts, part_o=self.part_o, part_ml=self.part_ml,
             logits_idx=self.lidx_d[:n_logits], num_tokens=num_tokens)
@@ -126,7 +136,8 @@ class MetaBuffers:
         KV is written this step; ctx_lens[i] context length AFTER this step;
         token_ids_per_seq[i]: the q_len input ids. Block tables must already
         hold the pages covering ctx_lens.  want_logits[i] (default all): emit a
-        logits row for sequence i's last token.  Returns (T, num_tiles, n_logits)."""
+        logits row for sequence i's last token.  Returns (T, num_tiles, n_logits);
+        the flash-tile count is left in ``self.npt``."""
         return self._fill_ragged(0, 0, 0, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits)
 
     def fill_mixed(self, d_rows: np.ndarray, d_ctx: np.ndarray, d_last: np.ndarray,
@@ -142,6 +153,8 @@ class MetaBuffers:
     def _fill_ragged(self, t, nt, nl, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits):
         pos_h, slot_h = self.view_h("positions"), self.view_h("slots")
         ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
+        pts_h, ptq_h = self.view_h("ptile_seq"), self.view_h("ptile_q0")
+        npt, pqt = 0, self.pqt
         qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")
         qt = self.qt
         for i, row in enumerate(rows):
@@ -151,20 +164,28 @@ class MetaBuffers:
             pos_h[t:t + ql] = p
             slot_h[t:t + ql] = self.bt_h[row, p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE
             self.ids_hn[t:t + ql] = token_ids_per_seq[i]
-            ntile = (ql + qt - 1) // qt
-            ts_h[nt:nt + ntile] = row
-            tq_h[nt:nt + ntile] = np.arange(ntile, dtype=np.int32) * qt
-            nt += ntile
+            if ql >= self.flash_min_q:
+                n = (ql + pqt - 1) // pqt
+                pts_h[npt:npt + n] = row
+                ptq_h[npt:npt + n] = np.arange(n - 1, -1, -1, dtype=np.int32) * pqt  # latest first
+                npt += n
+            else:
+                ntile = (ql + qt - 1) // qt
+                ts_h[nt:nt + ntile] = row
+                tq_h[nt:nt + ntile] = np.arange(ntile, dtype=np.int32) * qt
+                nt += ntile
             t += ql
             if want_logits is None or want_logits[i]:
                 self.lidx_hn[nl] = t - 1
                 nl += 1
+        self.npt = npt
         return t, nt, nl
 
     def fill_decode(self, rows: np.ndarray, ctx_lens: np.ndarray, last_tokens: np.ndarray, pad_to: int):
         """Vectorised decode fill: one query token per sequence, padded to the
         graph bucket ``pad_to`` with rows that attend to nothing."""
         B = len(rows)
+        self.npt = 0
         pos_h, slot_h = self.view_h("positions"), self.view_h("slots")
         ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
         qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")

@@ -42,7 +42,7 @@ KIND_STOP, KIND_EAGER, KIND_GRAPH = 0, 1, 2
 
 class StepSync:
     """Lock-step execution across a tensor-parallel group: rank 0 broadcasts
-    [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket] and the
+    [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket, num_flash_tiles] and the
     already-uploaded metadata / ids / logits-index device buffers (over RCCL
     on GPU, gloo on CPU); every rank then runs the identical forward."""
 
@@ -50,8 +50,8 @@ class StepSync:
         self.g = group
         self.is_leader = group.rank == 0
 
-    def send(self, eng, kind, T, nt, nl, part, nparts, bucket):
-        hdr = torch.tensor([kind, T, nt, nl, part, nparts, bucket, 0], dtype=torch.int64, device=eng.device)
+    def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0):
+        hdr = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt], dtype=torch.int64, device=eng.device)
         self.g.broadcast(hdr, 0)
         if kind == KIND_STOP:
             return
@@ -65,7 +65,7 @@ class StepSync:
     def recv(self, eng):
         hdr = torch.zeros(8, dtype=torch.int64, device=eng.device)
         self.g.broadcast(hdr, 0)
-        kind, T, nt, nl, part, nparts, bucket, _ = hdr.tolist()
+        kind, T, nt, nl, part, nparts, bucket, npt = hdr.tolist()
         if kind != KIND_STOP:
             m = eng.meta
             self.g.broadcast(m.d, 0)
@@ -73,7 +73,7 @@ class StepSync:
                 self.g.broadcast(m.ids_d[:T], 0)
             if nl:
                 self.g.broadcast(m.lidx_d[:nl], 0)
-        return kind, T, nt, nl, part, nparts, bucket
+        return kind, T, nt, nl, part, nparts, bucket, npt
 
 
 class Status(Enum):
@@ -592,16 +592,17 @@ class Engine:
         small header + the metadata buffers to the TP group (SURVEY §2.5 CL5);
         the other ranks run the same ``_execute`` from ``worker_loop``."""
         self.meta.upload(T, nl)
+        npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
         if self.step_sync is not None:
-            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket)
-        return self._execute(kind, T, nt, nl, part, nparts, bucket)
+            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt)
+        return self._execute(kind, T, nt, nl, part, nparts, bucket, npt)
 
-    def _execute(self, kind, T, nt, nl, part, nparts, bucket):
+    def _execute(self, kind, T, nt, nl, part, nparts, bucket, npt=0):
         if kind == KIND_GRAPH:
             graph, logits_buf = self.graphs[bucket]
             graph.replay()
             return logits_buf
-        meta = self.meta.meta(T, nt, nl, part, nparts)
+        meta = self.meta.meta(T, nt, nl, part, nparts, npt)
         hidden = self.model.forward(self.meta.ids_d[:T], meta, self.kv)
         if nl == 0:
             return None

@@ -75,7 +75,9 @@ class Meta:
     pass
 
 
-def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shuffle_rows=True):
+def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shuffle_rows=True,
+              flash_min_q=1 << 30):
+    """Rows with q_len >= flash_min_q get flash-prefill tiles (128/G tokens, latest first)."""
     from mlopamd.runtime.attn_meta import plan_partitions
 
     S = len(q_lens)
@@ -91,25 +93,54 @@ def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shu
         p += n
     qt = 16 // G
     q_start = np.zeros(R, np.int32); q_len = np.zeros(R, np.int32); ctx = np.zeros(R, np.int32)
-    ts, tq = [], []
+    ts, tq, pts, ptq = [], [], [], []
+    pqt = 128 // G
     t = 0
     for i in range(S):
         r = rows[i]
         q_start[r], q_len[r], ctx[r] = t, q_lens[i], ctx_lens[i]
-        nt = (q_lens[i] + qt - 1) // qt
-        ts += [r] * nt
-        tq += list(range(0, nt * qt, qt))
+        if q_lens[i] >= flash_min_q and G <= 8:
+            n = (q_lens[i] + pqt - 1) // pqt
+            pts += [r] * n
+            ptq += list(range((n - 1) * pqt, -1, -pqt))
+        else:
+            nt = (q_lens[i] + qt - 1) // qt
+            ts += [r] * nt
+            tq += list(range(0, nt * qt, qt))
         t += q_lens[i]
     m = Meta()
     d = lambda a: torch.tensor(np.asarray(a), dtype=torch.int32, device=gpu)  # noqa: E731
     m.block_tables, m.q_start, m.q_len, m.ctx_len = d(bt), d(q_start), d(q_len), d(ctx)
-    m.tile_seq, m.tile_q0 = d(ts), d(tq)
+    m.tile_seq, m.tile_q0 = d(np.asarray(ts, np.int32)), d(np.asarray(tq, np.int32))
+    m.ptile_seq, m.ptile_q0 = d(np.asarray(pts, np.int32)), d(np.asarray(ptq, np.int32))
     if part_tokens is None:
         part_tokens, nparts = plan_partitions(len(ts), Hkv, max(ctx_lens))
     m.part_tokens, m.nparts = part_tokens, nparts
     m.part_o = torch.empty(len(ts) * Hkv * nparts * 16 * 128, device=gpu)
     m.part_ml = torch.empty(len(ts) * Hkv * nparts * 16 * 2, device=gpu)
     return m, t
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16), (32, 16), (16, 8)])
+@pytest.mark.parametrize("q_lens,ctx_lens", [
+    ([1, 40, 200, 17], [1, 40, 200, 17]),            # fresh prompts, partial last tiles
+    ([300, 1, 130], [1500, 700, 130]),               # chunked prefill continuing a context + a decode row
+    ([1024], [1024]),                                # one long prompt (many causal tiles)
+])
+def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
+    """K7 flash-prefill tiles (with the decode kernel on the short rows of the
+    same launch) against the fp32 reference attention."""
+    torch.manual_seed(0)
+    np.random.seed(0)
+    G = Hq // Hkv
+    NB = sum((c + 15) // 16 for c in ctx_lens) + 8
+    kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, flash_min_q=17)
+    assert m.ptile_seq.numel() > 0
+    q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
+    out = ops.paged_attention(q, kc, vc, m)
+    close(out, ref.paged_attention(q, kc, vc, m), atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
