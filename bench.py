@@ -56,6 +56,9 @@ def parse(argv=None):
     ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree per replica (config 4: --model llama3-70b --tp 8); "
+                         "replicas = world / tp, each TP group's rank 0 schedules")
     return ap.parse_args(argv)
 
 
@@ -73,13 +76,32 @@ def main(argv=None):
 
     from mlopamd.runtime.deploy import deploy_for_bench
 
+    ekw = dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
+               max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
+               prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
+               mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk)
     t0 = time.perf_counter()
-    engine, ready_s, deploy_info = deploy_for_bench(
-        model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank,
-        engine_kwargs=dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
-                           max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
-                           prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
-                           mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk))
+    leader = True
+    if a.tp > 1:
+        assert world % a.tp == 0, f"world {world} not divisible by --tp {a.tp}"
+        os.environ.setdefault("MLOP_TP_GRAPHS", "1")  # the one-shot all-reduce is graph-capturable
+        from mlopamd.runtime.tp_worker import build_tp_engine
+
+        engine, ps = build_tp_engine(a.model, a.tp, device=dev, seed=a.seed + rank // a.tp, engine_kwargs=ekw)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        ready_s = time.perf_counter() - t0
+        deploy_info = {"path": "direct-tp", "tp": a.tp, "replicas": world // a.tp,
+                       "weight_gb_per_gpu": round(engine.model.weight_bytes() / 1e9, 2),
+                       "kv_blocks": engine.kv.num_blocks}
+        leader = ps.tp_rank == 0
+    else:
+        engine, ready_s, deploy_info = deploy_for_bench(
+            model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank, engine_kwargs=ekw)
+    if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
+        engine.worker_loop()
+        _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine)
+        return
     from mlopamd.runtime.sampler import SamplingParams
 
     rng = np.random.default_rng(1234 + rank)
@@ -106,19 +128,20 @@ def main(argv=None):
         return gen
 
     run_steps(a.warmup)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    engine.sync_point()  # device sync + world barrier (TP workers join it)
     s0 = dict(engine.stats)
     t_start = time.perf_counter()
     gen = run_steps(a.steps)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    engine.sync_point()
     elapsed = time.perf_counter() - t_start
     stats = {k: engine.stats[k] - s0.get(k, 0) for k in engine.stats}
+    if a.tp > 1:
+        engine.shutdown()  # release the TP workers before the result gather
+    _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine)
+
+
+def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine):
+    import torch.distributed as dist
 
     tot = torch.tensor([float(gen), elapsed, ready_s, float(stats.get("prefill_tokens", 0))], dtype=torch.float64)
     if world > 1:
@@ -130,7 +153,7 @@ def main(argv=None):
         gathered = [tot]
     total_gen = sum(float(g[0]) for g in gathered)
     max_t = max(float(g[1]) for g in gathered)
-    readies = sorted(float(g[2]) for g in gathered)
+    readies = sorted(float(g[2]) for g in gathered if float(g[1]) > 0 or world == 1)
     p50_ready = readies[len(readies) // 2] if len(readies) % 2 else 0.5 * (readies[len(readies) // 2 - 1] + readies[len(readies) // 2])
     total_prefill = sum(float(g[3]) for g in gathered)
     value = total_gen / max_t
@@ -148,8 +171,10 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random prompt tokens, random-init weights)",
-            "config": {"model": "Llama-3-8B" if a.model == "llama3-8b" else a.model, "global_batch": a.batch * world, "seq_len": P + O,
-                       "prompt_len": P, "output_len": O, "parallelism": f"dp{world}",
+            "config": {"model": "Llama-3-8B" if a.model == "llama3-8b" else a.model,
+                       "global_batch": a.batch * (world // a.tp), "seq_len": a.prompt_len + a.output_len,
+                       "prompt_len": a.prompt_len, "output_len": a.output_len,
+                       "parallelism": f"dp{world // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
                        "graphs": not a.no_graphs, "mixed_prefill": not a.no_mixed,
                        "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap},
             "p50_cr_ready_s": round(p50_ready, 3),
@@ -166,7 +191,8 @@ def main(argv=None):
         except Exception:  # noqa: BLE001
             pass
         print(json.dumps(res), flush=True)
-    engine.shutdown() if hasattr(engine, "shutdown") else None
+    if a.tp == 1:
+        engine.shutdown()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -37,7 +37,7 @@ from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, bl
 from .sampler import Sampler, SamplingParams
 
 
-KIND_STOP, KIND_EAGER, KIND_GRAPH = 0, 1, 2
+KIND_STOP, KIND_EAGER, KIND_GRAPH, KIND_BARRIER = 0, 1, 2, 3
 
 
 class StepSync:
@@ -53,7 +53,7 @@ class StepSync:
     def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0):
         hdr = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt], dtype=torch.int64, device=eng.device)
         self.g.broadcast(hdr, 0)
-        if kind == KIND_STOP:
+        if kind in (KIND_STOP, KIND_BARRIER):
             return
         m = eng.meta
         self.g.broadcast(m.d, 0)
@@ -66,7 +66,7 @@ class StepSync:
         hdr = torch.zeros(8, dtype=torch.int64, device=eng.device)
         self.g.broadcast(hdr, 0)
         kind, T, nt, nl, part, nparts, bucket, npt = hdr.tolist()
-        if kind != KIND_STOP:
+        if kind not in (KIND_STOP, KIND_BARRIER):
             m = eng.meta
             self.g.broadcast(m.d, 0)
             if T:
@@ -615,8 +615,26 @@ class Engine:
             hdr = self.step_sync.recv(self)
             if hdr[0] == KIND_STOP:
                 return
+            if hdr[0] == KIND_BARRIER:
+                self._world_barrier()
+                continue
             self._execute(*hdr)
             self.stats["worker_steps"] += 1
+
+    def sync_point(self):
+        """Device sync + a barrier of the WHOLE world that the TP workers join too
+        (they are parked in ``worker_loop``): the bench's timing brackets."""
+        if self.step_sync is not None and self.step_sync.is_leader:
+            self.step_sync.send(self, KIND_BARRIER, 0, 0, 0, 0, 0, 0)
+        self._world_barrier()
+
+    def _world_barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.barrier()
 
     def shutdown(self):
         if self.step_sync is not None and self.step_sync.is_leader:
