@@ -35,6 +35,7 @@ import torch
 from .attn_meta import MetaBuffers, plan_partitions
 from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, blocks_needed
 from .sampler import Sampler, SamplingParams
+from .tracing import StepTracer, TorchProfileWindow
 
 
 KIND_STOP, KIND_EAGER, KIND_GRAPH, KIND_BARRIER = 0, 1, 2, 3
@@ -235,6 +236,8 @@ class Engine:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.stats = collections.Counter()
+        self.tracer = StepTracer()
+        self.profile_window = TorchProfileWindow()
         import os
 
         tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS") == "1"
@@ -355,18 +358,30 @@ class Engine:
                 or (c.max_decode_gap and self._decode_since_prefill >= c.max_decode_gap))
 
     def step(self) -> list[StepOutput]:
+        """One scheduler step (traced: ``self.tracer`` spans, optional torch.profiler window)."""
+        self.profile_window.before_step()
+        t0 = time.perf_counter()
+        n0d, n0p = self.stats["decode_tokens"], self.stats["prefill_tokens"]
+        kind, out = self._step()
+        self.tracer.record(kind, t0, time.perf_counter(), decode_tokens=self.stats["decode_tokens"] - n0d,
+                           prefill_tokens=self.stats["prefill_tokens"] - n0p, running=len(self.running),
+                           waiting=len(self.waiting))
+        self.profile_window.after_step()
+        return out
+
+    def _step(self):
         if self._want_prefill():
             if self.running and self.cfg.mixed_prefill:
-                out = self._mixed_step()
+                kind, out = "mixed", self._mixed_step()
             else:
-                out = self._prefill_step()
+                kind, out = "prefill", self._prefill_step()
             if out is not None:
                 self._decode_since_prefill = 0
-                return out
+                return kind, out
         if self.running:
             self._decode_since_prefill += 1
-            return self._decode_step()
-        return []
+            return "decode", self._decode_step()
+        return "idle", []
 
     # ---------------------------------------------------------- prefill --
     def _collect_prefill(self, budget: int):

@@ -150,6 +150,18 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
         await resp.write_eof()
         return resp
 
+    async def trace(_):
+        eng = getattr(backend, "engine", None)
+        if eng is None or not hasattr(eng, "tracer"):
+            raise web.HTTPNotFound(text="no engine tracer on this predictor")
+        return web.json_response(eng.tracer.chrome_trace())
+
+    async def trace_summary(_):
+        eng = getattr(backend, "engine", None)
+        if eng is None or not hasattr(eng, "tracer"):
+            raise web.HTTPNotFound(text="no engine tracer on this predictor")
+        return web.json_response({"steps": eng.tracer.summary(), "stats": dict(eng.stats)})
+
     async def feedback(req):
         await req.read()
         return web.json_response({"status": "ok"})
@@ -177,6 +189,8 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
     r.add_post("/api/v1.0/feedback", feedback)
     r.add_post("/api/v1.0/predictions", infer)
     r.add_get("/metrics", prom)
+    r.add_get("/v2/debug/trace", trace)            # Chrome / Perfetto trace of recent engine steps
+    r.add_get("/v2/debug/steps", trace_summary)
     return app
 
 

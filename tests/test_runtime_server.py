@@ -87,7 +87,32 @@ def test_llm_generate_infer_stream(llm_backend):
             assert all(o.status == 200 for o in outs)
             txt = await (await c.get("/metrics")).text()
             assert "mlop_time_to_first_token_seconds_count" in txt and "mlop_generated_tokens_total" in txt
+            # engine step trace (Chrome trace events) and its summary
+            tr = await (await c.get("/v2/debug/trace")).json()
+            kinds = {e["name"] for e in tr["traceEvents"]}
+            assert tr["traceEvents"] and kinds <= {"prefill", "mixed", "decode", "idle"} and "decode" in kinds
+            assert all(e["dur"] >= 0 for e in tr["traceEvents"])
+            summ = await (await c.get("/v2/debug/steps")).json()
+            assert summ["steps"]["decode"]["steps"] > 0 and summ["stats"]["decode_tokens"] > 0
     asyncio.run(go())
+
+
+def test_torch_profile_window(tmp_path):
+    """MLOP_PROFILE_STEPS-style window: torch.profiler around engine steps a..b, Chrome trace written."""
+    import torch
+
+    from mlopamd.models import build_model
+    from mlopamd.models.config import TINY_LLAMA
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+    from mlopamd.runtime.tracing import TorchProfileWindow
+
+    eng = Engine(build_model(TINY_LLAMA, device="cpu", dtype=torch.float32, seed=1),
+                 EngineConfig(max_num_seqs=2, max_model_len=64, num_kv_blocks=16, use_graphs=False))
+    eng.profile_window = TorchProfileWindow("1:3", str(tmp_path))
+    eng.generate([[3, 4, 5]], SamplingParams(max_tokens=5, ignore_eos=True))
+    files = list(tmp_path.glob("engine_steps_1_3_*.json"))
+    assert files and json.loads(files[0].read_text())["traceEvents"]
 
 
 def test_fault_injection_counts_errors(tmp_path):
