@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import asyncio
 import itertools
+import json
 import logging
 import os
 import socket
@@ -327,7 +328,12 @@ class Router:
         session = session or aiohttp.ClientSession()
         try:
             async with session.post(pod.endpoint + path, json=payload) as r:
-                return r.status, await r.json(content_type=None), pod.predictor
+                text = await r.text()
+                try:
+                    body = json.loads(text) if text else {}
+                except ValueError:  # error responses may be plain text
+                    body = {"error": text}
+                return r.status, body, pod.predictor
         finally:
             if own:
                 await session.close()
