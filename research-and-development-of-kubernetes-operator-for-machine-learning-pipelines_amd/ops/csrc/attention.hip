@@ -406,9 +406,14 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
         pf[4 + i] = (short)f2bf(pb[i]);
       }
       l[c] = l[c] * alpha + rs;
+      // rescale O only when some row's running max moved (after the first pairs of a
+      // causal prefill it rarely does): wave-uniform branch, 32 v_mul saved per tile
+      if (__ballot(alpha != 1.f)) {
+#pragma unroll
+        for (int d = 0; d < 8; ++d) o[c][d] *= alpha;
+      }
 #pragma unroll
       for (int d = 0; d < 8; ++d) {
-        o[c][d] *= alpha;
         bf16x8 vf = {va[d][0], va[d][1], va[d][2], va[d][3], vb[d][0], vb[d][1], vb[d][2], vb[d][3]};
         o[c][d] = mfma16(vf, pf, o[c][d]);
       }

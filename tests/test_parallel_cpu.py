@@ -62,6 +62,33 @@ def _tp_engine(cfg_name):
     return {"worker_steps": eng.stats["worker_steps"]}
 
 
+def tp_sync(rank, world):
+    """Leader's sync_point() is a world barrier the parked TP worker joins."""
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    ps = make_parallel_state(tp_size=2)
+    m = build_model(get_config("tiny-llama"), device="cpu", dtype=torch.float32, pstate=ps, seed=4)
+    eng = Engine(m, EngineConfig(max_num_seqs=2, max_num_batched_tokens=32, max_model_len=64, num_kv_blocks=16,
+                                 use_graphs=False))
+    if ps.tp_rank == 0:
+        eng.sync_point()
+        out = eng.generate([[5, 6, 7]], SamplingParams(max_tokens=3, ignore_eos=True))
+        eng.sync_point()
+        eng.shutdown()
+        return {"out": out}
+    eng.worker_loop()
+    return {"worker_steps": eng.stats["worker_steps"]}
+
+
+def test_tp_sync_point_barrier():
+    r0, r1 = run_ranks("tp_sync")
+    assert len(r0["out"][0]) == 3 and r1["worker_steps"] > 0
+
+
 def tp_llama(rank, world):
     return _tp_engine("tiny-llama")
 
