@@ -149,7 +149,7 @@ class LlamaModel:
         return x
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        """[n, H] -> full-vocab logits [n, V] (fp32), gathered over the TP group."""
+        """[n, H] -> full-vocab logits [n, V] in the model dtype (bf16 on GPU: the
+        greedy argmax reads them directly, the sampler upcasts), gathered over TP."""
         lg = linear(hidden, self.lm_head)
-        lg = self.ps.tp.all_gather(lg, dim=-1)
-        return lg.float()
+        return self.ps.tp.all_gather(lg, dim=-1)

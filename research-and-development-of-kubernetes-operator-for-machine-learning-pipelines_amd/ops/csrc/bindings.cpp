@@ -279,8 +279,17 @@ void check_logits(const Tensor& logits) {
 }
 
 void argmax(Tensor out, Tensor logits) {
-  check_logits(logits);
   TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == logits.size(0), "out int64 [n]");
+  if (logits.scalar_type() == at::kBFloat16) {
+    TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
+                "bf16 logits must be [n, V] with unit inner stride and 16-B aligned rows");
+    c10::DeviceGuard g(logits.device());
+    mlop::launch_argmax_bf16(out.data_ptr<int64_t>(), logits.data_ptr(), (int)logits.size(0),
+                             (int)logits.size(1), logits.stride(0), cur_stream());
+    return;
+  }
+  check_logits(logits);
   c10::DeviceGuard g(logits.device());
   mlop::launch_argmax(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)logits.size(0),
                       (int)logits.size(1), logits.stride(0), cur_stream());

@@ -42,6 +42,7 @@ void launch_moe_permute(void* xp, int* offsets, int* src, int* inv, const void* 
 void launch_moe_combine(void* out, const void* y, const int* inv, const float* topw, int T, int k,
                         int H, hipStream_t st);
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st);
+void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, hipStream_t st);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
                    const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);
 

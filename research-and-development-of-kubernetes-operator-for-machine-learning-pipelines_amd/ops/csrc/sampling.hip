@@ -66,6 +66,45 @@ __global__ void __launch_bounds__(kSampleThreads) argmax_kernel(long* __restrict
   if (threadIdx.x == 0) out[blockIdx.x] = bi == 0x7fffffff ? 0 : bi;
 }
 
+// greedy over bf16 logits straight from the LM-head GEMM (no fp32 copy of the
+// [n, V] logits): 8 values per 16-B load; bf16 -> f32 is exact, so ties and the
+// result equal the fp32 path's
+__global__ void __launch_bounds__(kSampleThreads) argmax_bf16_kernel(long* __restrict__ out,
+                                                                    const uint16_t* __restrict__ logits,
+                                                                    int V, long ld) {
+  __shared__ float sv[kSampleThreads / 64];
+  __shared__ int si[kSampleThreads / 64];
+  const uint16_t* row = logits + blockIdx.x * ld;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  const int nv8 = V >> 3;
+  const u32x4* r8 = reinterpret_cast<const u32x4*>(row);
+  for (int j = threadIdx.x; j < nv8; j += blockDim.x) {
+    const u32x4 x = r8[j];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      amax_merge(v, idx, lo_bf(x[k]), 8 * j + 2 * k);
+      amax_merge(v, idx, hi_bf(x[k]), 8 * j + 2 * k + 1);
+    }
+  }
+  for (int j = (nv8 << 3) + threadIdx.x; j < V; j += blockDim.x) amax_merge(v, idx, bf2f(row[j]), j);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(idx, o, 64);
+    amax_merge(v, idx, ov, oi);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sv[wid] = v; si[wid] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bv = sv[0];
+    int bi = si[0];
+    for (int w = 1; w < kSampleThreads / 64; ++w) amax_merge(bv, bi, sv[w], si[w]);
+    out[blockIdx.x] = bi == 0x7fffffff ? 0 : bi;
+  }
+}
+
 __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
     long* __restrict__ out, const float* __restrict__ logits, int V, long ld,
     const float* __restrict__ temps, const int* __restrict__ top_ks,
@@ -197,6 +236,11 @@ __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st) {
   if (n == 0) return;
   argmax_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld);
+}
+
+void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, hipStream_t st) {
+  if (n == 0) return;
+  argmax_bf16_kernel<<<n, kSampleThreads, 0, st>>>(out, (const uint16_t*)logits, V, ld);
 }
 
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,

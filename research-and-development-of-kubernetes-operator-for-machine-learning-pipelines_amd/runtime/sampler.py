@@ -1,8 +1,8 @@
 """Token sampling (K10): greedy, temperature, top-k, top-p.
 
 GPU path: the fused HIP kernel ``torch.ops.mlop.sample`` (per-row top-k select
-+ softmax + top-p + inverse-CDF draw, no full-vocab sort).  Greedy rows use
-the HIP argmax.  CPU path: the same semantics in plain torch (oracle for tests).
++ softmax + top-p + inverse-CDF draw, no full-vocab sort).  Greedy batches use
+the HIP argmax directly on the LM head's bf16 logits (no fp32 copy).  CPU path: the same semantics in plain torch (oracle for tests).
 """
 from __future__ import annotations
 
@@ -75,6 +75,7 @@ class Sampler:
         if getattr(params, "all_greedy", False) or all(p.greedy for p in params[:n]):
             return ops.argmax(logits) if logits.is_cuda else logits.argmax(-1)
         dev = logits.device
+        logits = logits.float()  # the top-k / top-p kernel works on fp32 rows
         temps = torch.tensor([p.temperature for p in params[:n]], dtype=torch.float32)
         ks = torch.tensor([p.top_k for p in params[:n]], dtype=torch.int32)
         ps = torch.tensor([p.top_p for p in params[:n]], dtype=torch.float32)
