@@ -308,6 +308,7 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
   const int kv_end = ctx - ql + last_q + 1;  // exclusive causal limit of the workgroup
   const int n_pairs = (kv_end + 31) >> 5;
   const int n_pages = (kv_end + kBS - 1) / kBS;
+  const int wg_min_pos = ctx - ql + q0;      // position of the workgroup's first query token
   const int r = lane & 15, g4 = lane >> 4;
 
   bf16x8 qf[2][4];
@@ -374,6 +375,7 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
       vb[d] = *reinterpret_cast<const bf16x4*>(sV + PAGE + dim * kBS + c8);
     }
     const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
+    const bool full_pair = pp * 32 + 31 <= wg_min_pos;  // every key of the pair is visible to every row
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
@@ -382,25 +384,35 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
         sa = mfma16(ka[kk], qf[c][kk], sa);
         sb = mfma16(kb[kk], qf[c][kk], sb);
       }
+      // running max kept in RAW score units (scale > 0 preserves order); the scale
+      // folds into the exponent's FMA: p = exp2(s*c - m*c).  VALU, not MFMA, bounds
+      // this loop, so the causal mask is applied only on pairs that cross the
+      // workgroup's diagonal (wave-uniform test).
       float pa[4], pb[4];
-      float mx = kNegBig;
+      if (full_pair) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pa[i] = (tokA + i <= pos_r[c]) ? sa[i] * scale_log2 : -INFINITY;
-        pb[i] = (tokB + i <= pos_r[c]) ? sb[i] * scale_log2 : -INFINITY;
-        mx = fmaxf(mx, fmaxf(pa[i], pb[i]));
+        for (int i = 0; i < 4; ++i) { pa[i] = sa[i]; pb[i] = sb[i]; }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pa[i] = (tokA + i <= pos_r[c]) ? sa[i] : -INFINITY;
+          pb[i] = (tokB + i <= pos_r[c]) ? sb[i] : -INFINITY;
+        }
       }
+      float mx = fmaxf(fmaxf(fmaxf(pa[0], pa[1]), fmaxf(pa[2], pa[3])),
+                       fmaxf(fmaxf(pb[0], pb[1]), fmaxf(pb[2], pb[3])));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m[c], mx);
-      const float alpha = exp2f(m[c] - m_new);
+      const float alpha = exp2f((m[c] - m_new) * scale_log2);
       m[c] = m_new;
+      const float mc = -m_new * scale_log2;
       float rs = 0.f;
       bf16x8 pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        pa[i] = exp2f(pa[i] - m_new);
-        pb[i] = exp2f(pb[i] - m_new);
+        pa[i] = exp2f(fmaf(pa[i], scale_log2, mc));
+        pb[i] = exp2f(fmaf(pb[i], scale_log2, mc));
         rs += pa[i] + pb[i];
         pf[i] = (short)f2bf(pa[i]);
         pf[4 + i] = (short)f2bf(pb[i]);

@@ -2,6 +2,7 @@
 # bench: default + larger concurrency; kernel profile of the default (mixed-step) bench
 source scripts/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+step pytest_k 600 python -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -q -m gpu -x -k "argmax or flash or attention or engine or llama3"
 step b_default 600 python bench.py --steps 100 --warmup 40
 step b_1536 600 python bench.py --steps 100 --warmup 40 --batch 1536
 step b_2048 600 python bench.py --steps 100 --warmup 40 --batch 2048
