@@ -56,6 +56,8 @@ def parse(argv=None):
     ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--save-gemm-table", default=None,
+                    help="after the run, write the per-shape GEMM backend choices measured here to this JSON")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree per replica (config 4: --model llama3-70b --tp 8); "
                          "replicas = world / tp, each TP group's rank 0 schedules")
@@ -98,6 +100,7 @@ def main(argv=None):
     else:
         engine, ready_s, deploy_info = deploy_for_bench(
             model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank, engine_kwargs=ekw)
+    deploy_info["graph_capture_s"] = round(engine.stats.get("graph_capture_ms", 0) / 1e3, 2)
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()
         _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine)
@@ -191,6 +194,10 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
         except Exception:  # noqa: BLE001
             pass
         print(json.dumps(res), flush=True)
+        if a.save_gemm_table:
+            from mlopamd import ops
+
+            ops.save_gemm_table(a.save_gemm_table)
     if a.tp == 1:
         engine.shutdown()
     if world > 1:

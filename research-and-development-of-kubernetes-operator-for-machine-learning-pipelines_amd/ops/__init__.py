@@ -32,6 +32,7 @@ def load(build_if_missing: bool = True) -> bool:
         build()
     torch.ops.load_library(str(_LIB))
     _loaded = True
+    load_gemm_table()
     return True
 
 
@@ -268,6 +269,45 @@ def gemm_add_rmsnorm(x, w, residual, norm_w, eps: float):
         c = min(times, key=times.get)
         _GEMM_CHOICE[key], _GEMM_TIMES[key] = c, times
     return fused(residual) if c in (None, "mlop") else unfused(residual)
+
+
+GEMM_TABLE = Path(os.environ.get("MLOP_GEMM_TABLE", str(Path(__file__).with_name("gemm_table_gfx950.json"))))
+
+
+def load_gemm_table(path: str | os.PathLike | None = None) -> int:
+    """Seed the per-shape backend choice from a table measured earlier on this
+    architecture (a tuning database, like hipBLASLt's own): a predictor then skips
+    re-timing every projection shape during start-up / graph capture.  Shapes not
+    in the table are still timed on first use.  Returns the number of entries."""
+    p = Path(path) if path else GEMM_TABLE
+    if os.environ.get("MLOP_GEMM_TABLE") == "off" or not p.exists():
+        return 0
+    import json
+
+    d = json.loads(p.read_text())
+    n = 0
+    for mb, N, K, epi, choice in d.get("entries", []):
+        if choice in _GEMM_IMPL:
+            _GEMM_CHOICE.setdefault((int(mb), int(N), int(K), int(epi)), choice)
+            n += 1
+    return n
+
+
+def save_gemm_table(path: str | os.PathLike | None = None) -> str:
+    """Write the choices measured so far (merged with an existing table)."""
+    import json
+
+    p = Path(path) if path else GEMM_TABLE
+    entries = {}
+    if p.exists():
+        for e in json.loads(p.read_text()).get("entries", []):
+            entries[tuple(e[:4])] = e[4]
+    for k, c in _GEMM_CHOICE.items():
+        if k in _GEMM_TIMES:  # only shapes actually timed in this process
+            entries[k] = c
+    rows = [[*k, c] for k, c in sorted(entries.items())]
+    p.write_text(json.dumps({"arch": "gfx950", "entries": rows}, indent=0) + "\n")
+    return str(p)
 
 
 def gemm_choices() -> list:

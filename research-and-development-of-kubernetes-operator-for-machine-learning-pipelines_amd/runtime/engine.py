@@ -663,14 +663,15 @@ class Engine:
         stream.wait_stream(torch.cuda.current_stream(self.device))
         self.graph_pool = torch.cuda.graph_pool_handle()
         empty = np.zeros(0, dtype=np.int32)
+        t0 = time.perf_counter()
         with torch.cuda.stream(stream):
-            for b in sorted(self.buckets, reverse=True):
+            for bi, b in enumerate(sorted(self.buckets, reverse=True)):
                 self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=b)
                 self.meta.upload(b, b)
                 part, nparts = plan_partitions(b, m.n_kv, self.max_model_len)
                 meta = self.meta.meta(b, b, b, part, nparts)
                 ids = self.meta.ids_d[:b]
-                for _ in range(2):  # warm-up (allocator, lazy init)
+                for _ in range(2 if bi == 0 else 1):  # warm-up (allocator, autotune, lazy init)
                     m.logits(m.forward(ids, meta, self.kv)[meta.logits_idx])
                 stream.synchronize()
                 g = torch.cuda.CUDAGraph()
@@ -679,6 +680,7 @@ class Engine:
                 self.graphs[b] = (g, logits)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
+        self.stats["graph_capture_ms"] = int(1e3 * (time.perf_counter() - t0))
 
     # ------------------------------------------------------ offline API --
     def generate(self, prompts, params: SamplingParams | list | None = None):
