@@ -100,7 +100,8 @@ def main(argv=None):
     else:
         engine, ready_s, deploy_info = deploy_for_bench(
             model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank, engine_kwargs=ekw)
-    deploy_info["graph_capture_s"] = round(engine.stats.get("graph_capture_ms", 0) / 1e3, 2)
+    for k in ("model_build_ms", "kv_alloc_ms", "graph_capture_ms"):  # start-up breakdown
+        deploy_info[k] = engine.stats.get(k, 0)
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()
         _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine)

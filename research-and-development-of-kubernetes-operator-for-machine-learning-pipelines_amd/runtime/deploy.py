@@ -18,8 +18,14 @@ from .engine import Engine, EngineConfig
 
 def build_engine(model: str = "llama3-8b", device="cuda", seed: int = 0, tp_state=None,
                  dtype=torch.bfloat16, **engine_kwargs) -> Engine:
+    t0 = time.perf_counter()
     m = build_model(model, device=device, dtype=dtype, pstate=tp_state, seed=seed)
-    return Engine(m, EngineConfig(**engine_kwargs))
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    eng = Engine(m, EngineConfig(**engine_kwargs))
+    eng.stats["model_build_ms"] = int(1e3 * (t1 - t0))
+    return eng
 
 
 def deploy_for_bench(model: str, device, use_operator: bool = True, seed: int = 0,

@@ -124,6 +124,8 @@ class EngineConfig:
     num_kv_blocks: int | None = None       # None: size from kv_cache_bytes / free HBM
     kv_cache_bytes: int | None = None
     gpu_memory_utilization: float = 0.90
+    kv_fraction: float = 0.5  # pages for this share of max_num_seqs x max_model_len (mean context;
+                              # preemption covers the tail) - same policy as controller/placement.py
     use_graphs: bool = True
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024)
     prefill_min_batch: int = 1
@@ -202,7 +204,11 @@ class Engine:
 
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=tp.handle)
             nb = int(t.item())
+        t_kv = time.perf_counter()
         self.kv = KVCache(mc.num_layers, nb, model.n_kv, mc.head_dim, self.device, model.dtype)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        kv_alloc_ms = int(1e3 * (time.perf_counter() - t_kv))
         self.alloc = BlockAllocator(nb)
         self.max_blocks_per_seq = blocks_needed(self.max_model_len)
         self.buckets = sorted(b for b in cfg.graph_buckets if b <= cfg.max_num_seqs) or [cfg.max_num_seqs]
@@ -236,6 +242,7 @@ class Engine:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.stats = collections.Counter()
+        self.stats["kv_alloc_ms"] = kv_alloc_ms
         self.tracer = StepTracer()
         self.profile_window = TorchProfileWindow()
         import os
@@ -255,7 +262,8 @@ class Engine:
             budget = int(max(free - reserve, 2**30))
         else:
             budget = 64 * 2**20
-        need = self.cfg.max_num_seqs * blocks_needed(min(self.cfg.max_model_len, mc.max_position)) + 1
+        need = int(self.cfg.kv_fraction * self.cfg.max_num_seqs *
+                   blocks_needed(min(self.cfg.max_model_len, mc.max_position))) + 2
         nb = blocks_for_budget(budget, mc.num_layers, m.n_kv, mc.head_dim)
         return int(min(nb, need))
 

@@ -5,8 +5,7 @@ Device side: one K and one V tensor per layer, pages of 16 tokens:
   v[layer] : [num_blocks, Hkv, D, 16]   (dim-major:  A operand of O^T = V^T.P^T)
 allocated ZEROED once (the attention kernel relies on finite unused slots).
 
-Host side: ``BlockAllocator`` hands out page ids (free-list, O(1) alloc/free);
-the native C++ allocator (``mlopamd.runtime.native``) is used when built.
+Host side: ``BlockAllocator`` hands out page ids (free-list, O(1) alloc/free).
 """
 from __future__ import annotations
 
