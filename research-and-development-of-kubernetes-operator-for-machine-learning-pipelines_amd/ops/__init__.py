@@ -305,8 +305,8 @@ def save_gemm_table(path: str | os.PathLike | None = None) -> str:
     for k, c in _GEMM_CHOICE.items():
         if k in _GEMM_TIMES:  # only shapes actually timed in this process
             entries[k] = c
-    rows = [[*k, c] for k, c in sorted(entries.items())]
-    p.write_text(json.dumps({"arch": "gfx950", "entries": rows}, indent=0) + "\n")
+    rows = [json.dumps([*k, c]) for k, c in sorted(entries.items())]
+    p.write_text('{"arch": "gfx950", "entries": [\n' + ",\n".join(rows) + "\n]}\n")
     return str(p)
 
 
