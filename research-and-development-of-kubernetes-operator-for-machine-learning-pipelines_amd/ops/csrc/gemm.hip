@@ -348,20 +348,210 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
                                m_tiles, splits);
 }
 
-struct Plan {
-  int BM, BN, splits, k_chunk, m_tiles, variant;
-};
-
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong 256x256 GEMM (cdna_hip_programming.md "The 256^2 8-phase template"):
+// 8 waves = 2 wave GROUPS (A halves) x 4 column strips, 128x64 outputs per wave.
+// Each K-tile (BK = 64) is 4 phases, one 64x32 quadrant x K=64 (16 MFMAs) each:
+//     [ds_read the quadrant's fragments | issue LDS-DMA of the NEXT K-tile]
+//     s_barrier; lgkmcnt(0); setprio(1) 16 x MFMA setprio(0); s_barrier
+// Group 1 executes one extra barrier up front, so it is always one half-phase
+// behind group 0: while one group's waves issue LDS reads / DMA, the other
+// group's waves (one per SIMD each) keep the matrix cores busy — the barrier
+// and LDS latency that idles a single-group loop (27% SQ_WAIT_ANY in
+// profiles/r01_gemm_pmc.md) is overlapped by the partner group instead.
+// Two LDS buffers (K-tile parity, 2 x 64 KB), each wave retires its own DMA
+// of K-tile t+1 with vmcnt(0) in phase 3 of K-tile t; reads of buffer t&1 start
+// only after the barrier that follows every wave's retirement, and DMA into a
+// buffer starts only after every read of its previous K-tile has retired
+// (phase-window accounting in the comments below).  Quadrant order (0,0)
+// (0,1) (1,1) (1,0) reloads the A sub-tile twice and the B sub-tiles once.
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
+    const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
+    uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int BUF = (BM + BN) * kBK;  // bf16 per K-tile buffer (64 KB)
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, wc = wid & 3;
+  const int G = gridDim.x, Lb = blockIdx.x;
+  const int q = G >> 3, rr = G & 7, xcd = Lb & 7, slot = Lb >> 3;
+  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+  // tile order inside an XCD's contiguous range: bands of group_m m-tiles, m fastest
+  // within a band (a B panel is reused by group_m consecutive tiles while L2-resident)
+  const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
+  const int gm_here = min(group_m, m_tiles - band * group_m);
+  const int m0 = (band * group_m + in_band % gm_here) * BM, n0 = (in_band / gm_here) * BN;
+  const int nk = K / kBK;
+
+  // DMA sources: half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127,
+  // 3 B rows 128-255) = 16 pieces of 8 rows x 128 B; wave w moves pieces w, w+8
+  const int prow = lane >> 3;
+  const uint16_t* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row inside the 256-row operand tile
+      const int ch = (lane & 7) ^ swz(r);
+      src[h][i] = h < 2 ? A + (size_t)min(m0 + r, M - 1) * lda + ch * 8
+                        : B + (size_t)min(n0 + r, N - 1) * ldb + ch * 8;
+    }
+  auto issue_half = [&](int buf, int h, int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + ((h & 1) * 128 + (wid + 8 * i) * 8) * kBK;
+      __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
+    }
+  };
+  auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
+    const uint16_t* sA = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = grp * 128 + mi * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        fa[i][kk] = *reinterpret_cast<const bf16x8*>(sA + r * kBK + ((ch ^ swz(r)) << 3));
+      }
+    }
+  };
+  auto read_b = [&](int buf, int nj, bf16x8 (&fb)[2][2]) {
+    const uint16_t* sB = smem + buf * BUF + BM * kBK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wc * 64 + nj * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        fb[j][kk] = *reinterpret_cast<const bf16x8*>(sB + r * kBK + ((ch ^ swz(r)) << 3));
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+  };
+
+  // prologue: K-tile 0 -> buffer 0, visible to all; then stagger the groups
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
+  wait_vmcnt<0>();
+  raw_barrier();
+  if (grp == 1) raw_barrier();
+
+  // Window accounting (barriers numbered along group 0; group 1 runs one behind):
+  // DMA of K-tile t+1 into buffer (t+1)&1 is issued in phases 0-1 of t, after the
+  // last reads of K-tile t-1 from that buffer (group 1, phase 2 of t-1) retired;
+  // each wave retires its own DMA in phase 3 of t, and K-tile t+1 is first read
+  // one barrier after the last group's retirement.
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    const bool more = t + 1 < nk;
+    read_b(cur, 0, fb0);
+    read_a(cur, 0, fa);
+    if (more) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
+    phase_mma(0, 0, fa, fb0);
+    read_b(cur, 1, fb1);
+    if (more) { issue_half(nxt, 2, t + 1); issue_half(nxt, 3, t + 1); }
+    phase_mma(0, 1, fa, fb1);
+    read_a(cur, 1, fa);
+    phase_mma(1, 1, fa, fb1);
+    if (more) wait_vmcnt<0>();
+    phase_mma(1, 0, fa, fb0);
+  }
+  if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
+  __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
+
+  // epilogue: each wave stages its 128 x 64 (or 128 x 32 after SiLU.mul) bf16 tile
+  constexpr int OW = EPI == EPI_NONE ? 64 : 32;
+  constexpr int LD = OW + 8;
+  uint16_t* sC = smem + wid * 128 * LD;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i * 16 + 4 * (lane >> 4) + r;
+      if constexpr (EPI == EPI_NONE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sC[row * LD + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+      } else {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
+          sC[row * LD + jp * 16 + (lane & 15)] = f2bf(silu_bf(g) * bf2f(f2bf(u)));
+        }
+      }
+    }
+  __syncthreads();
+  constexpr int CPR = OW / 8;  // 16-B chunks per staged row
+  const int out_col0 = EPI == EPI_NONE ? n0 + wc * 64 : (n0 + wc * 64) / 2;
+  const int out_n = EPI == EPI_NONE ? N : N / 2;
+#pragma unroll
+  for (int it = 0; it < 128 * CPR / 64; ++it) {
+    const int c = it * 64 + lane;
+    const int row = c / CPR, cc = (c % CPR) * 8;
+    const int gm = m0 + grp * 128 + row, gn = out_col0 + cc;
+    if (gm < M && gn < out_n)
+      *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
+  }
+}
+
+template <int EPI>
+static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
+                   int N, int K, hipStream_t st) {
+  constexpr size_t ring = 2ull * (256 + 256) * kBK * 2;
+  constexpr size_t epi = 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
+  constexpr size_t lds = ring > epi ? ring : epi;
+  static_assert(lds <= 163840, "LDS budget");
+  auto kern = gemm_pp_kernel<EPI>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int gx = (N + 255) / 256, gy = (M + 255) / 256;
+  static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
+  const int gm = std::max(1, std::min(group_m, gy));
+  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm);
+}
+
+struct Plan {
+  int BM, BN, splits, k_chunk, m_tiles, variant;
+};
+
+
 // Tile choice by the (per-group) row count:
 //   M <= 64 / 128: narrow tiles, many WGs (weight streaming);  M <= 256: the whole
 //   batch in one tile (weights read once), BN by how many N tiles fill the chip;
 //   large M: variant 0 = 256x128 (3-stage ring), 1 = 256x256 (2-stage, 128x64 per
-//   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs.
+//   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs,
+//   3 (default) = 256x256 two-group ping-pong (gemm_pp_kernel).
 static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {
   Plan p{};
   p.variant = 0;
@@ -373,11 +563,16 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     p.BM = 256;
     p.BN = ((N + 127) / 128 >= bn_min_tiles) ? 128 : 64;
   } else {
-    static const int big = env_int("MLOP_GEMM_BIG_VARIANT", 0);
+    static const int big = env_int("MLOP_GEMM_BIG_VARIANT", 3);
     static const int big_min_m = env_int("MLOP_GEMM_BIG_MIN_M", 1024);
     p.BM = 256;
     p.BN = 128;
-    if (big && mrows >= big_min_m && !grouped) { p.BN = 256; p.variant = big; }
+    static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 192);
+    const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+    if (big && mrows >= big_min_m && !grouped && (big != 3 || (K % kBK == 0 && t256 >= pp_min_tiles))) {
+      p.BN = 256;
+      p.variant = big;
+    }
   }
   const int n_tiles = (N + p.BN - 1) / p.BN;
   const int real_m_tiles = (M + p.BM - 1) / p.BM;
@@ -407,6 +602,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
   else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
   else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
   else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
+  else if (!GROUPED && p.variant == 3 && p.splits == 1) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st);
   else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
   else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
 #undef MLOP_GEMM

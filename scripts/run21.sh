@@ -1,0 +1,12 @@
+#!/bin/bash
+# PMC counters of the ping-pong GEMM vs hipBLASLt (M=4096 qkv and gate_up)
+source scripts/gpu_check.sh
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+PMC1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES"
+for sh in 4096,6144,4096 4096,28672,4096; do
+  for be in mlop hipblaslt; do
+    export SHAPE=$sh BACKEND=$be ITERS=10
+    tag=pp_$(echo $sh | tr , x)_$be
+    step pmc_$tag 300 rocprofv3 --pmc $PMC1 --kernel-trace --stats -d gpurun_out/pmc_$tag -o pmc -- python3 scripts/gemm_one.py
+  done
+done

@@ -217,12 +217,17 @@ def test_sample_matches_reference(gpu):
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (7, 6144, 4096), (64, 4096, 14336),
                                    (128, 1280, 1024), (256, 4096, 4096), (256, 6144, 4096),
-                                   (300, 1024, 512), (1500, 4096, 4096), (1000, 16032, 1024)])
+                                   (300, 1024, 512), (1500, 4096, 4096), (1000, 16032, 1024),
+                                   (2048, 6144, 4096), (1100, 4352, 1024), (4096, 4096, 64), (3000, 1000, 512)])
 def test_gemm(gpu, M, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
-    y = ops.gemm(x, w)
+    ops.GEMM_BACKEND = "mlop"  # the hand-written kernel, whatever the autotuner would pick
+    try:
+        y = ops.gemm(x, w)
+    finally:
+        ops.GEMM_BACKEND = "auto"
     exp = (x.float() @ w.float().t())
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
 
@@ -247,14 +252,19 @@ def test_gemm_add_rmsnorm(gpu, M, N, K):
         close(out, exp_out, atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("M,I,K", [(1, 14336, 4096), (37, 3584, 4096), (256, 14336, 4096), (900, 512, 256)])
+@pytest.mark.parametrize("M,I,K", [(1, 14336, 4096), (37, 3584, 4096), (256, 14336, 4096), (900, 512, 256),
+                                   (2048, 14336, 4096), (1300, 640, 512)])
 def test_gemm_silu_mul(gpu, M, I, K):
     torch.manual_seed(I)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     g = (0.05 * torch.randn(I, K, device=gpu)).to(bf)
     u = (0.05 * torch.randn(I, K, device=gpu)).to(bf)
     w = ops.interleave_gate_up(g, u)
-    y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
+    finally:
+        ops.GEMM_BACKEND = "auto"
     gu = (x.float() @ torch.cat([g, u]).float().t()).to(bf)
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
