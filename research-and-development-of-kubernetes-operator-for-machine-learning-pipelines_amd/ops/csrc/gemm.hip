@@ -457,33 +457,48 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     raw_barrier();
   };
 
-  // prologue: K-tile 0 -> buffer 0, visible to all; then stagger the groups
+  // LDS-DMA schedule (barriers numbered along group 0; group 1 runs one behind):
+  //   A(t+1) -> buffer (t+1)&1 in phase 1 of t   (after the last A reads of t-1 retired)
+  //   B(t+2) -> buffer t&1     in phase 3 of t   (after B1(t), the last B read of t, retired)
+  //   retire B(t+1) in phase 2 of t (vmcnt(4): A(t+1) stays in flight), read B0(t+1) in
+  //   phase 3 of t into the other B0 register set; retire A(t+1) in phase 3 (vmcnt(4):
+  //   B(t+2) stays in flight), read it from phase 0 of t+1.  Every read happens at least
+  //   one barrier after the slower group's retirement; every DMA is issued at least one
+  //   barrier after the last read of its destination retired.  Per phase a wave issues
+  //   8 / 4+4 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
-  wait_vmcnt<0>();
+  if (nk > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
+  if (nk > 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
   raw_barrier();
-  if (grp == 1) raw_barrier();
+  bf16x8 fa[4][2], fb1[2][2], fbA[2][2], fbB[2][2];
+  read_b(0, 0, fbA);
+  if (grp == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
 
-  // Window accounting (barriers numbered along group 0; group 1 runs one behind):
-  // DMA of K-tile t+1 into buffer (t+1)&1 is issued in phases 0-1 of t, after the
-  // last reads of K-tile t-1 from that buffer (group 1, phase 2 of t-1) retired;
-  // each wave retires its own DMA in phase 3 of t, and K-tile t+1 is first read
-  // one barrier after the last group's retirement.
-  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
-  for (int t = 0; t < nk; ++t) {
+  auto ktile = [&](int t, bf16x8 (&fb0)[2][2], bf16x8 (&fb0n)[2][2]) {
     const int cur = t & 1, nxt = cur ^ 1;
-    const bool more = t + 1 < nk;
-    read_b(cur, 0, fb0);
-    read_a(cur, 0, fa);
-    if (more) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
+    const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
+    read_a(cur, 0, fa);                                  // phase 0: quadrant (0,0)
     phase_mma(0, 0, fa, fb0);
-    read_b(cur, 1, fb1);
-    if (more) { issue_half(nxt, 2, t + 1); issue_half(nxt, 3, t + 1); }
+    read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
+    if (m1) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
     phase_mma(0, 1, fa, fb1);
-    read_a(cur, 1, fa);
+    read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
+    if (m1) wait_vmcnt<4>();
     phase_mma(1, 1, fa, fb1);
-    if (more) wait_vmcnt<0>();
+    if (m1) read_b(nxt, 0, fb0n);                        // phase 3: quadrant (1,0)
+    if (m2) {
+      issue_half(cur, 2, t + 2);
+      issue_half(cur, 3, t + 2);
+      wait_vmcnt<4>();
+    } else {
+      wait_vmcnt<0>();
+    }
     phase_mma(1, 0, fa, fb0);
+  };
+  for (int t = 0; t < nk; t += 2) {
+    ktile(t, fbA, fbB);
+    if (t + 1 < nk) ktile(t + 1, fbB, fbA);
   }
   if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
   __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
