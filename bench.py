@@ -41,11 +41,12 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--batch", type=int, default=1024,
-                    help="concurrent requests per GPU (288 GB HBM holds their 64 GB of KV pages)")
+    ap.add_argument("--batch", type=int, default=2048,
+                    help="concurrent requests per GPU: 288 GB of HBM holds their ~100 GB of KV pages, and "
+                         "~4k-row mixed steps keep the MFMA GEMMs near their large-M rate")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--output-len", type=int, default=256)
-    ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--max-model-len", type=int, default=1024)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--prefill-min-batch", type=int, default=4)
     ap.add_argument("--max-decode-gap", type=int, default=24)
@@ -53,6 +54,8 @@ def parse(argv=None):
     ap.add_argument("--no-mixed", action="store_true",
                     help="separate prefill steps instead of prompt chunks riding in the decode step")
     ap.add_argument("--mixed-min-chunk", type=int, default=64)
+    ap.add_argument("--no-ramp", dest="ramp", action="store_false",
+                    help="start warmup right after submitting the first cohort (prefill-heavy first steps)")
     ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
@@ -131,6 +134,18 @@ def main(argv=None):
                 new_request(O)
         return gen
 
+    # ramp (untimed, not counted as warmup): the first cohort's prompts are all
+    # admitted and prefilled, so the W warmup + K timed steps see the steady-state
+    # mix (each step: every running sequence's decode token + the prompt chunks of
+    # the requests that replaced the ones that finished) whatever W the caller picks
+    ramp_cap = 4 * (a.batch * P) // max(1, a.max_batched_tokens) + 64
+    ramp = 0
+    backlog = max(a.prefill_min_batch, 2 * a.batch // max(1, O))  # ~2 steps of arrivals
+    while a.ramp and ramp < ramp_cap and (engine.stats["prefill_tokens"] < a.batch * P
+                                          or len(engine.waiting) > backlog):
+        run_steps(1)
+        ramp += 1
+    deploy_info["ramp_steps"] = ramp
     run_steps(a.warmup)
     engine.sync_point()  # device sync + world barrier (TP workers join it)
     s0 = dict(engine.stats)

@@ -4,7 +4,7 @@ Flattened ragged batches (every scheduled token of every sequence in one
 [T, H] matrix, vLLM-style) so prefill chunks and decode tokens share one
 forward.  Per layer:
 
-  add_rmsnorm -> QKV GEMM -> rope_cache (RoPE + paged KV write) -> paged_attention
+  add_rmsnorm -> QKV GEMM + RoPE + paged KV write (one kernel for M > 256) -> paged_attention
   -> O GEMM -> [TP all-reduce] -> add_rmsnorm -> gate_up GEMM -> silu_mul
   -> down GEMM -> [TP all-reduce]
 
@@ -131,8 +131,8 @@ class LlamaModel:
         residual = h
         x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         for i, L in enumerate(self.layers):
-            qkv = linear(x, L["qkv"])
-            q = ops.rope_cache(qkv, meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i], self.n_q)
+            q = ops.qkv_rope_cache(x, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i],
+                                   self.n_q)
             a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
             if tp.size == 1:

@@ -271,6 +271,57 @@ def gemm_add_rmsnorm(x, w, residual, norm_w, eps: float):
     return fused(residual) if c in (None, "mlop") else unfused(residual)
 
 
+EPI_ROPE = 3  # QKV projection + RoPE + paged-cache stores in the GEMM epilogue
+
+
+def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads: int,
+                   q_out: torch.Tensor | None = None):
+    """q_out <- RoPE(x @ Wq^T); k_cache / v_cache[slot] <- RoPE(x @ Wk^T), x @ Wv^T.
+
+    On GPU the MFMA GEMM does the rotation and the cache scatter from its LDS-staged
+    C tile (one launch, no [T, (Hq+2Hkv)D] round trip through HBM) when the M of the
+    step takes whole-head tiles (M > 256); the per-shape choice against hipBLASLt +
+    rope_cache is timed like every other projection (key epi = EPI_ROPE)."""
+    T = x.shape[0]
+    D = k_cache.shape[3]
+    if not x.is_cuda:
+        return rope_cache(gemm(x, w), positions, cos_sin, slots, k_cache, v_cache, n_q_heads, q_out)
+    _need_gpu()
+    x2 = x if (x.stride(-1) == 1 and x.stride(0) % 8 == 0) else x.contiguous()
+    M, K = x2.shape
+    N = w.shape[0]
+    q_out = torch.empty(T, n_q_heads, D, dtype=x.dtype, device=x.device) if q_out is None else q_out
+
+    def fused():
+        if not torch.ops.mlop.gemm_rope_cache(q_out, k_cache, v_cache, x2, w, positions, cos_sin, slots):
+            raise RuntimeError("fused QKV+RoPE tiling not applicable")
+        return q_out
+
+    def unfused():
+        return rope_cache(gemm(x2, w), positions, cos_sin, slots, k_cache, v_cache, n_q_heads, q_out)
+
+    if GEMM_BACKEND == "hipblaslt" or not torch.ops.mlop.gemm_rope_supported(M, N, K):
+        return unfused()
+    if GEMM_BACKEND == "mlop":
+        return fused()
+    key = (_mbucket(M), N, K, EPI_ROPE)
+    c = _GEMM_CHOICE.get(key)
+    if c is None and not torch.cuda.is_current_stream_capturing():
+        times = {}
+        for name, fn in (("mlop", fused), ("hipblaslt", unfused)):
+            fn()  # re-writes the same cache slots with the same values: idempotent
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                fn()
+            e.record()
+            e.synchronize()
+            times[name] = s.elapsed_time(e) / 3
+        c = min(times, key=times.get)
+        _GEMM_CHOICE[key], _GEMM_TIMES[key] = c, times
+    return fused() if c in (None, "mlop") else unfused()
+
+
 GEMM_TABLE = Path(os.environ.get("MLOP_GEMM_TABLE", str(Path(__file__).with_name("gemm_table_gfx950.json"))))
 
 

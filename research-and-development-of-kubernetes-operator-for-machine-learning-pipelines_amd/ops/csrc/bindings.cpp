@@ -201,6 +201,38 @@ void gemm(Tensor out, Tensor a, Tensor w, Tensor ws, int64_t epi) {
                     (int)out.stride(0), wsp, wsn, (int)M, (int)N, (int)K, (int)epi, cur_stream());
 }
 
+// QKV projection with RoPE + paged-cache stores in the GEMM epilogue; false = this M
+// does not take the fused tiling (caller runs gemm + rope_cache)
+bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor w, Tensor pos,
+                     Tensor cos_sin, Tensor slots) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(q_out, "q_out"); check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache"); check_i32(pos, "pos"); check_i32(slots, "slots");
+  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous(),
+              "cos_sin f32");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && K % 64 == 0, "w [N, K], K % 64");
+  TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "ranks");
+  const int64_t Hq = q_out.size(1), D = q_out.size(2), Hkv = k_cache.size(1), BS = k_cache.size(2);
+  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
+                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
+              "head_dim 128; k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D && q_out.size(0) == M, "qkv width / q_out rows");
+  TORCH_CHECK(pos.numel() == M && slots.numel() == M, "pos/slots length");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin [max_pos, D]");
+  c10::DeviceGuard g(a.device());
+  mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
+                   (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                   slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
+  return mlop::launch_gemm_rope(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)M, (int)N, (int)K,
+                                re, cur_stream());
+}
+
+bool gemm_rope_supported(int64_t M, int64_t N, int64_t K) {
+  return mlop::gemm_rope_supported((int)M, (int)N, (int)K);
+}
+
 // out = rmsnorm(residual += a . w^T) * norm_w through the split-K path; false = not taken
 bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor norm_w, Tensor ws,
                       double eps) {
@@ -347,6 +379,9 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
+  m.def("gemm_rope_supported(int M, int N, int K) -> bool", &gemm_rope_supported);
+  m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
+        "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
   m.def("grouped_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int max_rows, "
         "int epi) -> ()");
@@ -384,6 +419,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);
+  m.impl("gemm_rope_cache", &gemm_rope_cache);
   m.impl("moe_route", &moe_route);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);

@@ -29,6 +29,8 @@
 // Epilogues (fp32 LDS copy of the tile, 16-B coalesced stores):
 //   EPI_NONE      C = bf16(acc)
 //   EPI_SILU_MUL  B rows gate/up interleaved in groups of 16, C[:, j] = silu(g_j) * u_j (N/2 cols)
+//   EPI_ROPE      QKV projection: RoPE on q/k heads + q_out / paged K,V cache stores from the
+//                 staged tile (RopeEpi, launch.h); needs whole 128-wide heads per staged chunk
 // Grouped mode (MoE K13): A rows sorted by expert, offsets[e]..offsets[e+1];
 // B = W[e] ([E, N, K]); blockIdx.y enumerates (expert, m-tile) pairs on device.
 #include "common.h"
@@ -36,7 +38,7 @@
 
 namespace mlop {
 
-enum { EPI_NONE = 0, EPI_SILU_MUL = 1 };
+enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3 };
 constexpr int kBK = 64;
 constexpr int kStages = 3;
 
@@ -51,11 +53,96 @@ __device__ __forceinline__ float silu_bf(float g) {
   return bf2f(f2bf(gb / (1.f + __expf(-gb))));
 }
 
+// RoPE / paged-cache stores of `nheads` consecutive 128-wide heads of a staged 256-row
+// C tile (EPI_ROPE).  `at(r, c)` returns the bf16-rounded projection output of tile row r,
+// column c (column 0 = first column of head `head0`), so the math is rope_cache_kernel's
+// on the same bf16 inputs.  Latency-shaped: every per-row index (position, slot) and the
+// cos/sin values a thread needs are loaded up front in one batch (the accumulators are
+// dead by now, so the registers are free), then the heads are rotated and stored; rows
+// >= `rows` are skipped.
+template <int NT, typename At>
+__device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nheads, int m0, int rows,
+                                                const RopeEpi& re, int tid) {
+  constexpr int D = 128, HALF = 64, BM = 256;
+  constexpr int QK = BM * (HALF / 8) / NT;  // (row, 8-column) items per thread, q/k heads
+  // v heads: lane -> row, so one store instruction writes a dim of 64 consecutive rows
+  // (a prefill chunk's consecutive slots: 16 tokens = one contiguous 32-B run of the
+  // dim-major [NB, Hkv, D, BS] page instead of 64 scattered 2-B writes)
+  constexpr int VD = D / (NT / BM);          // dims per thread
+  const int cq = (tid & 7) * 8, rq = tid >> 3;       // q/k item k: row rq + k * NT/8
+  const int rv = tid % BM, dv0 = (tid / BM) * VD;
+  const int n_rope = re.Hq + re.Hkv, n_all = re.Hq + 2 * re.Hkv;
+  const bool any_rope = head0 < n_rope, any_k = head0 + nheads > re.Hq && head0 < n_rope;
+  const bool any_v = head0 + nheads > n_rope;
+  int slot_q[QK], slot_v = -1;
+  float4 cs[QK][4];
+  if (any_rope) {
+    int p[QK];
+#pragma unroll
+    for (int k = 0; k < QK; ++k) {
+      const int r = rq + k * (NT / 8);
+      p[k] = r < rows ? re.pos[m0 + r] : 0;
+      slot_q[k] = (any_k && r < rows) ? re.slots[m0 + r] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < QK; ++k) {
+      const float4* row = reinterpret_cast<const float4*>(re.cos_sin + (size_t)p[k] * D);
+      cs[k][0] = row[cq / 4];
+      cs[k][1] = row[cq / 4 + 1];
+      cs[k][2] = row[(HALF + cq) / 4];
+      cs[k][3] = row[(HALF + cq) / 4 + 1];
+    }
+  }
+  if (any_v && rv < rows) slot_v = re.slots[m0 + rv];
+  for (int hh = 0; hh < nheads; ++hh) {
+    const int head = head0 + hh;
+    if (head >= n_all) break;
+    if (head < n_rope) {
+#pragma unroll
+      for (int k = 0; k < QK; ++k) {
+        const int r = rq + k * (NT / 8);
+        if (r >= rows) continue;
+        uint16_t* dst;
+        if (head < re.Hq) {
+          dst = re.q_out + ((size_t)(m0 + r) * re.Hq + head) * D;
+        } else {
+          const int slot = slot_q[k];
+          if (slot < 0) continue;
+          dst = re.k_cache + (((size_t)(slot / re.BS) * re.Hkv + (head - re.Hq)) * re.BS + slot % re.BS) * D;
+        }
+        const float cc[8] = {cs[k][0].x, cs[k][0].y, cs[k][0].z, cs[k][0].w,
+                             cs[k][1].x, cs[k][1].y, cs[k][1].z, cs[k][1].w};
+        const float ss[8] = {cs[k][2].x, cs[k][2].y, cs[k][2].z, cs[k][2].w,
+                             cs[k][3].x, cs[k][3].y, cs[k][3].z, cs[k][3].w};
+        u32x4 oa, ob;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x0 = at(r, hh * D + cq + 2 * j), x1 = at(r, hh * D + cq + 2 * j + 1);
+          const float y0 = at(r, hh * D + HALF + cq + 2 * j), y1 = at(r, hh * D + HALF + cq + 2 * j + 1);
+          oa[j] = pack2(x0 * cc[2 * j] - y0 * ss[2 * j], x1 * cc[2 * j + 1] - y1 * ss[2 * j + 1]);
+          ob[j] = pack2(y0 * cc[2 * j] + x0 * ss[2 * j], y1 * cc[2 * j + 1] + x1 * ss[2 * j + 1]);
+        }
+        *reinterpret_cast<u32x4*>(dst + cq) = oa;
+        *reinterpret_cast<u32x4*>(dst + HALF + cq) = ob;
+      }
+    } else {
+      const int kh = head - n_rope;
+      if (slot_v >= 0) {
+        uint16_t* dst = re.v_cache + (((size_t)(slot_v / re.BS) * re.Hkv + kh) * D + dv0) * re.BS +
+                        slot_v % re.BS;
+#pragma unroll 16
+        for (int j = 0; j < VD; ++j) dst[j * re.BS] = f2bf(at(rv, hh * D + dv0 + j));
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES = 3, bool SETPRIO = false>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, float* __restrict__ ws, int M, int N, int K, int k_chunk,
-    const int* __restrict__ offsets, int n_groups, int n_tiles_x, int m_tiles_y, int n_splits) {
+    const int* __restrict__ offsets, int n_groups, int n_tiles_x, int m_tiles_y, int n_splits,
+    RopeEpi re) {
   constexpr int NW = WM * WN, T = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -198,7 +285,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
         }
       }
     __syncthreads();
-    if constexpr (EPI == EPI_NONE) {
+    if constexpr (EPI == EPI_ROPE) {
+      static_assert(EW == 128, "EPI_ROPE stages one whole head per chunk");
+      static_assert(BM == 256, "EPI_ROPE tiles are 256 rows");
+      auto at = [&](int r, int c) { return bf2f(f2bf(sC[r * LDC + c])); };
+      rope_tile_store<T>(at, (n0 + c0) / 128, 1, m0, rows_here, re, tid);
+    } else if constexpr (EPI == EPI_NONE) {
       constexpr int VPR = EW / 8;
       for (int v = tid; v < BM * VPR; v += T) {
         const int r = v / VPR, c = (v % VPR) * 8;
@@ -332,7 +424,7 @@ constexpr size_t lds_bytes() {
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES, bool SETPRIO>
 static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc,
                     float* ws, int M, int N, int K, int splits, int k_chunk, const int* offsets,
-                    int n_groups, int m_tiles, hipStream_t st) {
+                    int n_groups, int m_tiles, hipStream_t st, const RopeEpi& re) {
   constexpr int T = WM * WN * 64;
   constexpr size_t lds = lds_bytes<BM, BN, STAGES>();
   static_assert(lds <= 163840, "LDS budget");
@@ -345,7 +437,7 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
   const int gx = (N + BN - 1) / BN;
   const int blocks = gx * m_tiles * splits;
   kern<<<blocks, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups, gx,
-                               m_tiles, splits);
+                               m_tiles, splits, re);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -373,7 +465,8 @@ static int env_int(const char* name, int dflt) {
 template <int EPI>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
-    uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m) {
+    uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m,
+    RopeEpi re) {
   constexpr int BM = 256, BN = 256;
   constexpr int BUF = (BM + BN) * kBK;  // bf16 per K-tile buffer (64 KB)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -503,6 +596,23 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
   if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
   __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
 
+  if constexpr (EPI == EPI_ROPE) {
+    // stage the whole 256 x 256 bf16 tile (two heads), then rotate / scatter per head
+    constexpr int LDR = BN + 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = grp * 128 + i * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) smem[row * LDR + wc * 64 + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+      }
+    __syncthreads();
+    const int rows = min(BM, M - m0);
+    auto at = [&](int r, int c) { return bf2f(smem[r * LDR + c]); };
+    rope_tile_store<512>(at, n0 / 128, 2, m0, rows, re, tid);
+    return;
+  }
   // epilogue: each wave stages its 128 x 64 (or 128 x 32 after SiLU.mul) bf16 tile
   constexpr int OW = EPI == EPI_NONE ? 64 : 32;
   constexpr int LD = OW + 8;
@@ -539,9 +649,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
 
 template <int EPI>
 static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
-                   int N, int K, hipStream_t st) {
+                   int N, int K, hipStream_t st, const RopeEpi& re) {
   constexpr size_t ring = 2ull * (256 + 256) * kBK * 2;
-  constexpr size_t epi = 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
+  constexpr size_t epi = EPI == EPI_ROPE ? 256ull * (256 + 8) * 2
+                                         : 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
   constexpr size_t lds = ring > epi ? ring : epi;
   static_assert(lds <= 163840, "LDS budget");
   auto kern = gemm_pp_kernel<EPI>;
@@ -553,7 +664,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   const int gx = (N + 255) / 256, gy = (M + 255) / 256;
   static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
   const int gm = std::max(1, std::min(group_m, gy));
-  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm);
+  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re);
 }
 
 struct Plan {
@@ -608,19 +719,45 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
 template <int EPI, bool GROUPED>
 static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_t* B, int ldb,
                         uint16_t* C, int ldc, float* ws, int M, int N, int K, const int* offsets,
-                        int n_groups, hipStream_t st) {
+                        int n_groups, hipStream_t st, const RopeEpi& re = RopeEpi{}) {
 #define MLOP_GEMM(bm, bn, wm, wn, stages, prio)                                                   \
   run_cfg<bm, bn, wm, wn, EPI, GROUPED, stages, prio>(A, lda, B, ldb, C, ldc, ws, M, N, K,        \
                                                       p.splits, p.k_chunk, offsets, n_groups,     \
-                                                      p.m_tiles, st)
-  if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
-  else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
-  else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
-  else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
-  else if (!GROUPED && p.variant == 3 && p.splits == 1) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st);
-  else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
-  else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
+                                                      p.m_tiles, st, re)
+  if constexpr (EPI == EPI_ROPE) {  // whole heads per staged chunk, no split-K (launch_gemm_rope)
+    if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
+    else if (!GROUPED && p.variant == 3) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
+    else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
+  } else {
+    if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
+    else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
+    else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
+    else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
+    else if (!GROUPED && p.variant == 3 && p.splits == 1) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
+    else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
+  }
 #undef MLOP_GEMM
+}
+
+// EPI_ROPE: the plain (no split-K) plan must stage whole heads: BN >= 128, i.e. M > 256
+bool gemm_rope_supported(int M, int N, int K) {
+  if (M <= 0 || N % 128 || K % kBK) return false;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  return p.BM == 256 && p.BN >= 128;
+}
+
+bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
+                      hipStream_t st) {
+  if (M == 0) return true;
+  if (!gemm_rope_supported(M, N, K)) return false;
+  Plan p = plan(M, N, K, false, 0, 0);
+  p.splits = 1;
+  p.k_chunk = K;
+  launch_plan<EPI_ROPE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, nullptr,
+                               M, N, K, nullptr, 0, st, re);
+  return true;
 }
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {

@@ -27,7 +27,24 @@ void launch_flash_prefill(void* out, const void* q, const void* kc, const void* 
                           int bt_stride, const int* ptile_seq, const int* ptile_q0,
                           const int* q_start, const int* q_len, const int* ctx_len, int num_ptiles,
                           int Hq, int Hkv, float scale_log2, int num_blocks, hipStream_t st);
+// QKV projection epilogue (EPI_ROPE): the GEMM's C tile is [q heads | k heads | v heads]
+// of head_dim 128; q/k are rotated (HF rotate-half, cos/sin table [max_pos, 128]) and
+// q goes to q_out [T, Hq, 128], k / v into the paged cache (k [NB, Hkv, BS, 128],
+// v [NB, Hkv, 128, BS]; slot < 0 = padding row, no cache write) - rope_cache.hip's
+// layout, done from the GEMM's LDS-staged tile instead of a [T, N] round trip.
+struct RopeEpi {
+  uint16_t* q_out;
+  uint16_t* k_cache;
+  uint16_t* v_cache;
+  const int* pos;
+  const float* cos_sin;
+  const int* slots;
+  int Hq, Hkv, BS;
+};
 long gemm_workspace_floats(int M, int N, int K, int epi);
+bool gemm_rope_supported(int M, int N, int K);
+bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
+                      hipStream_t st);
 void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws,
                  long ws_floats, int M, int N, int K, int epi, hipStream_t st);
 bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, void* residual,

@@ -71,6 +71,39 @@ def test_rope_cache(gpu, Hq, Hkv):
     close(vc, vr, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("M,Hq,Hkv", [(300, 32, 8), (1024, 32, 8), (2048, 32, 8), (3000, 32, 8),
+                                      (600, 8, 1)])
+def test_qkv_rope_cache_fused(gpu, M, Hq, Hkv):
+    """QKV GEMM with RoPE + paged K/V stores in its epilogue (EPI_ROPE; the ping-pong
+    256x256 kernel at M=2048/3000, the 256x128 kernel otherwise) vs fp32 GEMM + rope_cache."""
+    from mlopamd.models.layers import rope_table
+
+    D, K, BS = 128, 4096, 16
+    N = (Hq + 2 * Hkv) * D
+    NB = M // BS + 8
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
+    slots[5] = -1
+    slots[M - 1] = -1
+    assert torch.ops.mlop.gemm_rope_supported(M, N, K)
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
+    assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
+    qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref)
+    close(kc, kr)
+    close(vc, vr)
+    # the wrapper (autotuned fused vs hipBLASLt + rope_cache) agrees too
+    q2 = ops.qkv_rope_cache(x, w, pos, cs, slots, kc, vc, Hq)
+    close(q2, q_ref)
+
+
 class Meta:
     pass
 
