@@ -1,0 +1,48 @@
+"""bench.py contract on CPU: the driver's JSON line, single process and 2 ranks over
+gloo (torch.distributed.run, 127.0.0.1), tiny Llama shapes through the same
+operator-deploy + engine path as the MI355X run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # exactly one JSON line (rank 0)
+    return json.loads(lines[0])
+
+
+ARGS = ["--model", "tiny-llama", "--steps", "4", "--warmup", "2", "--batch", "8"]
+
+
+def test_bench_single_process_json():
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS])
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["value"] > 0
+    assert d["config"]["parallelism"] == "dp1" and d["higher_is_better"] is True
+    assert d["deploy"]["path"] == "operator" and d["p50_cr_ready_s"] > 0
+
+
+def test_bench_two_ranks_gloo():
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+              os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 16 and d["value"] > 0
+    # whole-job aggregate over ranks = per-GPU value x N
+    assert abs(d["served_tokens_per_sec_per_gpu"] * 2 - d["value"]) < 1e-3 * d["value"] + 0.02

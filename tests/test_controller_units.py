@@ -186,9 +186,9 @@ def test_placement_70b():
 
 
 def test_placement_bench_config_is_one_gpu():
-    """The headline bench (1024 concurrent x 2048 max len) is one 288 GB GPU per replica."""
-    p = placement.plan("llama3-8b", 2048, 1024)
-    assert p.tensorParallel == 1 and p.fits and p.kvTokenCapacity >= 1024 * 1024
+    """The headline bench (2048 concurrent x 1024 max len) is one 288 GB GPU per replica."""
+    p = placement.plan("llama3-8b", 1024, 2048)
+    assert p.tensorParallel == 1 and p.fits and p.kvTokenCapacity >= 2048 * 512
 
 
 def test_placement_mixtral_ep():
