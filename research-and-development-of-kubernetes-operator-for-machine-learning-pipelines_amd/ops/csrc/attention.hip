@@ -8,8 +8,13 @@
 // softmax (max, exp2, rescale of O) is entirely lane-local except the two
 // cross-lane max steps (xor 16, xor 32), and P^T feeds the second MFMA straight
 // from the first one's accumulator registers (cdna_hip_programming.md §3
-// "An accumulator tile as the next MFMA's operand", with a permuted k order:
-// lane group g = lane>>4 owns tokens {4g..4g+3} of page A and {4g..4g+3} of page B).
+// "An accumulator tile as the next MFMA's operand", with a permuted k order).
+// Decode kernel token order of a page pair (A, B; pair token t = 16*page + offset):
+// lane group g = lane>>4 owns the 8 CONSECUTIVE pair tokens 8g..8g+7 - the first S
+// MFMA produces 8g..8g+3 of every group, the second 8g+4..8g+7 (its K rows are
+// loaded in that permuted row order) - so each lane's V^T fragment is ONE 16-B load
+// of a dim-major page row (8-B loads stream at 0.54-0.70x the 16-B rate,
+// MI355X_MICROARCH.md "visibility" table) and P^T = {S1 rows, S2 rows} as before.
 //
 // MFMA rows: 16 q-rows per tile = (16/G query tokens) x (G heads of one kv head).
 // A workgroup = 4 waves = one (tile, kv head, kv partition); the waves split
@@ -92,18 +97,19 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const uint16_t* vA = vc + pgA * page_stride + (size_t)kvh * kD * kBS;
     const uint16_t* vB = vc + pgB * page_stride + (size_t)kvh * kD * kBS;
 
+    // K rows of MFMA row r: pair tokens 8*(r>>2) + (r&3) (first S MFMA) and +4 (second)
+    const uint16_t* kR = (r >> 3 ? kB : kA) + (8 * ((r >> 2) & 1) + (r & 3)) * kD;
     bf16x8 ka[4], kb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      ka[kk] = *reinterpret_cast<const bf16x8*>(kA + r * kD + kk * 32 + g4 * 8);
-      kb[kk] = *reinterpret_cast<const bf16x8*>(kB + r * kD + kk * 32 + g4 * 8);
+      ka[kk] = *reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8);
+      kb[kk] = *reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8);
     }
-    bf16x4 va[8], vb[8];
+    // V^T fragment of lane group g4: dims d*16 + r, pair tokens 8*g4 .. 8*g4+7 (16 B)
+    const uint16_t* vR = (g4 >> 1 ? vB : vA) + r * kBS + 8 * (g4 & 1);
+    bf16x8 vf8[8];
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      va[d] = *reinterpret_cast<const bf16x4*>(vA + (d * 16 + r) * kBS + g4 * 4);
-      vb[d] = *reinterpret_cast<const bf16x4*>(vB + (d * 16 + r) * kBS + g4 * 4);
-    }
+    for (int d = 0; d < 8; ++d) vf8[d] = *reinterpret_cast<const bf16x8*>(vR + d * 16 * kBS);
 
     // S^T[token][row]: lane holds row r, tokens 4*g4 + i of each page
     f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
@@ -112,7 +118,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       sa = mfma16(ka[kk], qf[kk], sa);
       sb = mfma16(kb[kk], qf[kk], sb);
     }
-    const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
+    const int tokA = pp * 32 + g4 * 8, tokB = tokA + 4;
     float pa[4], pb[4];
     float mx = kNegBig;
 #pragma unroll
@@ -144,8 +150,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
       o[d] *= alpha;
-      bf16x8 vf = {va[d][0], va[d][1], va[d][2], va[d][3], vb[d][0], vb[d][1], vb[d][2], vb[d][3]};
-      o[d] = mfma16(vf, pf, o[d]);
+      o[d] = mfma16(vf8[d], pf, o[d]);
     }
   }
 
