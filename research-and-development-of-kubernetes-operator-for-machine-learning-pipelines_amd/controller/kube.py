@@ -66,6 +66,21 @@ class FakeKube:
         self._faults: dict[str, list[int]] = defaultdict(list)
         self.calls = defaultdict(int)
 
+    def _next_rv(self) -> int:
+        self._last_rv = next(self._rv)
+        return self._last_rv
+
+    def current_rv(self) -> int:
+        """The newest resourceVersion handed out (a List's metadata.resourceVersion)."""
+        return getattr(self, "_last_rv", 0)
+
+    def subscribe(self, group, plural, ns=None):
+        """Raw event queue of (type, object) for a watch front-end; returns (queue, unsubscribe)."""
+        q: asyncio.Queue = asyncio.Queue()
+        entry = ((group, plural, ns), q)
+        self._watchers.append(entry)
+        return q, lambda: self._watchers.remove(entry) if entry in self._watchers else None
+
     # -- fault injection --
     def fail_next(self, verb: str, status: int = 500, times: int = 1):
         self._faults[verb].extend([status] * times)
@@ -111,7 +126,7 @@ class FakeKube:
         key = self._key(group, plural, ns, name)
         if key in self._objs:
             raise ApiError(409, "AlreadyExists", f'{plural} "{name}" already exists')
-        md.update(namespace=ns, uid=str(uuid.uuid4()), resourceVersion=str(next(self._rv)),
+        md.update(namespace=ns, uid=str(uuid.uuid4()), resourceVersion=str(self._next_rv()),
                   generation=1, creationTimestamp=_now_iso())
         md.pop("deletionTimestamp", None)
         if (group, plural) in self.STATUS_SUBRESOURCE:
@@ -145,7 +160,7 @@ class FakeKube:
         if not status_only and obj.get("spec") != cur.get("spec"):
             gen += 1
         md["generation"] = gen
-        md["resourceVersion"] = str(next(self._rv))
+        md["resourceVersion"] = str(self._next_rv())
         self._objs[key] = obj
         self._emit("MODIFIED", group, plural, obj)
         return copy.deepcopy(obj)
@@ -193,7 +208,7 @@ class FakeKube:
     async def create_event(self, ns, event: dict):
         self._maybe_fail("event")
         ev = copy.deepcopy(event)
-        ev.setdefault("metadata", {}).setdefault("name", f"ev-{next(self._rv)}")
+        ev.setdefault("metadata", {}).setdefault("name", f"ev-{self._next_rv()}")
         ev["metadata"]["namespace"] = ns
         self.events.append(ev)
         return ev
