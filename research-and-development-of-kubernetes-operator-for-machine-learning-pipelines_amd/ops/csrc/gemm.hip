@@ -163,7 +163,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
   const int q = G >> 3, rr = G & 7, xcd = L & 7, slot = L >> 3;
   const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
   const int gx = n_tiles_x;
-  const int bx = lid % gx, by = (lid / gx) % m_tiles_y, bz = lid / (gx * m_tiles_y);
+  // grouped: the (expert, m-tile) slot is the FAST index, so the slots left empty by a
+  // routing (the grid is sized for the worst case, m_tiles + n_groups) are spread over
+  // every XCD's contiguous range instead of idling the XCDs that drew the tail slots
+  const int bx = GROUPED ? (lid / m_tiles_y) % gx : lid % gx;
+  const int by = GROUPED ? lid % m_tiles_y : (lid / gx) % m_tiles_y;
+  const int bz = lid / (gx * m_tiles_y);
   const int n0 = bx * BN;
   int m0 = by * BM, m_end = M;
   const uint16_t* Bg = B;
@@ -462,11 +467,15 @@ static int env_int(const char* name, int dflt) {
 // buffer starts only after every read of its previous K-tile has retired
 // (phase-window accounting in the comments below).  Quadrant order (0,0)
 // (0,1) (1,1) (1,0) reloads the A sub-tile twice and the B sub-tiles once.
-template <int EPI>
+//
+// GROUPED (MoE K13 at >= 512 rows per expert): the (expert, m-tile) slot is the fast
+// tile index (empty slots of the worst-case grid spread over all XCDs), B = W[e] and
+// rows stop at offsets[e+1]; everything else is the dense schedule.
+template <int EPI, bool GROUPED = false>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m,
-    RopeEpi re) {
+    RopeEpi re, const int* __restrict__ offsets, int n_groups) {
   constexpr int BM = 256, BN = 256;
   constexpr int BUF = (BM + BN) * kBK;  // bf16 per K-tile buffer (64 KB)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -478,9 +487,25 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
   const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
   // tile order inside an XCD's contiguous range: bands of group_m m-tiles, m fastest
   // within a band (a B panel is reused by group_m consecutive tiles while L2-resident)
-  const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
-  const int gm_here = min(group_m, m_tiles - band * group_m);
-  const int m0 = (band * group_m + in_band % gm_here) * BM, n0 = (in_band / gm_here) * BN;
+  int m0, n0, m_end = M;
+  if constexpr (GROUPED) {
+    int t = lid % m_tiles, e = 0;
+    n0 = (lid / m_tiles) * BN;
+    for (; e < n_groups; ++e) {
+      const int tiles = (offsets[e + 1] - offsets[e] + BM - 1) / BM;
+      if (t < tiles) break;
+      t -= tiles;
+    }
+    if (e >= n_groups) return;  // whole workgroup, before any barrier
+    m0 = offsets[e] + t * BM;
+    m_end = offsets[e + 1];
+    B += (size_t)e * N * ldb;
+  } else {
+    const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
+    const int gm_here = min(group_m, m_tiles - band * group_m);
+    m0 = (band * group_m + in_band % gm_here) * BM;
+    n0 = (in_band / gm_here) * BN;
+  }
   const int nk = K / kBK;
 
   // DMA sources: half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127,
@@ -493,7 +518,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     for (int i = 0; i < 2; ++i) {
       const int r = (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row inside the 256-row operand tile
       const int ch = (lane & 7) ^ swz(r);
-      src[h][i] = h < 2 ? A + (size_t)min(m0 + r, M - 1) * lda + ch * 8
+      src[h][i] = h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda + ch * 8
                         : B + (size_t)min(n0 + r, N - 1) * ldb + ch * 8;
     }
   auto issue_half = [&](int buf, int h, int kt) {
@@ -608,7 +633,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
         for (int j = 0; j < 4; ++j) smem[row * LDR + wc * 64 + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
       }
     __syncthreads();
-    const int rows = min(BM, M - m0);
+    const int rows = min(BM, m_end - m0);
     auto at = [&](int r, int c) { return bf2f(smem[r * LDR + c]); };
     rope_tile_store<512>(at, n0 / 128, 2, m0, rows, re, tid);
     return;
@@ -642,29 +667,30 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const int c = it * 64 + lane;
     const int row = c / CPR, cc = (c % CPR) * 8;
     const int gm = m0 + grp * 128 + row, gn = out_col0 + cc;
-    if (gm < M && gn < out_n)
+    if (gm < m_end && gn < out_n)
       *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
   }
 }
 
-template <int EPI>
+template <int EPI, bool GROUPED = false>
 static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
-                   int N, int K, hipStream_t st, const RopeEpi& re) {
+                   int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets = nullptr,
+                   int n_groups = 0) {
   constexpr size_t ring = 2ull * (256 + 256) * kBK * 2;
   constexpr size_t epi = EPI == EPI_ROPE ? 256ull * (256 + 8) * 2
                                          : 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
   constexpr size_t lds = ring > epi ? ring : epi;
   static_assert(lds <= 163840, "LDS budget");
-  auto kern = gemm_pp_kernel<EPI>;
+  auto kern = gemm_pp_kernel<EPI, GROUPED>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  const int gx = (N + 255) / 256, gy = (M + 255) / 256;
+  const int gx = (N + 255) / 256, gy = (M + 255) / 256 + (GROUPED ? n_groups : 0);
   static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
   const int gm = std::max(1, std::min(group_m, gy));
-  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re);
+  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups);
 }
 
 struct Plan {
@@ -682,7 +708,10 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   Plan p{};
   p.variant = 0;
   const int mrows = grouped ? rows_per_group : M;
-  if (mrows <= 64) { p.BM = 64; p.BN = 64; }
+  static const int pp_group_min_rows = env_int("MLOP_GEMM_PP_GROUP_MIN_ROWS", 256);
+  if (grouped && mrows >= pp_group_min_rows && K % kBK == 0 && N % 256 == 0) {
+    p.BM = 256; p.BN = 256; p.variant = 3;  // grouped ping-pong
+  } else if (mrows <= 64) { p.BM = 64; p.BN = 64; }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
   else if (mrows <= 256) {
     static const int bn_min_tiles = env_int("MLOP_GEMM_BN128_MIN_TILES", 192);
@@ -734,6 +763,8 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
     else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
     else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
+    else if (GROUPED && p.variant == 3)
+      run_pp<EPI, true>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
     else if (!GROUPED && p.variant == 3 && p.splits == 1) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);

@@ -302,6 +302,28 @@ def test_gemm_silu_mul(gpu, M, I, K):
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("rows", [[520, 700, 0, 613], [1024, 1024, 1024, 1024], [512, 3, 900, 257]])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_grouped_gemm_large_groups(gpu, rows, epi):
+    """>= 512 rows per expert on average: the grouped ping-pong 256x256 kernel; ragged,
+    empty and tiny groups included; vs per-group fp32 matmul."""
+    torch.manual_seed(sum(rows))
+    E, K, N = len(rows), 512, 1024
+    off = torch.tensor([0] + list(np.cumsum(rows)), device=gpu, dtype=torch.int32)
+    Mt = int(off[-1])
+    x = torch.randn(Mt, K, device=gpu, dtype=bf)
+    w = (0.05 * torch.randn(E, N, K, device=gpu)).to(bf)
+    y = ops.grouped_gemm(x, w, off, epi=epi, avg_rows=max(512, Mt // E))
+    for e in range(E):
+        a, b = int(off[e]), int(off[e + 1])
+        if a == b:
+            continue
+        r = (x[a:b].float() @ w[e].float().t()).to(bf)
+        if epi:
+            r = ref.silu_mul(ops.deinterleave_cols(r))
+        close(y[a:b], r)
+
+
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (77, 8, 2, 1024, 512), (512, 8, 2, 512, 256),
                                        (300, 4, 1, 256, 256)])
 def test_moe_pipeline(gpu, T, E, k, H, I):
