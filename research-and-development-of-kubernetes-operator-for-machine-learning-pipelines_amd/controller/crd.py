@@ -166,3 +166,99 @@ def artifact_uri(source: str, base: str = "s3://mlflow") -> str:
     if source.startswith("file://") or source.startswith("mlop://"):
         return source
     return f"{base.rstrip('/')}/{extract_relative_path(source)}"
+
+
+# ---------------------------------------------- structural schema checks --
+# What the kube-apiserver does with a CR body before storing it (structural
+# OpenAPI v3 subset used by crd.yaml): reject type / bound / enum / required
+# violations with 422 Invalid, prune fields the schema does not declare unless
+# ``x-kubernetes-preserve-unknown-fields`` or ``additionalProperties`` allow them.
+# The reference relies on the real apiserver for this (crd.yaml:11-37 there);
+# the in-memory fake (kube.FakeKube) and its REST front-end apply it here.
+
+_ROOT_FIELDS = ("apiVersion", "kind", "metadata")
+
+
+def _type_ok(v, t: str) -> bool:
+    if t == "object":
+        return isinstance(v, dict)
+    if t == "array":
+        return isinstance(v, list)
+    if t == "string":
+        return isinstance(v, str)
+    if t == "boolean":
+        return isinstance(v, bool)
+    if t == "integer":
+        return isinstance(v, int) and not isinstance(v, bool)
+    if t == "number":
+        return isinstance(v, (int, float)) and not isinstance(v, bool)
+    return True
+
+
+def schema_errors(value, schema: dict, path: str = "") -> list[str]:
+    """Field errors of ``value`` against a structural schema, kubectl-style
+    (``spec.tensorParallel: Invalid value: 9: must be <= 8``)."""
+    errs: list[str] = []
+    where = path or "<root>"
+    if value is None:
+        if not schema.get("nullable", False) and path:
+            errs.append(f"{where}: Invalid value: null: must not be null")
+        return errs
+    t = schema.get("type")
+    if t and not _type_ok(value, t):
+        return [f"{where}: Invalid value: {value!r}: must be of type {t}"]
+    if "enum" in schema and value not in schema["enum"]:
+        errs.append(f"{where}: Unsupported value: {value!r}: supported values: {schema['enum']}")
+    if isinstance(value, (int, float)) and not isinstance(value, bool):
+        if "minimum" in schema and value < schema["minimum"]:
+            errs.append(f"{where}: Invalid value: {value}: must be >= {schema['minimum']}")
+        if "maximum" in schema and value > schema["maximum"]:
+            errs.append(f"{where}: Invalid value: {value}: must be <= {schema['maximum']}")
+    if isinstance(value, dict):
+        props = schema.get("properties", {})
+        for req in schema.get("required", []):
+            if req not in value:
+                errs.append(f"{path + '.' if path else ''}{req}: Required value")
+        extra = schema.get("additionalProperties")
+        for k, v in value.items():
+            sub = f"{path}.{k}" if path else k
+            if k in props:
+                errs += schema_errors(v, props[k], sub)
+            elif isinstance(extra, dict):
+                errs += schema_errors(v, extra, sub)
+    if isinstance(value, list) and isinstance(schema.get("items"), dict):
+        for i, v in enumerate(value):
+            errs += schema_errors(v, schema["items"], f"{path}[{i}]")
+    return errs
+
+
+def prune(value, schema: dict, root: bool = True):
+    """Drop undeclared fields (apiserver pruning); returns a new value."""
+    if isinstance(value, dict):
+        if schema.get("x-kubernetes-preserve-unknown-fields"):
+            return dict(value)
+        props = schema.get("properties", {})
+        extra = schema.get("additionalProperties")
+        out = {}
+        for k, v in value.items():
+            if root and k in _ROOT_FIELDS:
+                out[k] = v
+            elif k in props:
+                out[k] = prune(v, props[k], root=False)
+            elif isinstance(extra, dict):
+                out[k] = prune(v, extra, root=False)
+            elif extra is True:
+                out[k] = v
+        return out
+    if isinstance(value, list) and isinstance(schema.get("items"), dict):
+        return [prune(v, schema["items"], root=False) for v in value]
+    return value
+
+
+def admit(obj: dict, schema: dict | None = None) -> tuple[dict, list[str]]:
+    """(pruned object, field errors) for an MlflowModel body, as the apiserver
+    would store or reject it."""
+    schema = schema or crd_schema()
+    body = {k: v for k, v in obj.items() if k not in _ROOT_FIELDS}
+    errs = schema_errors(body, schema)
+    return prune(obj, schema), errs

@@ -58,13 +58,36 @@ class FakeKube:
     STATUS_SUBRESOURCE = {("mlflow.nizepart.com", "mlflowmodels"),
                           ("machinelearning.seldon.io", "seldondeployments")}
 
-    def __init__(self):
+    def __init__(self, validate: bool = True):
         self._objs: dict[tuple, dict] = {}
         self._rv = itertools.count(1)
         self._watchers: list[tuple[tuple, asyncio.Queue]] = []
         self.events: list[dict] = []
         self._faults: dict[str, list[int]] = defaultdict(list)
         self.calls = defaultdict(int)
+        # structural schemas of installed CRDs: bodies are validated (422 Invalid) and
+        # pruned like the real apiserver does (crd.admit)
+        self.schemas: dict[tuple, tuple[str, dict]] = {}
+        if validate:
+            from .crd import crd_schema
+            self.register_crd("mlflow.nizepart.com", "mlflowmodels", "MlflowModel", crd_schema())
+
+    def register_crd(self, group: str, plural: str, kind: str, schema: dict) -> None:
+        self.schemas[(group, plural)] = (kind, schema)
+
+    def _admit(self, group, plural, body, name, status_only: bool = False):
+        ent = self.schemas.get((group, plural))
+        if ent is None:
+            return body
+        from .crd import admit
+        kind, schema = ent
+        if status_only:  # /status writes: only .status is taken from the body
+            schema = {"type": "object", "properties": {"status": schema.get("properties", {}).get("status", {})}}
+            body = {k: v for k, v in body.items() if k in ("apiVersion", "kind", "metadata", "status")}
+        pruned, errs = admit(body, schema)
+        if errs:
+            raise ApiError(422, "Invalid", f'{kind}.{group} "{name}" is invalid: ' + "; ".join(errs))
+        return pruned
 
     def _next_rv(self) -> int:
         self._last_rv = next(self._rv)
@@ -126,6 +149,7 @@ class FakeKube:
         key = self._key(group, plural, ns, name)
         if key in self._objs:
             raise ApiError(409, "AlreadyExists", f'{plural} "{name}" already exists')
+        body = self._admit(group, plural, body, name)
         md.update(namespace=ns, uid=str(uuid.uuid4()), resourceVersion=str(self._next_rv()),
                   generation=1, creationTimestamp=_now_iso())
         md.pop("deletionTimestamp", None)
@@ -137,6 +161,7 @@ class FakeKube:
 
     def _write(self, group, plural, key, new, status_only: bool):
         cur = self._objs[key]
+        new = self._admit(group, plural, new, key[3], status_only)
         sub = (group, plural) in self.STATUS_SUBRESOURCE
         if sub and status_only:
             obj = copy.deepcopy(cur)

@@ -264,15 +264,25 @@ def test_fake_kube_semantics():
     async def go():
         k = FakeKube()
         o = await k.create("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels",
-                           {"metadata": {"name": "a"}, "spec": {"x": 1}, "status": {"s": 1}})
+                           {"metadata": {"name": "a"}, "spec": {"modelName": "m", "modelAlias": "c", "x": 1},
+                            "status": {"s": 1}})
+        assert "x" not in o["spec"]  # undeclared field pruned like the apiserver does
         assert "status" not in o and o["metadata"]["generation"] == 1
         o2 = await k.patch_status("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels", "a",
                                   {"status": {"currentModelVersion": "1", "error": None}})
         assert o2["status"] == {"currentModelVersion": "1"} and o2["metadata"]["generation"] == 1
         o3 = await k.patch("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels", "a",
-                           {"spec": {"x": 2}, "status": {"hack": 1}})
+                           {"spec": {"monitoringInterval": 30}, "status": {"hack": 1}})
         assert o3["metadata"]["generation"] == 2 and "hack" not in o3["status"]
-        stale = dict(o, spec={"x": 3})
+        with pytest.raises(ApiError) as e:  # schema violation: 422 Invalid, nothing stored
+            await k.patch("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels", "a",
+                          {"spec": {"tensorParallel": 9, "monitoringInterval": "soon"}})
+        assert e.value.status == 422 and "tensorParallel" in e.value.message and "monitoringInterval" in e.value.message
+        with pytest.raises(ApiError) as e:
+            await k.patch_status("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels", "a",
+                                 {"status": {"canaryTraffic": "ten"}})
+        assert e.value.status == 422
+        stale = dict(o, spec={"modelName": "m", "modelAlias": "d"})
         with pytest.raises(ApiError) as e:
             await k.replace("mlflow.nizepart.com", "v1alpha1", "ns", "mlflowmodels", "a", stale)
         assert e.value.status == 409
@@ -340,3 +350,30 @@ def test_gate_gpu_guards_skip_missing_series():
     g = prometheus.should_promote(dict(base, tpot_avg=None), dict(base, tpot_avg=0.01), {}, 0.0,
                                   extra_max_ratio={"tpot_avg": 1.1})
     assert g.promote
+
+
+def test_example_crs_admit_and_place():
+    """manifests/examples: one CR per BASELINE config; each passes the CRD's
+    structural schema unchanged (nothing pruned) and its GPU placement fits."""
+    import glob
+    import os
+
+    files = sorted(glob.glob(os.path.join(str(crd.MANIFESTS), "examples", "*.yaml")))
+    assert len(files) == 5, files
+    schema = crd.crd_schema()
+    for f in files:
+        with open(f) as fh:
+            (cr,) = [d for d in yaml.safe_load_all(fh) if d]
+        pruned, errs = crd.admit(cr, schema)
+        assert errs == [] and pruned == cr, (f, errs)
+        spec = crd.ModelSpec.from_spec(cr["spec"])
+        assert spec.validate() == []
+        if spec.architecture:
+            p = placement.plan(spec.architecture, max_model_len=spec.max_model_len or 4096,
+                               max_num_seqs=spec.max_num_seqs or 256, requested_tp=spec.tensor_parallel,
+                               requested_ep=spec.expert_parallel)
+            assert p.fits, (f, p)
+    bad = {"apiVersion": "mlflow.nizepart.com/v1alpha1", "kind": "MlflowModel", "metadata": {"name": "x"},
+           "spec": {"modelName": "m", "modelAlias": "a", "tensorParallel": 0, "canary": {"step": "10"}}}
+    _, errs = crd.admit(bad, schema)
+    assert any("tensorParallel" in e for e in errs) and any("canary.step" in e for e in errs)
