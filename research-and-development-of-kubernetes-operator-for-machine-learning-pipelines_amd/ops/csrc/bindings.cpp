@@ -317,8 +317,12 @@ void argmax(Tensor out, Tensor logits) {
                     reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
                 "bf16 logits must be [n, V] with unit inner stride and 16-B aligned rows");
     c10::DeviceGuard g(logits.device());
-    mlop::launch_argmax_bf16(out.data_ptr<int64_t>(), logits.data_ptr(), (int)logits.size(0),
-                             (int)logits.size(1), logits.stride(0), cur_stream());
+    const int n = (int)logits.size(0), V = (int)logits.size(1);
+    const int S = mlop::argmax_splits(n, V);
+    at::Tensor ws;  // per-(row, split) keys from the caching allocator (graph-capture safe)
+    if (S > 1) ws = at::empty({(int64_t)n * S}, logits.options().dtype(at::kLong));
+    mlop::launch_argmax_bf16(out.data_ptr<int64_t>(), logits.data_ptr(), n, V, logits.stride(0),
+                             S > 1 ? ws.data_ptr() : nullptr, cur_stream());
     return;
   }
   check_logits(logits);

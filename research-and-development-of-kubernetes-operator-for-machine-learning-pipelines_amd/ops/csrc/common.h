@@ -81,6 +81,12 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// SiLU of a bf16-rounded gate, rounded to bf16 (the GEMM epilogues' rounding)
+__device__ __forceinline__ float silu_bf(float g) {
+  const float gb = bf2f(f2bf(g));
+  return bf2f(f2bf(gb / (1.f + __expf(-gb))));
+}
+
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 }  // namespace mlop

@@ -48,10 +48,6 @@ constexpr int kStages = 3;
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 
-__device__ __forceinline__ float silu_bf(float g) {
-  const float gb = bf2f(f2bf(g));
-  return bf2f(f2bf(gb / (1.f + __expf(-gb))));
-}
 
 // RoPE / paged-cache stores of `nheads` consecutive 128-wide heads of a staged 256-row
 // C tile (EPI_ROPE).  `at(r, c)` returns the bf16-rounded projection output of tile row r,
@@ -775,6 +771,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
 // EPI_ROPE: the plain (no split-K) plan must stage whole heads: BN >= 128, i.e. M > 256
 bool gemm_rope_supported(int M, int N, int K) {
   if (M <= 0 || N % 128 || K % kBK) return false;
+  if (gemv_takes(M, N, K, EPI_ROPE)) return true;  // decode M <= 8: gemv.hip
   const Plan p = plan(M, N, K, false, 0, 0);
   return p.BM == 256 && p.BN >= 128;
 }
@@ -783,6 +780,10 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
                       hipStream_t st) {
   if (M == 0) return true;
   if (!gemm_rope_supported(M, N, K)) return false;
+  if (gemv_takes(M, N, K, EPI_ROPE) && lda % 8 == 0) {
+    launch_gemv_rope(A, lda, B, M, N, K, re, st);
+    return true;
+  }
   Plan p = plan(M, N, K, false, 0, 0);
   p.splits = 1;
   p.k_chunk = K;
@@ -792,7 +793,7 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
 }
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {
-  (void)epi;
+  if (gemv_takes(M, N, K, epi)) return 0;
   const Plan p = plan(M, N, K, false, 0, 0);
   return p.splits > 1 ? (long)p.splits * M * N : 0;
 }
@@ -800,6 +801,10 @@ long gemm_workspace_floats(int M, int N, int K, int epi) {
 void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws,
                  long ws_floats, int M, int N, int K, int epi, hipStream_t st) {
   if (M == 0) return;
+  if (gemv_takes(M, N, K, epi) && lda % 8 == 0 && ldb % 8 == 0) {
+    launch_gemv(A, lda, B, ldb, C, ldc, M, N, K, epi, st);
+    return;
+  }
   Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits > 1 && (long)p.splits * M * N > ws_floats) { p.splits = 1; p.k_chunk = K; }
   if (epi == EPI_NONE)
@@ -826,6 +831,7 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              const void* w, float eps, float* ws, long ws_floats, int M, int N,
                              int K, hipStream_t st) {
   if (M == 0) return true;
+  if (gemv_takes(M, N, K, EPI_NONE)) return false;  // GEMV + add_rmsnorm
   const Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
   launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,

@@ -1,0 +1,279 @@
+// K2: bf16 skinny GEMM / GEMV for decode at M <= 8 rows (default M <= 4: batch-1 .. batch-4 decode).
+//
+//   C[M, N] = A[M, K] . B[N, K]^T      (A activations, B weights [out, in], both bf16)
+//
+// At M <= 8 a decode projection is pure weight streaming: every weight byte is read
+// once and the arithmetic (M dot products per byte pair) is noise, so the MFMA GEMM's
+// LDS ring, 64-row tiles (56+ rows of padding) and split-K slabs are all overhead.
+// Here (cdna_hip_programming.md §5 "glds vs register staging", row "GEMV / M <= 16":
+// load straight to VGPRs, deep unroll, late vmcnt):
+//   * a wave owns 2*RP weight rows; each lane streams 16-B chunks of every row with
+//     nontemporal global loads (weights are read by exactly one CU, once:
+//     MI355X_MICROARCH.md "nt-weights"), U chunks per row in flight before the
+//     first dot: 64 lanes x 16 B = one contiguous 1 KiB run of a row per load
+//     instruction;
+//   * the activation chunks come through the normal (cached) path: A is a few KiB
+//     re-read by every wave from L1/L2;
+//   * v_dot2c_f32_bf16 (two bf16 products per op, fp32 accumulate), then a
+//     butterfly wave reduction per (row, m) output;
+//   * KW = 4 puts the 4 waves of a workgroup on the SAME rows with K interleaved
+//     over them (LDS combine) when N alone gives too few waves to keep 256 CUs
+//     streaming (70B TP=8 shards: N = 1280 / 1024).
+// Epilogues:
+//   EPI_NONE      bf16 store;
+//   EPI_SILU_MUL  gate/up rows interleaved in groups of 16: a wave takes gate rows
+//                 32g+i.. and their up rows 32g+16+i.., so silu(g)*u is formed in
+//                 registers and only N/2 columns are stored (gemm.hip's rounding);
+//   EPI_ROPE      QKV projection: a wave takes the rotate-half PAIR of rows (d, d+64) of
+//                 one q/k head (or two v rows), rotates the bf16-rounded outputs and
+//                 stores q to q_out and k / v straight into the paged cache
+//                 (rope_cache.hip's math and layouts, no [M, N] round trip, one
+//                 launch fewer per layer).
+#include <stdlib.h>
+
+#include "common.h"
+#include "launch.h"
+
+namespace mlop {
+
+namespace {
+
+enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3 };
+constexpr int kHeadD = 128;
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b),
+                                        c, false);
+}
+
+__device__ __forceinline__ float dot8(const u32x4& w, const u32x4& x, float c) {
+  c = dot2(w.x, x.x, c);
+  c = dot2(w.y, x.y, c);
+  c = dot2(w.z, x.z, c);
+  return dot2(w.w, x.w, c);
+}
+
+template <int M, int RP, int EPI, int KW, int U>
+__global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ A, int lda,
+                                                   const uint16_t* __restrict__ B, int ldb,
+                                                   uint16_t* __restrict__ C, int ldc, int N, int K,
+                                                   RopeEpi re) {
+  constexpr int R = 2 * RP;  // weight rows per wave
+  static_assert(EPI != EPI_ROPE || RP == 1, "rope sets are single row pairs");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // row set: KW == 1 -> one per wave; KW == 4 -> one per workgroup (its waves split K)
+  const int set = KW == 1 ? blockIdx.x * 4 + wv : blockIdx.x;
+  if (set >= N / R) return;  // every epilogue has N / R sets
+  int rows[R];
+  if constexpr (EPI == EPI_SILU_MUL) {
+    const int col = set * RP, g = col >> 4, i0 = col & 15;  // RP outputs inside one 16-group
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      rows[p] = 32 * g + i0 + p;            // gate
+      rows[RP + p] = 32 * g + 16 + i0 + p;  // up
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    const int rope_sets = (re.Hq + re.Hkv) * (kHeadD / 2);
+    if (set < rope_sets) {
+      const int h = set / (kHeadD / 2), d = set % (kHeadD / 2);
+      rows[0] = h * kHeadD + d;
+      rows[1] = h * kHeadD + kHeadD / 2 + d;
+    } else {
+      rows[0] = 2 * set;  // v rows: plain consecutive pairs after the q/k rows
+      rows[1] = 2 * set + 1;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows[r] = set * R + r;
+  }
+  const int KC = K >> 3;  // 16-B chunks per row
+  const u32x4* Bv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) Bv[r] = reinterpret_cast<const u32x4*>(B + (size_t)rows[r] * ldb);
+  const u32x4* Av[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) Av[m] = reinterpret_cast<const u32x4*>(A + (size_t)m * lda);
+
+  float acc[R][M];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+
+  const int lane_off = (KW == 1 ? 0 : wv * 64) + lane;
+  constexpr int STEP = 64 * KW;  // chunk stride between a lane's consecutive loads
+  for (int c0 = 0; c0 < KC; c0 += STEP * U) {
+    u32x4 w[U][R], x[U][M];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * STEP + lane_off;
+      const bool ok = c < KC;
+#pragma unroll
+      for (int r = 0; r < R; ++r) w[u][r] = ok ? __builtin_nontemporal_load(Bv[r] + c) : u32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int m = 0; m < M; ++m) x[u][m] = ok ? Av[m][c] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[r][m] = dot8(w[u][r], x[u][m], acc[r][m]);
+  }
+
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+
+  if constexpr (KW > 1) {
+    __shared__ float red[KW][R * M];
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int m = 0; m < M; ++m) red[wv][r * M + m] = acc[r][m];
+    }
+    __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) s += red[k][r * M + m];
+        acc[r][m] = s;
+      }
+  }
+
+  // every lane holds every sum now; lane j stores output j of the set
+  if constexpr (EPI == EPI_SILU_MUL) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int p = 0; p < RP; ++p)
+        if (lane == m * RP + p)
+          C[(size_t)m * ldc + set * RP + p] = f2bf(silu_bf(acc[p][m]) * bf2f(f2bf(acc[RP + p][m])));
+  } else if constexpr (EPI == EPI_ROPE) {
+    const int rope_sets = (re.Hq + re.Hkv) * (kHeadD / 2);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (lane != m) continue;
+      const int slot = re.slots[m];
+      const int blk = slot >= 0 ? slot / re.BS : 0, off = slot >= 0 ? slot % re.BS : 0;
+      if (set < rope_sets) {
+        const int h = set / (kHeadD / 2), d = set % (kHeadD / 2);
+        const float* cs = re.cos_sin + (size_t)re.pos[m] * kHeadD;
+        const float c = cs[d], s = cs[kHeadD / 2 + d];
+        const float x = bf2f(f2bf(acc[0][m])), y = bf2f(f2bf(acc[1][m]));
+        const uint16_t oa = f2bf(x * c - y * s), ob = f2bf(y * c + x * s);
+        uint16_t* dst;
+        if (h < re.Hq) {
+          dst = re.q_out + ((size_t)m * re.Hq + h) * kHeadD;
+        } else {
+          if (slot < 0) continue;
+          dst = re.k_cache + (((size_t)blk * re.Hkv + (h - re.Hq)) * re.BS + off) * kHeadD;
+        }
+        dst[d] = oa;
+        dst[kHeadD / 2 + d] = ob;
+      } else if (slot >= 0) {
+        const int vr = 2 * set - 2 * rope_sets;  // first v row (0 .. Hkv*128)
+        const int kh = vr / kHeadD, dd = vr % kHeadD;
+        uint16_t* dst = re.v_cache + (((size_t)blk * re.Hkv + kh) * kHeadD + dd) * re.BS + off;
+        dst[0] = f2bf(acc[0][m]);
+        dst[re.BS] = f2bf(acc[1][m]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (lane == m * R + r) C[(size_t)m * ldc + set * R + r] = f2bf(acc[r][m]);
+  }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+int gemv_max_m() {
+  // measured (scripts/run38.sh): the GEMV wins every decode projection at M <= 4 in the
+  // running model; at M = 8 the 64-row MFMA tiles stream gate_up / down faster
+  static const int max_m = std::min(8, env_int("MLOP_GEMV_MAX_M", 4));
+  return max_m;
+}
+
+template <int M, int EPI>
+void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int N,
+                int K, const RopeEpi& re, hipStream_t st) {
+  constexpr int U = M <= 2 ? 4 : 2;  // chunks per row in flight per lane (VGPR budget)
+  // sets of RP row pairs; aim for >= 2048 waves in flight (8 per CU), else KW = 4
+  const int pairs = N / 2;
+  const int rp = (EPI != EPI_ROPE && pairs / 2 >= 2048) ? 2 : 1;
+  const int sets = pairs / rp;
+  const bool kw4 = sets < 2048;
+#define MLOP_GEMV(RP, KW)                                                                          \
+  do {                                                                                             \
+    const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
+    gemv_kernel<M, RP, EPI, KW, U><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, N, K, re);      \
+  } while (0)
+  if constexpr (EPI == EPI_ROPE) {
+    if (kw4) MLOP_GEMV(1, 4); else MLOP_GEMV(1, 1);
+  } else {
+    if (rp == 2) {
+      if (kw4) MLOP_GEMV(2, 4); else MLOP_GEMV(2, 1);
+    } else {
+      if (kw4) MLOP_GEMV(1, 4); else MLOP_GEMV(1, 1);
+    }
+  }
+#undef MLOP_GEMV
+}
+
+template <int EPI>
+void run_gemv(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
+              int N, int K, const RopeEpi& re, hipStream_t st) {
+  switch (M) {
+    case 1: run_gemv_m<1, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 2: run_gemv_m<2, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 3: run_gemv_m<3, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 4: run_gemv_m<4, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 5: run_gemv_m<5, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 6: run_gemv_m<6, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 7: run_gemv_m<7, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    default: run_gemv_m<8, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+  }
+}
+
+}  // namespace
+
+// Shapes this path takes: 1 <= M <= MLOP_GEMV_MAX_M (default 4, at most 8), 16-B aligned rows,
+// whole row pairs (EPI_NONE), whole 32-row gate/up groups (EPI_SILU_MUL), or a QKV
+// projection of 128-wide heads (EPI_ROPE: N = (Hq + 2 Hkv) * 128).
+bool gemv_takes(int M, int N, int K, int epi) {
+  if (M < 1 || M > gemv_max_m() || K % 8 || N < 4) return false;
+  if (epi == EPI_SILU_MUL) return N % 32 == 0;
+  if (epi == EPI_ROPE) return N % kHeadD == 0;
+  return epi == EPI_NONE && N % 4 == 0;
+}
+
+void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                 int epi, hipStream_t st) {
+  auto* a = (const uint16_t*)A;
+  auto* b = (const uint16_t*)B;
+  auto* c = (uint16_t*)C;
+  const RopeEpi none{};
+  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL>(a, lda, b, ldb, c, ldc, M, N, K, none, st);
+  else run_gemv<EPI_NONE>(a, lda, b, ldb, c, ldc, M, N, K, none, st);
+}
+
+void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
+                      hipStream_t st) {
+  run_gemv<EPI_ROPE>((const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, M, N, K, re, st);
+}
+
+}  // namespace mlop

@@ -42,6 +42,12 @@ struct RopeEpi {
   int Hq, Hkv, BS;
 };
 long gemm_workspace_floats(int M, int N, int K, int epi);
+// K2 skinny GEMV (gemv.hip): decode projections at M <= 8 (epi 0 none, 1 silu-mul, 3 rope)
+bool gemv_takes(int M, int N, int K, int epi);
+void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                 int epi, hipStream_t st);
+void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
+                      hipStream_t st);
 bool gemm_rope_supported(int M, int N, int K);
 bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st);
@@ -59,7 +65,9 @@ void launch_moe_permute(void* xp, int* offsets, int* src, int* inv, const void* 
 void launch_moe_combine(void* out, const void* y, const int* inv, const float* topw, int T, int k,
                         int H, hipStream_t st);
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st);
-void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, hipStream_t st);
+// bf16 greedy argmax; ws (>= argmax_splits(n, V) * n int64, or null) splits small batches' rows
+int argmax_splits(int n, int V);
+void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, void* ws, hipStream_t st);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
                    const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);
 

@@ -8,6 +8,8 @@
 // truncated at the top-p mass.  Rows re-read in each pass come from L2/MALL
 // (a 128k-vocab row is 512 KB), the kernel is a few tens of microseconds for
 // a 256-row decode batch.
+#include <algorithm>
+
 #include "common.h"
 #include "launch.h"
 
@@ -102,6 +104,69 @@ __global__ void __launch_bounds__(kSampleThreads) argmax_bf16_kernel(long* __res
     int bi = si[0];
     for (int w = 1; w < kSampleThreads / 64; ++w) amax_merge(bv, bi, sv[w], si[w]);
     out[blockIdx.x] = bi == 0x7fffffff ? 0 : bi;
+  }
+}
+
+// Small decode batches (n rows << 256 CUs): one workgroup per row streams a 256 KB row
+// at a single CU's rate (~46 us for 128k vocab).  Split each row over S workgroups; each
+// writes its (value, index) as one ordered 64-bit key (max key = max value, ties to the
+// smallest index), and a one-wave-per-row pass picks the max of the S keys.
+__device__ __forceinline__ unsigned long long amax_key(float v, int i) {
+  return ((unsigned long long)fkey(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)i);
+}
+
+__global__ void __launch_bounds__(kSampleThreads) argmax_bf16_split_kernel(
+    unsigned long long* __restrict__ keys, const uint16_t* __restrict__ logits, int V, long ld, int S) {
+  __shared__ float sv[kSampleThreads / 64];
+  __shared__ int si[kSampleThreads / 64];
+  const int s = blockIdx.x, row_id = blockIdx.y;
+  const uint16_t* row = logits + row_id * ld;
+  const int nv8 = V >> 3, per = (nv8 + S - 1) / S;
+  const int j0 = s * per, j1 = min(nv8, j0 + per);
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  const u32x4* r8 = reinterpret_cast<const u32x4*>(row);
+  for (int j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+    const u32x4 x = r8[j];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      amax_merge(v, idx, lo_bf(x[k]), 8 * j + 2 * k);
+      amax_merge(v, idx, hi_bf(x[k]), 8 * j + 2 * k + 1);
+    }
+  }
+  if (s == S - 1)
+    for (int j = (nv8 << 3) + threadIdx.x; j < V; j += blockDim.x) amax_merge(v, idx, bf2f(row[j]), j);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(idx, o, 64);
+    amax_merge(v, idx, ov, oi);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sv[wid] = v; si[wid] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bv = sv[0];
+    int bi = si[0];
+    for (int w = 1; w < kSampleThreads / 64; ++w) amax_merge(bv, bi, sv[w], si[w]);
+    keys[(size_t)row_id * S + s] = amax_key(bv, bi);
+  }
+}
+
+__global__ void __launch_bounds__(64) argmax_keys_kernel(long* __restrict__ out,
+                                                         const unsigned long long* __restrict__ keys,
+                                                         int S) {
+  const int row_id = blockIdx.x, lane = threadIdx.x;
+  unsigned long long k = 0;
+  for (int s = lane; s < S; s += 64) k = max(k, keys[(size_t)row_id * S + s]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t hi = __shfl_xor((uint32_t)(k >> 32), o, 64), lo = __shfl_xor((uint32_t)k, o, 64);
+    k = max(k, ((unsigned long long)hi << 32) | lo);
+  }
+  if (lane == 0) {
+    const int i = (int)(0xffffffffu - (uint32_t)k);
+    out[row_id] = (k == 0 || i == 0x7fffffff) ? 0 : i;
   }
 }
 
@@ -238,9 +303,23 @@ void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStr
   argmax_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld);
 }
 
-void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, hipStream_t st) {
+// workgroups per row: enough to put ~256 workgroups on the chip, >= 2 16-B loads per thread
+int argmax_splits(int n, int V) {
+  if (n <= 0 || n >= 128) return 1;
+  const int by_size = V / (8 * kSampleThreads * 2);
+  return std::max(1, std::min({64, by_size, (256 + n - 1) / n}));
+}
+
+void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, void* ws, hipStream_t st) {
   if (n == 0) return;
-  argmax_bf16_kernel<<<n, kSampleThreads, 0, st>>>(out, (const uint16_t*)logits, V, ld);
+  const int S = ws ? argmax_splits(n, V) : 1;
+  if (S <= 1) {
+    argmax_bf16_kernel<<<n, kSampleThreads, 0, st>>>(out, (const uint16_t*)logits, V, ld);
+    return;
+  }
+  auto* keys = (unsigned long long*)ws;
+  argmax_bf16_split_kernel<<<dim3(S, n), kSampleThreads, 0, st>>>(keys, (const uint16_t*)logits, V, ld, S);
+  argmax_keys_kernel<<<n, 64, 0, st>>>(out, keys, S);
 }
 
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,

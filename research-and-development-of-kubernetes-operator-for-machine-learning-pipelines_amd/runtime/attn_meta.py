@@ -14,6 +14,7 @@ latest-first so the longest causal ranges start first).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -42,11 +43,17 @@ class AttnMeta:
     num_tokens: int
 
 
-def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int = 256,
+# 128-token partitions: one 32-token page pair per wave at batch 1 (256: 312 tok/s, 128: 322,
+# 64: 246 - the reduce pass and partial traffic grow faster than the parallelism; run38/39)
+MIN_PART = int(os.environ.get("MLOP_ATTN_MIN_PART", 128))
+
+
+def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int | None = None,
                     target_wgs: int = 1024) -> tuple[int, int]:
     """Split the KV range so a launch has >= ~target_wgs workgroups (256 CUs),
     partitions no shorter than ``min_part`` tokens; one partition when the batch
     already fills the chip (no reduce pass)."""
+    min_part = MIN_PART if min_part is None else min_part
     max_ctx = max(32, max_ctx)
     base = max(1, num_tiles * n_kv)
     if base >= target_wgs // 2:

@@ -217,7 +217,8 @@ def test_attention_spike_rescale(gpu):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,V", [(1, 128256), (64, 128256), (5, 32000), (3, 1000), (2, 1003)])
+@pytest.mark.parametrize("n,V", [(1, 128256), (2, 128256), (64, 128256), (5, 32000), (100, 32000), (3, 1000),
+                                 (2, 1003), (1, 16040)])
 def test_argmax(gpu, n, V, dtype):
     if V % (8 if dtype == torch.bfloat16 else 4):
         pytest.skip("rows must be 16-B aligned")
@@ -263,6 +264,69 @@ def test_gemm(gpu, M, N, K):
         ops.GEMM_BACKEND = "auto"
     exp = (x.float() @ w.float().t())
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1280, 8192), (8192, 1024),
+                                 (8192, 3584), (16, 1024)])
+def test_gemv(gpu, M, N, K):
+    """K2 skinny GEMV (gemv.hip, M <= 4; M = 5 / 8 take the MFMA tiles): wave-per-row-pair
+    (N >= 4096) and the 4-waves-split-K form (N = 1280 / 16: 70B TP=8 shards, tiny N), K
+    not a multiple of the unrolled stride (1024, 3584); vs fp32 matmul."""
+    torch.manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
+    if M <= 4:
+        assert torch.ops.mlop.gemm_workspace(M, N, K, 0) == 0  # no split-K slabs on this path
+    y = torch.empty(M, N, device=gpu, dtype=bf)
+    nws = torch.ops.mlop.gemm_workspace(M, N, K, 0)
+    torch.ops.mlop.gemm(y, x, w, torch.empty(max(nws, 0), device=gpu), 0)
+    exp = x.float() @ w.float().t()
+    close(y, exp, atol=2e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("I,K", [(14336, 4096), (3584, 8192)])
+def test_gemv_silu_mul(gpu, M, I, K):
+    torch.manual_seed(M + I)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    g = (0.05 * torch.randn(I, K, device=gpu)).to(bf)
+    u = (0.05 * torch.randn(I, K, device=gpu)).to(bf)
+    w = ops.interleave_gate_up(g, u)
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
+    finally:
+        ops.GEMM_BACKEND = "auto"
+    gu = (x.float() @ torch.cat([g, u]).float().t()).to(bf)
+    close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (3, 32, 8), (4, 32, 8), (2, 8, 1), (4, 64, 8)])
+def test_gemv_rope_cache(gpu, M, Hq, Hkv):
+    """Decode QKV GEMV with RoPE + paged K/V stores in its epilogue (EPI_ROPE at M <= 8)."""
+    from mlopamd.models.layers import rope_table
+
+    D, K, BS, NB = 128, 4096, 16, 64
+    N = (Hq + 2 * Hkv) * D
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
+    if M > 2:
+        slots[1] = -1  # padding row: no cache write
+    assert torch.ops.mlop.gemm_rope_supported(M, N, K)
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
+    assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
+    qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref)
+    close(kc, kr)
+    close(vc, vr)
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (64, 4096, 14336), (256, 4096, 4096), (256, 4096, 14336)])
