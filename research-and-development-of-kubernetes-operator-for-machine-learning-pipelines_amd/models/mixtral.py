@@ -48,6 +48,11 @@ class MixtralModel(LlamaModel):
         return moe_forward(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.ps.ep,
                            self.expert_start, self.n_local_experts, mode=mode)
 
+    def post_attention(self, i, o, residual, eps):
+        """MoE block in the decode forward: the router / grouped GEMM take a normed x."""
+        x = ops.add_rmsnorm(o, residual, self.layers[i]["post_norm"], eps)
+        return self.mlp(i, x), residual
+
     def mlp_add_norm(self, i, x, residual, next_norm, eps):
         return ops.add_rmsnorm(self.mlp(i, x), residual, next_norm, eps)
 

@@ -338,6 +338,54 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
     return fused() if c in (None, "mlop") else unfused()
 
 
+# Residual add + RMSNorm as the decode GEMV's prologue (gemv.hip NORM).  Measured a wash at
+# batch 1 (315-318 vs 318 tok/s unfused, scripts/run41.sh: the two norm launches it removes
+# cost what the heavier prologue adds to the two GEMVs) and a loss at batch 2-4, so it is
+# opt-in: MLOP_NORM_FUSION=1.
+NORM_FUSION = os.environ.get("MLOP_NORM_FUSION", "0") == "1"
+
+
+def norm_fusable(M: int, N: int, K: int, epi: int) -> bool:
+    """True when the residual add + RMSNorm can ride in the consuming projection
+    (decode sizes: the GEMV's NORM prologue, gemv.hip)."""
+    if not NORM_FUSION:
+        return False
+    _need_gpu()
+    return bool(torch.ops.mlop.gemm_norm_supported(M, N, K, epi))
+
+
+def norm_gemm(y, residual, norm_w, w, eps: float, epi: int = EPI_NONE):
+    """(epi(rmsnorm(residual + y) * norm_w @ w^T), residual + y) in ONE launch at decode
+    sizes (the add + norm become the GEMV's prologue); otherwise add_rmsnorm (residual
+    updated in place) + gemm.  Callers must use the returned residual."""
+    M, K = y.shape[0], y.shape[-1]
+    N = w.shape[0]
+    if y.is_cuda and norm_fusable(M, N, K, epi):
+        res_out = torch.empty_like(residual)
+        out = torch.empty(M, N if epi == EPI_NONE else N // 2, dtype=y.dtype, device=y.device)
+        if torch.ops.mlop.gemm_norm(out, res_out, y, residual, norm_w, w, eps, epi):
+            return out, res_out
+    x = add_rmsnorm(y, residual, norm_w, eps)
+    return gemm(x, w, epi=epi), residual
+
+
+def norm_qkv_rope_cache(y, residual, norm_w, w, positions, cos_sin, slots, k_cache, v_cache,
+                        n_q_heads: int, eps: float):
+    """QKV projection of the next layer with the previous layer's residual add + RMSNorm
+    as its prologue and RoPE + paged K/V stores as its epilogue (one launch at decode
+    sizes).  Returns (q, new residual)."""
+    M, K = y.shape[0], y.shape[-1]
+    N = w.shape[0]
+    if y.is_cuda and norm_fusable(M, N, K, EPI_ROPE):
+        res_out = torch.empty_like(residual)
+        q = torch.empty(M, n_q_heads, k_cache.shape[3], dtype=y.dtype, device=y.device)
+        if torch.ops.mlop.gemm_norm_rope(q, k_cache, v_cache, res_out, y, residual, norm_w, w, positions,
+                                         cos_sin, slots, eps):
+            return q, res_out
+    x = add_rmsnorm(y, residual, norm_w, eps)
+    return qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads), residual
+
+
 GEMM_TABLE = Path(os.environ.get("MLOP_GEMM_TABLE", str(Path(__file__).with_name("gemm_table_gfx950.json"))))
 
 

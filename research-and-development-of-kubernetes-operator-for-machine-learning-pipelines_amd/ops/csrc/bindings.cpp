@@ -251,6 +251,61 @@ bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor no
                                        cur_stream());
 }
 
+// Decode projection with the residual add + RMSNorm feeding it fused in as a prologue
+// (gemv.hip NORM, M <= 4): res_out = bf16(res_in + y); out = epi(rmsnorm(res_out) * norm_w @ w^T).
+// epi 0 / 1 write out [M, N or N/2]; epi 3 (RoPE) writes q_out / k_cache / v_cache instead.
+// false = shape not on this path (caller runs add_rmsnorm + the projection).
+bool gemm_norm_impl(Tensor* out, Tensor* q_out, Tensor* k_cache, Tensor* v_cache, Tensor res_out,
+                    Tensor y, Tensor res_in, Tensor norm_w, Tensor w, const Tensor* pos,
+                    const Tensor* cos_sin, const Tensor* slots, double eps, int64_t epi) {
+  check_bf16(res_out, "res_out"); check_bf16(y, "y"); check_bf16(res_in, "res_in");
+  check_bf16(norm_w, "norm_w"); check_bf16(w, "w");
+  const int64_t N = w.size(0), K = w.size(1), M = y.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(w.dim() == 2 && y.numel() == M * K && res_in.numel() == M * K && res_out.numel() == M * K &&
+                  norm_w.numel() == K, "y / residual [M, K], norm_w [K], w [N, K]");
+  TORCH_CHECK(res_out.data_ptr() != res_in.data_ptr(), "res_out must not alias res_in");
+  if (!mlop::gemv_norm_takes((int)M, (int)N, (int)K, (int)epi)) return false;
+  mlop::NormPro np{(const uint16_t*)y.data_ptr(), (const uint16_t*)res_in.data_ptr(),
+                   (uint16_t*)res_out.data_ptr(), (const uint16_t*)norm_w.data_ptr(), (float)eps};
+  c10::DeviceGuard g(y.device());
+  if (epi == 3) {
+    check_bf16(*q_out, "q_out"); check_bf16(*k_cache, "k_cache"); check_bf16(*v_cache, "v_cache");
+    check_i32(*pos, "pos"); check_i32(*slots, "slots");
+    const int64_t Hq = q_out->size(1), D = q_out->size(2), Hkv = k_cache->size(1), BS = k_cache->size(2);
+    TORCH_CHECK(D == 128 && N == (Hq + 2 * Hkv) * D && q_out->size(0) == M && pos->numel() == M &&
+                    slots->numel() == M && v_cache->size(2) == D && v_cache->size(3) == BS,
+                "qkv layout: head_dim 128, q_out [M, Hq, 128], k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+    TORCH_CHECK(cos_sin->is_cuda() && cos_sin->scalar_type() == at::kFloat && cos_sin->size(1) == D, "cos_sin");
+    mlop::RopeEpi re{(uint16_t*)q_out->data_ptr(), (uint16_t*)k_cache->data_ptr(),
+                     (uint16_t*)v_cache->data_ptr(), pos->data_ptr<int>(), cos_sin->data_ptr<float>(),
+                     slots->data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
+    mlop::launch_gemv_norm(np, w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re, cur_stream());
+    return true;
+  }
+  check_bf16(*out, "out");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi");
+  TORCH_CHECK(out->numel() == M * (epi == 0 ? N : N / 2), "out [M, N or N/2]");
+  mlop::launch_gemv_norm(np, w.data_ptr(), out->data_ptr(), (int)(epi == 0 ? N : N / 2), (int)M, (int)N,
+                         (int)K, (int)epi, mlop::RopeEpi{}, cur_stream());
+  return true;
+}
+
+bool gemm_norm(Tensor out, Tensor res_out, Tensor y, Tensor res_in, Tensor norm_w, Tensor w, double eps,
+               int64_t epi) {
+  return gemm_norm_impl(&out, nullptr, nullptr, nullptr, res_out, y, res_in, norm_w, w, nullptr, nullptr,
+                        nullptr, eps, epi);
+}
+
+bool gemm_norm_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor res_out, Tensor y, Tensor res_in,
+                    Tensor norm_w, Tensor w, Tensor pos, Tensor cos_sin, Tensor slots, double eps) {
+  return gemm_norm_impl(nullptr, &q_out, &k_cache, &v_cache, res_out, y, res_in, norm_w, w, &pos, &cos_sin,
+                        &slots, eps, 3);
+}
+
+bool gemm_norm_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return mlop::gemv_norm_takes((int)M, (int)N, (int)K, (int)epi);
+}
+
 // grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
 void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi) {
   check_bf16(out, "out"); check_bf16(a, "a"); check_bf16(w, "w"); check_i32(offsets, "offsets");
@@ -391,6 +446,12 @@ TORCH_LIBRARY(mlop, m) {
         "int epi) -> ()");
   m.def("gemm_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor a, Tensor w, Tensor norm_w, "
         "Tensor(c!) ws, float eps) -> bool");
+  m.def("gemm_norm_supported(int M, int N, int K, int epi) -> bool", &gemm_norm_supported);
+  m.def("gemm_norm(Tensor(a!) out, Tensor(b!) res_out, Tensor y, Tensor res_in, Tensor norm_w, Tensor w, "
+        "float eps, int epi) -> bool");
+  m.def("gemm_norm_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor(d!) res_out, "
+        "Tensor y, Tensor res_in, Tensor norm_w, Tensor w, Tensor pos, Tensor cos_sin, Tensor slots, "
+        "float eps) -> bool");
   m.def("moe_route(Tensor(a!) topw, Tensor(b!) topi, Tensor logits) -> ()");
   m.def("moe_permute(Tensor(a!) xp, Tensor(b!) offsets, Tensor(c!) src, Tensor(d!) inv, Tensor x, "
         "Tensor topi, int e0, int n_local) -> ()");
@@ -424,6 +485,8 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);
   m.impl("gemm_rope_cache", &gemm_rope_cache);
+  m.impl("gemm_norm", &gemm_norm);
+  m.impl("gemm_norm_rope", &gemm_norm_rope);
   m.impl("moe_route", &moe_route);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);

@@ -29,6 +29,13 @@
 //                 stores q to q_out and k / v straight into the paged cache
 //                 (rope_cache.hip's math and layouts, no [M, N] round trip, one
 //                 launch fewer per layer).
+// Prologue NORM (the decoder's residual add + RMSNorm feeding this projection, one
+// launch fewer per norm): instead of loading A, every activation chunk is formed from
+// the previous projection's output y and the residual stream, r = bf16(res + y), and
+// x = bf16(r * norm_w); sum(r^2) accumulates beside the dots and the row's
+// rsqrt(mean(r^2) + eps) scales the finished sums (a per-row scalar commutes with the
+// dot; vs the unfused bf16(bf16(r * inv) * w) it skips one rounding).  The set-0 wave(s)
+// also store r to res_out (a different buffer than res_in: other waves still read it).
 #include <stdlib.h>
 
 #include "common.h"
@@ -55,11 +62,11 @@ __device__ __forceinline__ float dot8(const u32x4& w, const u32x4& x, float c) {
   return dot2(w.w, x.w, c);
 }
 
-template <int M, int RP, int EPI, int KW, int U>
+template <int M, int RP, int EPI, int KW, int U, bool NORM>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ B, int ldb,
                                                    uint16_t* __restrict__ C, int ldc, int N, int K,
-                                                   RopeEpi re) {
+                                                   RopeEpi re, NormPro np) {
   constexpr int R = 2 * RP;  // weight rows per wave
   static_assert(EPI != EPI_ROPE || RP == 1, "rope sets are single row pairs");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -101,6 +108,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+  float ss[M];  // NORM: sum of r^2 over this lane's chunks
+#pragma unroll
+  for (int m = 0; m < M; ++m) ss[m] = 0.f;
+  const bool writer = NORM && (KW == 1 ? set == 0 : blockIdx.x == 0);
 
   const int lane_off = (KW == 1 ? 0 : wv * 64) + lane;
   constexpr int STEP = 64 * KW;  // chunk stride between a lane's consecutive loads
@@ -112,8 +123,29 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       const bool ok = c < KC;
 #pragma unroll
       for (int r = 0; r < R; ++r) w[u][r] = ok ? __builtin_nontemporal_load(Bv[r] + c) : u32x4{0, 0, 0, 0};
+      if constexpr (NORM) {
+        const u32x4 wn = ok ? reinterpret_cast<const u32x4*>(np.w)[c] : u32x4{0, 0, 0, 0};
 #pragma unroll
-      for (int m = 0; m < M; ++m) x[u][m] = ok ? Av[m][c] : u32x4{0, 0, 0, 0};
+        for (int m = 0; m < M; ++m) {
+          u32x4 rr = u32x4{0, 0, 0, 0};
+          if (ok) {
+            const u32x4 ya = reinterpret_cast<const u32x4*>(np.y + (size_t)m * K)[c];
+            const u32x4 ra = reinterpret_cast<const u32x4*>(np.res_in + (size_t)m * K)[c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rr[j] = pack2(lo_bf(ya[j]) + lo_bf(ra[j]), hi_bf(ya[j]) + hi_bf(ra[j]));
+            if (writer) reinterpret_cast<u32x4*>(np.res_out + (size_t)m * K)[c] = rr;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float a0 = lo_bf(rr[j]), a1 = hi_bf(rr[j]);
+            ss[m] += a0 * a0 + a1 * a1;
+            x[u][m][j] = pack2(a0 * lo_bf(wn[j]), a1 * hi_bf(wn[j]));
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < M; ++m) x[u][m] = ok ? Av[m][c] : u32x4{0, 0, 0, 0};
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -127,26 +159,42 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+  if constexpr (NORM) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = wave_sum(ss[m]);
+  }
 
   if constexpr (KW > 1) {
-    __shared__ float red[KW][R * M];
+    constexpr int NV = R * M + (NORM ? M : 0);
+    __shared__ float red[KW][NV];
     if (lane == 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m) red[wv][r * M + m] = acc[r][m];
+      if constexpr (NORM) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) red[wv][R * M + m] = ss[m];
+      }
     }
     __syncthreads();
     if (wv != 0) return;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int i = 0; i < NV; ++i) {
+      float t = 0.f;
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        float s = 0.f;
+      for (int k = 0; k < KW; ++k) t += red[k][i];
+      if (i < R * M) acc[i / M][i % M] = t;
+      else if constexpr (NORM) ss[i - R * M] = t;
+    }
+  }
+  if constexpr (NORM) {
 #pragma unroll
-        for (int k = 0; k < KW; ++k) s += red[k][r * M + m];
-        acc[r][m] = s;
-      }
+    for (int m = 0; m < M; ++m) {
+      const float inv = rsqrtf(ss[m] / (float)K + np.eps);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][m] *= inv;
+    }
   }
 
   // every lane holds every sum now; lane j stores output j of the set
@@ -208,9 +256,9 @@ int gemv_max_m() {
   return max_m;
 }
 
-template <int M, int EPI>
+template <int M, int EPI, bool NORM>
 void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int N,
-                int K, const RopeEpi& re, hipStream_t st) {
+                int K, const RopeEpi& re, const NormPro& np, hipStream_t st) {
   constexpr int U = M <= 2 ? 4 : 2;  // chunks per row in flight per lane (VGPR budget)
   // sets of RP row pairs; aim for >= 2048 waves in flight (8 per CU), else KW = 4
   const int pairs = N / 2;
@@ -220,7 +268,8 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
-    gemv_kernel<M, RP, EPI, KW, U><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, N, K, re);      \
+    gemv_kernel<M, RP, EPI, KW, U, NORM><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, N, K, re, \
+                                                                  np);                        \
   } while (0)
   if constexpr (EPI == EPI_ROPE) {
     if (kw4) MLOP_GEMV(1, 4); else MLOP_GEMV(1, 1);
@@ -234,18 +283,27 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 #undef MLOP_GEMV
 }
 
-template <int EPI>
+template <int EPI, bool NORM = false>
 void run_gemv(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
-              int N, int K, const RopeEpi& re, hipStream_t st) {
+              int N, int K, const RopeEpi& re, hipStream_t st, const NormPro& np = NormPro{}) {
+  if constexpr (NORM) {  // the fused-norm prologue is built for the decode sizes only (M <= 4)
+    switch (M) {
+      case 1: run_gemv_m<1, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 2: run_gemv_m<2, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 3: run_gemv_m<3, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      default: run_gemv_m<4, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    }
+    return;
+  }
   switch (M) {
-    case 1: run_gemv_m<1, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 2: run_gemv_m<2, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 3: run_gemv_m<3, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 4: run_gemv_m<4, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 5: run_gemv_m<5, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 6: run_gemv_m<6, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    case 7: run_gemv_m<7, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
-    default: run_gemv_m<8, EPI>(A, lda, B, ldb, C, ldc, N, K, re, st); break;
+    case 1: run_gemv_m<1, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 2: run_gemv_m<2, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 3: run_gemv_m<3, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 4: run_gemv_m<4, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 5: run_gemv_m<5, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 6: run_gemv_m<6, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 7: run_gemv_m<7, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    default: run_gemv_m<8, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
   }
 }
 
@@ -274,6 +332,25 @@ void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ld
 void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st) {
   run_gemv<EPI_ROPE>((const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, M, N, K, re, st);
+}
+
+// residual add + RMSNorm fused into the projection that consumes it (prologue NORM):
+// C = epi(rmsnorm(res_in + y) @ B^T), res_out = bf16(res_in + y); M <= 4 only.
+// Each wave re-forms the normed activations of every K chunk it streams, so the prologue's
+// VALU work grows with M: measured (scripts/run40.sh) it pays at M = 1 (-5 us per layer) and
+// loses at M = 2 / 4 (gate_up turns VALU-bound); MLOP_NORM_FUSION_MAX_M (default 1, max 4).
+bool gemv_norm_takes(int M, int N, int K, int epi) {
+  static const int max_m = std::min(4, env_int("MLOP_NORM_FUSION_MAX_M", 1));
+  return M <= max_m && gemv_takes(M, N, K, epi);
+}
+
+void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M, int N, int K, int epi,
+                      const RopeEpi& re, hipStream_t st) {
+  auto* b = (const uint16_t*)B;
+  auto* c = (uint16_t*)C;
+  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+  else if (epi == EPI_ROPE) run_gemv<EPI_ROPE, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+  else run_gemv<EPI_NONE, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
 }
 
 }  // namespace mlop

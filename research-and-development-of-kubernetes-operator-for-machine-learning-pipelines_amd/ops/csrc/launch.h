@@ -48,6 +48,17 @@ void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ld
                  int epi, hipStream_t st);
 void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st);
+// residual add + RMSNorm prologue (gemv.hip NORM): rows of y / res_in / res_out are K wide
+struct NormPro {
+  const uint16_t* y;
+  const uint16_t* res_in;
+  uint16_t* res_out;
+  const uint16_t* w;
+  float eps;
+};
+bool gemv_norm_takes(int M, int N, int K, int epi);
+void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M, int N, int K, int epi,
+                      const RopeEpi& re, hipStream_t st);
 bool gemm_rope_supported(int M, int N, int K);
 bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st);

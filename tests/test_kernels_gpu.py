@@ -425,3 +425,64 @@ def test_moe_pipeline(gpu, T, E, k, H, I):
                 exp[t] += w[t, j] * h.to(bf).float()
         close(out, exp, atol=3e-2, rtol=3e-2)
         assert n == int(((idx >= e0) & (idx < e0 + nl)).sum())
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("epi,N,K", [(0, 4096, 4096), (1, 28672, 4096), (0, 1280, 8192), (1, 7168, 8192)])
+def test_norm_gemm_fused(gpu, M, epi, N, K):
+    """Residual add + RMSNorm as the GEMV's prologue (gemv.hip NORM) vs add_rmsnorm + fp32
+    matmul: the new residual is bit-exact, the output within bf16 tolerance (the fused form
+    applies 1/rms after the dot, one rounding fewer)."""
+    torch.manual_seed(M + N + K)
+    y = torch.randn(M, K, device=gpu, dtype=bf)
+    res = torch.randn(M, K, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(bf)
+    w = (0.03 * torch.randn(N, K, device=gpu)).to(bf)
+    ops.NORM_FUSION = True  # opt-in path (MLOP_NORM_FUSION=1)
+    try:
+        fused = ops.norm_fusable(M, N, K, epi)
+    finally:
+        ops.NORM_FUSION = False
+    assert fused == (M == 1)  # MLOP_NORM_FUSION_MAX_M default
+    ops.NORM_FUSION = True
+    try:
+        out, r2 = ops.norm_gemm(y, res.clone(), nw, w, 1e-5, epi)
+    finally:
+        ops.NORM_FUSION = False
+    x_ref, r_ref = ref.add_rmsnorm(y, res, nw, 1e-5)
+    assert torch.equal(r2.cpu(), r_ref.cpu())
+    exp = (x_ref.float() @ ops.deinterleave_rows(w).float().t() if epi else x_ref.float() @ w.float().t())
+    if epi:  # SiLU-mul amplifies the one-rounding-fewer difference of the deferred 1/rms
+        exp = ref.silu_mul(exp.to(bf))
+    close(out, exp, atol=1.5e-1 if epi else 3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (4, 32, 8), (2, 8, 1)])
+def test_norm_qkv_rope_fused(gpu, M, Hq, Hkv):
+    from mlopamd.models.layers import rope_table
+
+    D, K, BS, NB = 128, 4096, 16, 32
+    N = (Hq + 2 * Hkv) * D
+    torch.manual_seed(M + Hq)
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    y = torch.randn(M, K, device=gpu, dtype=bf)
+    res = torch.randn(M, K, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    ops.NORM_FUSION = True
+    try:
+        q, r2 = ops.norm_qkv_rope_cache(y, res.clone(), nw, w, pos, cs, slots, kc, vc, Hq, 1e-5)
+    finally:
+        ops.NORM_FUSION = False
+    x_ref, r_ref = ref.add_rmsnorm(y, res, nw, 1e-5)
+    assert torch.equal(r2.cpu(), r_ref.cpu())
+    qkv_ref = (x_ref.float() @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref, atol=3e-2, rtol=3e-2)
+    close(kc, kr, atol=3e-2, rtol=3e-2)
+    close(vc, vr, atol=3e-2, rtol=3e-2)
