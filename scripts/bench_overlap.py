@@ -116,3 +116,97 @@ for _ in range(2):
         res[name] = min(res.get(name, 1e9), t)
 print(json.dumps(dict(M=M_TOTAL, B=B_TOTAL, ctx=CTX, layers=LAYERS, **{k: round(v, 2) for k, v in res.items()},
                       gemm_backends=ops.gemm_choices())), flush=True)
+
+
+# ---------------------------------------------------------------------------------------
+# CU-partitioned pipeline (ATTN_CUS > 0): GEMMs on a stream masked to the other CUs,
+# decode attention on a stream masked to ATTN_CUS CUs (the same number in every XCD whether
+# the CU ids count XCD-major (i // 32) or round-robin (i % 8)),
+# two half batches interleaved so one half's attention runs beside the other half's MLP:
+#   G: qkvA(l) mlpB(l-1) qkvB(l) mlpA(l) ...      T: attnA(l) attnB(l) ...
+def cu_mask_stream(cus):
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    words = [0] * ((n + 31) // 32)
+    for i in cus:
+        words[i // 32] |= 1 << (i % 32)
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    h = ctypes.c_void_p()
+    err = lib.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
+    assert err == 0, f"hipExtStreamCreateWithCUMask: {err}"
+    return torch.cuda.ExternalStream(h.value)
+
+
+ATTN_CUS = int(os.environ.get("ATTN_CUS", 0))
+if ATTN_CUS:
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    per = ATTN_CUS // 8  # attention CUs per 32-CU block, spread over the mod-8 classes too
+    # balanced pick: in 32-CU block b take CUs b*32 + 4*k + (b % 4), k < per
+    attn_set = [b * 32 + 4 * k + (b % 4) for b in range(n // 32) for k in range(per)]
+    gemm_set = [i for i in range(n) if i not in set(attn_set)]
+    G, Tst = cu_mask_stream(gemm_set), cu_mask_stream(attn_set)
+
+    def mlp(h):
+        ops.gemm(h.x, w_o)
+        a = ops.gemm(h.x, w_gu, epi=ops.EPI_SILU_MUL)
+        ops.gemm(a, w_dn)
+
+    def pipelined():
+        cur = torch.cuda.current_stream()
+        G.wait_stream(cur)
+        Tst.wait_stream(cur)
+        ev = {}
+        for l in range(LAYERS):
+            for h, tag in ((ha, "A"), (hb, "B")):
+                with torch.cuda.stream(G):
+                    ops.gemm(h.x, w_qkv)
+                    e = torch.cuda.Event()
+                    e.record(G)
+                with torch.cuda.stream(Tst):
+                    Tst.wait_event(e)
+                    ops.paged_attention(h.q, h.kc, h.vc, h.meta)
+                    ea = torch.cuda.Event()
+                    ea.record(Tst)
+                # the OTHER half's MLP of the previous step runs now on G
+                other, otag = (hb, "B") if tag == "A" else (ha, "A")
+                key = "pending" + otag
+                if key in ev:
+                    with torch.cuda.stream(G):
+                        G.wait_event(ev.pop(key))
+                        mlp(other)
+                ev["pending" + tag] = ea
+        for tag, h in (("A", ha), ("B", hb)):
+            if "pending" + tag in ev:
+                with torch.cuda.stream(G):
+                    G.wait_event(ev.pop("pending" + tag))
+                    mlp(h)
+        cur.wait_stream(G)
+        cur.wait_stream(Tst)
+
+    def attn_masked():
+        cur = torch.cuda.current_stream()
+        Tst.wait_stream(cur)
+        with torch.cuda.stream(Tst):
+            for _ in range(LAYERS):
+                ops.paged_attention(ha.q, ha.kc, ha.vc, ha.meta)
+        cur.wait_stream(Tst)
+
+    def gemm_masked():
+        cur = torch.cuda.current_stream()
+        G.wait_stream(cur)
+        with torch.cuda.stream(G):
+            for _ in range(LAYERS):
+                ops.gemm(ha.x, w_qkv)
+                mlp(ha)
+        cur.wait_stream(G)
+
+    r2 = {}
+    for _ in range(2):
+        for name, fn in (("pipelined", pipelined), ("halves_serial", halves_serial),
+                         ("half_attn_on_attn_cus", attn_masked), ("half_gemms_on_gemm_cus", gemm_masked)):
+            t = timeit(fn)
+            r2[name] = min(r2.get(name, 1e9), t)
+    print(json.dumps(dict(M=M_TOTAL, B=B_TOTAL, ctx=CTX, layers=LAYERS, attn_cus=len(attn_set),
+                          **{k: round(v, 2) for k, v in r2.items()})), flush=True)
