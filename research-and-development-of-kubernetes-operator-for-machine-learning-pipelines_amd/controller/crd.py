@@ -34,6 +34,7 @@ EV_PROMOTION_FAILED = "PromotionFailed"
 EV_PROMOTION_COMPLETE = "PromotionComplete"
 EV_ROLLBACK_COMPLETE = "RollbackComplete"
 EV_PREDICTOR_READY = "PredictorReady"
+EV_PREDICTOR_UNAVAILABLE = "PredictorUnavailable"
 EV_REGISTRY_UNAVAILABLE = "RegistryUnavailable"
 
 
@@ -55,6 +56,7 @@ class CanaryPolicy:
     latency_floor_s: float = 0.0    # latencies below this always pass (0 = reference)
     window_s: int = 60              # PromQL range (mlflow_operator.py:363)
     ready_timeout_s: float = 1800.0  # wait for the new predictor's readiness before gating
+    max_restarts: int = 3            # a canary predictor restarted this often is rolled back
     # GPU-side guards {metric: max new/old ratio} over prometheus.gpu_guard_queries;
     # skipped for predictors that do not export the series (reference runtimes)
     gpu_guards: dict = field(default_factory=lambda: {
@@ -77,6 +79,7 @@ class CanaryPolicy:
                    latency_floor_s=float(c.get("latencyFloorSeconds", base.latency_floor_s)),
                    window_s=int(c.get("windowSeconds", base.window_s)),
                    ready_timeout_s=float(c.get("readyTimeoutSeconds", base.ready_timeout_s)),
+                   max_restarts=int(c.get("maxRestarts", base.max_restarts)),
                    gpu_guards=dict(base.gpu_guards if c.get("gpuGuards") is None else c["gpuGuards"]))
 
 

@@ -48,6 +48,8 @@ class Pod:
     proc: subprocess.Popen | None = None
     task: asyncio.Task | None = None
     extra: dict = field(default_factory=dict)
+    restarts: int = 0
+    last_error: str = ""
 
     @property
     def key(self):
@@ -84,6 +86,11 @@ class InProcessLauncher:
             b.stop()
         pod.ready = False
 
+    def alive(self, pod: Pod):
+        """None = running, else the reason it is gone."""
+        b = pod.backend
+        return getattr(b, "failure", None) if b is not None else None
+
 
 def free_port() -> int:
     with socket.socket() as s:
@@ -112,15 +119,22 @@ class ProcessLauncher:
         env["SELDON_NAMESPACE"] = pod.namespace
         repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+        import tempfile
+
+        # stderr to a file: the tail of a dead predictor's log becomes the reason the SD
+        # status and the CR report (`kubectl logs --previous` in a real cluster)
+        pod.extra["log"] = log_f = tempfile.NamedTemporaryFile(prefix=f"mlop-{pod.predictor}-", suffix=".log",
+                                                             delete=False)
         pod.proc = subprocess.Popen([self.python, "-m", "mlopamd.runtime.server", "--port", str(port),
                                      "--host", "127.0.0.1"], env=env, stdout=subprocess.DEVNULL,
-                                    stderr=subprocess.DEVNULL, start_new_session=True)
+                                    stderr=log_f, start_new_session=True)
         pod.endpoint = f"http://127.0.0.1:{port}"
         t0 = time.monotonic()
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as s:
             while time.monotonic() - t0 < self.ready_timeout_s:
                 if pod.proc.poll() is not None:
-                    raise RuntimeError(f"predictor {pod.predictor} exited with {pod.proc.returncode}")
+                    raise RuntimeError(f"predictor {pod.predictor} exited with {pod.proc.returncode}: "
+                                       f"{self._log_tail(pod)}")
                 try:
                     async with s.get(pod.endpoint + "/v2/health/ready") as r:
                         if r.status == 200:
@@ -132,6 +146,25 @@ class ProcessLauncher:
         if self.scraper is not None:
             self.scraper.add_target(pod.endpoint + "/metrics")
 
+    def alive(self, pod: Pod):
+        if pod.proc is None or pod.proc.poll() is None:
+            return None
+        return f"process exited with code {pod.proc.returncode}: {self._log_tail(pod)}"
+
+    @staticmethod
+    def _log_tail(pod: Pod, n: int = 240) -> str:
+        f = pod.extra.get("log")
+        if f is None:
+            return ""
+        try:
+            with open(f.name, "rb") as fh:
+                fh.seek(0, 2)
+                fh.seek(max(0, fh.tell() - 4096))
+                lines = [ln for ln in fh.read().decode("utf-8", "replace").splitlines() if ln.strip()]
+            return (lines[-1] if lines else "")[-n:]
+        except OSError:
+            return ""
+
     async def stop(self, pod: Pod):
         if self.scraper is not None and pod.endpoint:
             self.scraper.remove_target(pod.endpoint + "/metrics")
@@ -141,6 +174,13 @@ class ProcessLauncher:
                 pod.proc.wait(timeout=10)
             except subprocess.TimeoutExpired:
                 pod.proc.kill()
+        f = pod.extra.pop("log", None)
+        if f is not None:
+            f.close()
+            try:
+                os.unlink(f.name)
+            except OSError:
+                pass
         pod.ready = False
 
 
@@ -150,7 +190,10 @@ class SimLauncher:
     Seldon executor would (cumulative histogram buckets, counts per code).
     ``profiles[version] = {"latency": s, "error_rate": f, "startup_s": s}``; an LLM
     predictor profile may add ``tpot`` (s per output token), ``gpu_mem`` (bytes)
-    and ``gpu_power`` (W): the runtime's TPOT histogram and amd-smi gauges."""
+    and ``gpu_power`` (W): the runtime's TPOT histogram and amd-smi gauges.
+    Fault injection: ``fail_start`` (message: the predictor dies while starting, e.g.
+    "HIP out of memory"), ``crash_after_s`` (it dies that long after becoming ready;
+    ``crashes`` = how many times, default forever: a crash loop)."""
 
     BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0)
 
@@ -164,8 +207,25 @@ class SimLauncher:
         startup = prof.get("startup_s", 0.0)
         if startup:
             await self.clock.sleep(startup)
+        if prof.get("fail_start"):
+            raise RuntimeError(str(prof["fail_start"]))
         pod.ready = True
+        pod.extra["started_at"] = self.clock.now()
+        pod.extra.pop("dead", None)
         pod.task = asyncio.get_running_loop().create_task(self._emit(pod, prof))
+
+    def alive(self, pod: Pod):
+        prof = self.profiles.get(pod.predictor[1:], {})
+        after = prof.get("crash_after_s")
+        if pod.extra.get("dead"):
+            return pod.extra["dead"]
+        if after is not None and pod.ready and pod.restarts < int(prof.get("crashes", 1 << 30)):
+            if self.clock.now() - pod.extra.get("started_at", self.clock.now()) >= float(after):
+                if pod.task:
+                    pod.task.cancel()
+                pod.extra["dead"] = "process exited with code 139 (segmentation fault)"
+                return pod.extra["dead"]
+        return None
 
     async def _emit(self, pod: Pod, prof: dict):
         lbl = {"deployment_name": pod.sd, "predictor_name": pod.predictor, "namespace": pod.namespace}
@@ -211,19 +271,60 @@ class SimLauncher:
 class FakeSeldonController:
     """Turns SeldonDeployments into pods and reports their availability."""
 
+    # kubelet-style restart policy: liveness probe period and CrashLoopBackOff (10 s doubling, 300 s cap)
+    PROBE_PERIOD_S = 5.0
+    BACKOFF_S, BACKOFF_MAX_S = 10.0, 300.0
+
     def __init__(self, kube, launcher, clock=None):
         self.kube, self.launcher, self.clock = kube, launcher, clock or RealClock()
         self.pods: dict[tuple, Pod] = {}
+        self._probe = None
         self.traffic: dict[tuple, int] = {}
         self._task = None
         self._starting: dict[tuple, asyncio.Task] = {}
         self._seen_gen: dict[tuple, int | None] = {}
 
     def start(self):
-        self._task = asyncio.get_running_loop().create_task(self._run())
+        loop = asyncio.get_running_loop()
+        self._task = loop.create_task(self._run())
+        if hasattr(self.launcher, "alive"):
+            self._probe = loop.create_task(self._supervise())
         return self
 
+    async def _supervise(self):
+        """Liveness: a predictor that died is reported unavailable (restarts counted in
+        the SD status) and restarted after the CrashLoopBackOff delay, like the kubelet
+        does for the Seldon pods (restartPolicy Always)."""
+        while True:
+            await self.clock.sleep(self.PROBE_PERIOD_S)
+            for key, pod in list(self.pods.items()):
+                if not pod.ready or key in self._starting:
+                    continue
+                why = self.launcher.alive(pod)
+                if why is None:
+                    continue
+                pod.ready = False
+                pod.restarts += 1
+                pod.last_error = why
+                log.warning("predictor %s/%s/%s died (%s); restart %d", *key, why, pod.restarts)
+                await self._report(pod.namespace, pod.sd)
+                delay = min(self.BACKOFF_MAX_S, self.BACKOFF_S * 2 ** (pod.restarts - 1))
+                self._starting[key] = asyncio.get_running_loop().create_task(self._restart(pod, delay))
+
+    async def _restart(self, pod: Pod, delay: float):
+        await self.clock.sleep(delay)
+        if self.pods.get(pod.key) is not pod:  # removed meanwhile
+            self._starting.pop(pod.key, None)
+            return
+        try:
+            await self.launcher.stop(pod)
+        except Exception:  # noqa: BLE001
+            pass
+        await self._bring_up(pod)
+
     async def stop(self):
+        if self._probe:
+            self._probe.cancel()
         if self._task:
             self._task.cancel()
             try:
@@ -272,6 +373,7 @@ class FakeSeldonController:
         except Exception as e:  # noqa: BLE001
             log.error("predictor %s failed to start: %s", pod.predictor, e)
             pod.extra["error"] = str(e)
+            pod.last_error = str(e)
         finally:
             self._starting.pop(pod.key, None)
         await self._report(pod.namespace, pod.sd)
@@ -283,6 +385,9 @@ class FakeSeldonController:
             g = seldon.graph_name(pname[1:])
             ds[f"{name}-{pname}-0-{g}"] = {"replicas": int(pod.spec.get("replicas", 1)),
                                            "availableReplicas": int(pod.spec.get("replicas", 1)) if pod.ready else 0}
+            if pod.restarts or "error" in pod.extra:
+                ds[f"{name}-{pname}-0-{g}"].update(restarts=pod.restarts, failed="error" in pod.extra,
+                                                   reason=pod.last_error[:300])
         failed = any("error" in p.extra for p in mine.values())
         state = "Failed" if failed else ("Available" if mine and all(p.ready for p in mine.values()) else "Creating")
         try:

@@ -26,8 +26,8 @@ import asyncio
 import logging
 
 from . import seldon
-from .crd import (EV_ALIAS_NOT_FOUND, EV_NEW_VERSION, EV_PREDICTOR_READY, EV_PROMOTION_COMPLETE,
-                  EV_PROMOTION_FAILED, EV_REGISTRY_UNAVAILABLE, EV_ROLLBACK_COMPLETE,
+from .crd import (EV_ALIAS_NOT_FOUND, EV_NEW_VERSION, EV_PREDICTOR_READY, EV_PREDICTOR_UNAVAILABLE,
+                  EV_PROMOTION_COMPLETE, EV_PROMOTION_FAILED, EV_REGISTRY_UNAVAILABLE, EV_ROLLBACK_COMPLETE,
                   EV_TRAFFIC_INCREASE, GROUP, PLURAL, SELDON_GROUP, SELDON_PLURAL, SELDON_VERSION,
                   VERSION, ModelSpec, OperatorSettings, artifact_uri)
 from .kube import ApiError
@@ -246,19 +246,30 @@ class MlflowModelReconciler:
             sd = await self._get_sd(ns, name)
         # ---- readiness of the current predictor
         cur = status.get("currentModelVersion")
-        if cur is not None and status.get("ready") != "True" and seldon.predictor_ready(sd, seldon.predictor_name(cur)):
+        pcur = seldon.predictor_name(cur)
+        cur_ready = cur is not None and seldon.predictor_ready(sd, pcur)
+        if cur is not None and status.get("ready") != "True" and cur_ready:
             created = body["metadata"].get("creationTimestamp")
-            ready_patch = {"ready": "True", "readyTime": now}
+            first = status.get("readyTime") is None
+            ready_patch = {"ready": "True", "readyTime": now if first else status.get("readyTime")}
             if status.get("phase") == PH_DEPLOYING:
                 ready_patch["phase"] = PH_READY
             body = await self._patch_status(ns, name, ready_patch)
             status.update(ready_patch)
             dt = now - float(status.get("versionDetectedTime") or now)
-            if self.metrics:
+            if first and self.metrics:
                 self.metrics.observe_ready(dt)
             await self.op.event(body, "Normal", EV_PREDICTOR_READY,
-                                f"Predictor {seldon.predictor_name(cur)} ready {dt:.1f}s after version detection "
-                                f"(CR created {created}).")
+                                f"Predictor {pcur} ready {dt:.1f}s after version detection (CR created {created})."
+                                if first else f"Predictor {pcur} available again after a restart.")
+        elif cur is not None and status.get("ready") == "True" and sd is not None and not cur_ready:
+            # the serving predictor died (crash, GPU fault): the Seldon controller restarts
+            # it; surface the outage on the CR until it is back
+            restarts, _, reason = seldon.predictor_health(sd, pcur)
+            body = await self._patch_status(ns, name, {"ready": "False", "predictorRestarts": restarts})
+            status.update(ready="False", predictorRestarts=restarts)
+            await self.op.event(body, "Warning", EV_PREDICTOR_UNAVAILABLE,
+                                f"Predictor {pcur} unavailable (restart {restarts}): {reason}"[:1000])
         wait = interval
         if status.get("phase") == PH_CANARY:
             wait = min(wait, await self.canary_tick(body, ns, name, spec, status, sd, logger))
@@ -272,10 +283,20 @@ class MlflowModelReconciler:
         now = self.clock.now()
         cur, prev = status["currentModelVersion"], status.get("previousModelVersion")
         pc, pp = seldon.predictor_name(cur), seldon.predictor_name(prev)
+        restarts, failed, reason = seldon.predictor_health(sd, pc)
+        if failed or restarts >= pol.max_restarts:
+            # a canary that cannot start (GPU OOM at load) or crash-loops never gets
+            # healthy: fail it now instead of after ready_timeout (SURVEY.md §5 recovery)
+            why = (f"new predictor {pc} failed to start: {reason}" if failed else
+                   f"new predictor {pc} restarted {restarts} times: {reason}")
+            logger.warning("[%s/%s] %s", ns, name, why)
+            await self._fail(body, ns, name, spec, status, logger, why, unhealthy=True)
+            return 0.01
         if not seldon.predictor_ready(sd, pc):
             if now - float(status.get("canaryStepStarted", now)) > pol.ready_timeout_s:
                 logger.warning("[%s/%s] new predictor %s not ready after %.0fs", ns, name, pc, pol.ready_timeout_s)
-                await self._fail(body, ns, name, spec, status, logger, "new predictor never became ready")
+                await self._fail(body, ns, name, spec, status, logger, "new predictor never became ready",
+                                 unhealthy=True)
                 return 0.01
             return min(5.0, pol.attempt_delay_s)
         next_at = float(status.get("canaryNextAttempt", now))
@@ -320,12 +341,14 @@ class MlflowModelReconciler:
         await self._fail(body, ns, name, spec, status, logger, "; ".join(gate.reasons))
         return 0.01
 
-    async def _fail(self, body, ns, name, spec, status, logger, why: str):
+    async def _fail(self, body, ns, name, spec, status, logger, why: str, unhealthy: bool = False):
         pol = spec.canary
-        logger.warning("[%s/%s] Metrics did not meet conditions after %d attempts, stopping promotion.",
-                       ns, name, pol.max_attempts)
-        await self.op.event(body, "Warning", EV_PROMOTION_FAILED,
-                            f"Metrics did not meet conditions after {pol.max_attempts} attempts, stopping promotion.")
+        if unhealthy:  # the canary predictor itself failed (start error, crash loop, never ready)
+            msg = f"Canary predictor unhealthy ({why}), stopping promotion."
+        else:  # the reference's message (mlflow_operator.py:343-344)
+            msg = f"Metrics did not meet conditions after {pol.max_attempts} attempts, stopping promotion."
+        logger.warning("[%s/%s] %s", ns, name, msg)
+        await self.op.event(body, "Warning", EV_PROMOTION_FAILED, msg[:1000])
         if not pol.rollback:  # reference behaviour: leave the split as it is
             await self._patch_status(ns, name, {"phase": PH_FAILED, "canaryLastGate": why[:500]})
             return

@@ -122,6 +122,20 @@ def predictor_ready(sd: dict | None, predictor: str) -> bool:
     return st.get("state") == "Available" and names == [predictor]
 
 
+def predictor_health(sd: dict | None, predictor: str) -> tuple[int, bool, str]:
+    """(restarts, failed, reason) the Seldon controller reports for a predictor's
+    deployments (pods that died and were restarted, or that could not start, e.g. a
+    GPU out-of-memory at weight load)."""
+    ds = ((sd or {}).get("status") or {}).get("deploymentStatus") or {}
+    restarts, failed, reason = 0, False, ""
+    for k, v in ds.items():
+        if f"-{predictor}-" in k or k.endswith(f"-{predictor}"):
+            restarts = max(restarts, int(v.get("restarts", 0)))
+            failed = failed or bool(v.get("failed", False))
+            reason = v.get("reason") or reason
+    return restarts, failed, reason
+
+
 def traffic_of(sd: dict | None) -> dict:
     return {p["name"]: p.get("traffic", 0) for p in ((sd or {}).get("spec") or {}).get("predictors", [])}
 

@@ -14,7 +14,9 @@ code, which is what the operator's canary gate queries.
 ``python -m mlopamd.runtime.server --runtime mlop-llm --architecture llama3-8b``
 starts it; configuration also comes from the env the SeldonDeployment sets
 (MLOP_RUNTIME, MLOP_MODEL_URI, MLOP_ARCHITECTURE, MLOP_ENGINE_*).
-Fault injection for canary tests: MLOP_INJECT_LATENCY_S, MLOP_INJECT_ERROR_RATE.
+Fault injection for canary tests: MLOP_INJECT_LATENCY_S, MLOP_INJECT_ERROR_RATE,
+MLOP_INJECT_START_ERROR (fail at start-up, e.g. a GPU OOM message), MLOP_INJECT_CRASH_AFTER_S
+(exit with status 139 after serving that long).
 """
 from __future__ import annotations
 
@@ -247,8 +249,15 @@ def main(argv=None):
         from .tp_worker import serve_tp
 
         return serve_tp(a, metrics)
+    if os.environ.get("MLOP_INJECT_START_ERROR"):  # fault injection: e.g. a GPU OOM at weight load
+        raise RuntimeError(os.environ["MLOP_INJECT_START_ERROR"])
     backend = build_backend(a.runtime, a.model_uri, a.architecture, a.name, metrics, a.device,
                             engine_kwargs_from_env(), tp_state=tp_state)
+    crash_after = float(os.environ.get("MLOP_INJECT_CRASH_AFTER_S", 0) or 0)
+    if crash_after > 0:  # fault injection: the process dies (SIGSEGV-like exit) after serving a while
+        import threading
+
+        threading.Timer(crash_after, lambda: os._exit(139)).start()
     web.run_app(make_app(backend, metrics, version=a.version), host=a.host, port=a.port, print=None)
 
 

@@ -382,3 +382,75 @@ def test_invalid_spec_reports_error():
         assert st["phase"] == "Invalid" and "modelName" in st["error"]
         await env.stop()
     run(go())
+
+
+# ------------------------------------------------- failure detection / recovery --
+
+def test_canary_oom_at_start_rolls_back_fast():
+    """The new version's predictor dies while loading (GPU out of memory): the Seldon
+    controller reports it Failed and the canary is rolled back at once, not after the
+    30-minute readiness timeout; the old version keeps 100 % of the traffic."""
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05},
+                            "2": {"fail_start": "HIP out of memory: tried to allocate 96.00 GiB"}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        t0 = env.clock.now()
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "RolledBack"), 600)
+        assert env.clock.now() - t0 < 300  # well inside readyTimeoutSeconds (1800)
+        st = await env.status()
+        assert st["currentModelVersion"] == "1" and st["rolledBackVersion"] == "2"
+        assert "out of memory" in st["error"] and any(
+            "out of memory" in e.get("message", "") for e in env.kube.events)
+        assert seldon.traffic_of(await env.sd()) == {"v1": 100}
+        await env.stop()
+    run(go())
+
+
+def test_crashed_predictor_is_restarted_and_recovers():
+    """The serving predictor segfaults once after 100 s: the controller's liveness probe
+    marks it unavailable (CR ready=False, PredictorUnavailable, restart counted) and
+    restarts it after the CrashLoopBackOff delay; the CR is ready again."""
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05, "crash_after_s": 100, "crashes": 1}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        assert await env.run_until(lambda: _not_ready(env), 400)
+        st = await env.status()
+        assert st["predictorRestarts"] == 1
+        assert "PredictorUnavailable" in env.reasons()
+        assert await env.run_until(lambda: _ready(env), 400)
+        assert env.reasons().count("PredictorReady") == 2
+        restarts, failed, reason = seldon.predictor_health(await env.sd(), "v1")
+        assert restarts == 1 and not failed and "139" in reason
+        await env.stop()
+    run(go())
+
+
+def test_crash_looping_canary_rolls_back():
+    """A new version that crashes 30 s after every start is restarted with backoff and
+    rolled back as soon as it reaches maxRestarts (2 here), whatever its gate said."""
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"latency": 0.05, "crash_after_s": 30}})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr(canary={"maxRestarts": 2})
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "RolledBack"), 2000)
+        st = await env.status()
+        assert st["currentModelVersion"] == "1" and "restarted 2 times" in st["error"]
+        fail = [e for e in env.kube.events if e["reason"] == "PromotionFailed"]
+        assert fail and "unhealthy" in fail[-1]["message"]
+        assert seldon.traffic_of(await env.sd()) == {"v1": 100}
+        await env.stop()
+    run(go())
+
+
+async def _not_ready(env):
+    return (await env.status()).get("ready") == "False"

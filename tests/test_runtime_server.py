@@ -139,3 +139,77 @@ def test_config1_demo_end_to_end():
     assert out["final_predictors"] == {"v2": 100}
     assert out["events"][:2] == ["NewModelVersionDetected", "PredictorReady"]
     assert "PromotionComplete" in out["events"]
+
+
+def _sd(name, model_uri, env):
+    return {"apiVersion": "machinelearning.seldon.io/v1", "kind": "SeldonDeployment",
+            "metadata": {"name": name},
+            "spec": {"predictors": [{"name": "v1", "traffic": 100, "replicas": 1,
+                                     "graph": {"name": "classifier-1", "implementation": "MLFLOW_SERVER",
+                                               "modelUri": model_uri},
+                                     "componentSpecs": [{"spec": {"containers": [
+                                         {"name": "classifier-1",
+                                          "env": [{"name": k, "value": v} for k, v in env.items()]}]}}]}]}}
+
+
+def test_process_predictor_crash_is_detected_and_restarted(tmp_path):
+    """A real runtime process (V2 server, CPU sklearn-style model) exits with 139 after 1 s:
+    the fake Seldon controller's liveness probe reports it (SD status restarts / reason) and
+    restarts it as a new process, like the kubelet would."""
+    from mlopamd.controller import seldon
+    from mlopamd.controller.kube import FakeKube
+    from mlopamd.controller.local import FakeSeldonController, ProcessLauncher
+
+    p = save_linear_model(tmp_path / "m", [[1.0, -1.0]], [0.0], [0, 1])
+
+    async def go():
+        kube = FakeKube()
+        launcher = ProcessLauncher(ready_timeout_s=60)
+        ctl = FakeSeldonController(kube, launcher)
+        ctl.PROBE_PERIOD_S, ctl.BACKOFF_S = 0.3, 0.3
+        ctl.start()
+        await kube.create("machinelearning.seldon.io", "v1", "ns", "seldondeployments",
+                          _sd("m", f"file://{p}", {"MLOP_RUNTIME": "mlop-sklearn",
+                                                   "MLOP_INJECT_CRASH_AFTER_S": "1.0"}))
+        key = ("ns", "m", "v1")
+        pids = set()
+        for _ in range(300):
+            pod = ctl.pods.get(key)
+            if pod is not None and pod.proc is not None and pod.ready:
+                pids.add(pod.proc.pid)
+            if pod is not None and pod.restarts >= 2 and len(pids) >= 2:
+                break
+            await asyncio.sleep(0.1)
+        sd = await kube.get("machinelearning.seldon.io", "v1", "ns", "seldondeployments", "m")
+        restarts, failed, reason = seldon.predictor_health(sd, "v1")
+        await ctl.stop()
+        assert len(pids) >= 2, pids
+        assert restarts >= 1 and not failed and "139" in reason
+
+    asyncio.run(asyncio.wait_for(go(), 90))
+
+
+def test_process_predictor_start_failure_reports_failed(tmp_path):
+    from mlopamd.controller import seldon
+    from mlopamd.controller.kube import FakeKube
+    from mlopamd.controller.local import FakeSeldonController, ProcessLauncher
+
+    p = save_linear_model(tmp_path / "m", [[1.0, -1.0]], [0.0], [0, 1])
+
+    async def go():
+        kube = FakeKube()
+        ctl = FakeSeldonController(kube, ProcessLauncher(ready_timeout_s=60)).start()
+        await kube.create("machinelearning.seldon.io", "v1", "ns", "seldondeployments",
+                          _sd("m", f"file://{p}", {"MLOP_RUNTIME": "mlop-sklearn",
+                                                   "MLOP_INJECT_START_ERROR": "HIP out of memory"}))
+        for _ in range(300):
+            sd = await kube.get("machinelearning.seldon.io", "v1", "ns", "seldondeployments", "m")
+            if (sd.get("status") or {}).get("state") == "Failed":
+                break
+            await asyncio.sleep(0.1)
+        await ctl.stop()
+        assert sd["status"]["state"] == "Failed"
+        _, failed, reason = seldon.predictor_health(sd, "v1")
+        assert failed and "exited" in reason and "HIP out of memory" in reason
+
+    asyncio.run(asyncio.wait_for(go(), 90))
