@@ -409,14 +409,16 @@ def load_gemm_table(path: str | os.PathLike | None = None) -> int:
 
 
 def save_gemm_table(path: str | os.PathLike | None = None) -> str:
-    """Write the choices measured so far (merged with an existing table)."""
+    """Write the choices measured so far, merged over the shipped table and over an
+    existing file at ``path`` (so a table saved elsewhere is a complete drop-in)."""
     import json
 
     p = Path(path) if path else GEMM_TABLE
     entries = {}
-    if p.exists():
-        for e in json.loads(p.read_text()).get("entries", []):
-            entries[tuple(e[:4])] = e[4]
+    for src in dict.fromkeys([GEMM_TABLE, p]):
+        if src.exists():
+            for e in json.loads(src.read_text()).get("entries", []):
+                entries[tuple(e[:4])] = e[4]
     for k, c in _GEMM_CHOICE.items():
         if k in _GEMM_TIMES:  # only shapes actually timed in this process
             entries[k] = c
