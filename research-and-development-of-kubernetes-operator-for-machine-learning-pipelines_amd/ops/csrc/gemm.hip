@@ -855,6 +855,10 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
                          int M, int N, int K, int max_rows, int epi, hipStream_t st) {
   if (M == 0) return;
+  if (gemv_grouped_takes(M, N, K, epi)) {  // MoE decode: stream only the routed experts' weights
+    launch_gemv_grouped(A, B, C, offsets, n_groups, M, N, K, epi, st);
+    return;
+  }
   const Plan p = plan(M, N, K, true, n_groups, max_rows);
   if (epi == EPI_NONE)
     launch_plan<EPI_NONE, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N,

@@ -62,17 +62,44 @@ __device__ __forceinline__ float dot8(const u32x4& w, const u32x4& x, float c) {
   return dot2(w.w, x.w, c);
 }
 
-template <int M, int RP, int EPI, int KW, int U, bool NORM>
+// grouped mode (MoE decode, K13 at <= 8 routed rows): rows of A sorted by expert, offsets[E+1]
+struct GroupArgs {
+  const int* offsets;
+  int n_groups;
+};
+
+template <int M, int RP, int EPI, int KW, int U, bool NORM, bool GROUPED = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ B, int ldb,
                                                    uint16_t* __restrict__ C, int ldc, int N, int K,
-                                                   RopeEpi re, NormPro np) {
+                                                   RopeEpi re, NormPro np, GroupArgs ga = GroupArgs{}) {
   constexpr int R = 2 * RP;  // weight rows per wave
   static_assert(EPI != EPI_ROPE || RP == 1, "rope sets are single row pairs");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // row set: KW == 1 -> one per wave; KW == 4 -> one per workgroup (its waves split K)
-  const int set = KW == 1 ? blockIdx.x * 4 + wv : blockIdx.x;
-  if (set >= N / R) return;  // every epilogue has N / R sets
+  int set = KW == 1 ? blockIdx.x * 4 + wv : blockIdx.x;
+  int mc = M;  // rows of A present (grouped: this expert's routed rows)
+  if constexpr (GROUPED) {
+    // slot = set / (N / R) is the slot-th expert that received rows (the grid covers
+    // min(E, M) slots, so experts nobody routed to cost neither a block nor a weight byte)
+    const int spg = N / R, slot = set / spg;
+    set -= slot * spg;
+    int e = -1, seen = 0;
+    for (int g = 0; g < ga.n_groups; ++g) {
+      if (ga.offsets[g + 1] > ga.offsets[g]) {
+        if (seen == slot) { e = g; break; }
+        ++seen;
+      }
+    }
+    if (e < 0) return;
+    const int m0 = ga.offsets[e];
+    mc = min(M, ga.offsets[e + 1] - m0);
+    A += (size_t)m0 * lda;
+    C += (size_t)m0 * ldc;
+    B += (size_t)e * N * ldb;
+  } else if (set >= N / R) {
+    return;  // every epilogue has N / R sets
+  }
   int rows[R];
   if constexpr (EPI == EPI_SILU_MUL) {
     const int col = set * RP, g = col >> 4, i0 = col & 15;  // RP outputs inside one 16-group
@@ -144,7 +171,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < M; ++m) x[u][m] = ok ? Av[m][c] : u32x4{0, 0, 0, 0};
+        for (int m = 0; m < M; ++m) x[u][m] = (ok && m < mc) ? Av[m][c] : u32x4{0, 0, 0, 0};
       }
     }
 #pragma unroll
@@ -152,7 +179,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int m = 0; m < M; ++m) acc[r][m] = dot8(w[u][r], x[u][m], acc[r][m]);
+        for (int m = 0; m < M; ++m)
+          if (!GROUPED || m < mc) acc[r][m] = dot8(w[u][r], x[u][m], acc[r][m]);  // mc: wave-uniform
   }
 
 #pragma unroll
@@ -203,7 +231,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int p = 0; p < RP; ++p)
-        if (lane == m * RP + p)
+        if (lane == m * RP + p && m < mc)
           C[(size_t)m * ldc + set * RP + p] = f2bf(silu_bf(acc[p][m]) * bf2f(f2bf(acc[RP + p][m])));
   } else if constexpr (EPI == EPI_ROPE) {
     const int rope_sets = (re.Hq + re.Hkv) * (kHeadD / 2);
@@ -240,7 +268,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int r = 0; r < R; ++r)
-        if (lane == m * R + r) C[(size_t)m * ldc + set * R + r] = f2bf(acc[r][m]);
+        if (lane == m * R + r && m < mc) C[(size_t)m * ldc + set * R + r] = f2bf(acc[r][m]);
   }
 }
 
@@ -332,6 +360,55 @@ void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ld
 void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st) {
   run_gemv<EPI_ROPE>((const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, M, N, K, re, st);
+}
+
+template <int M, int EPI>
+void run_gemv_grouped_m(const uint16_t* A, const uint16_t* B, uint16_t* C, int ldc, int N, int K,
+                        const int* offsets, int n_groups, hipStream_t st) {
+  constexpr int U = M <= 2 ? 4 : 2;
+  const int pairs = N / 2;
+  const int rp = pairs / 2 >= 2048 ? 2 : 1;
+  const int spg = pairs / rp, slots = std::min(n_groups, M);
+  const bool kw4 = spg * slots < 2048;
+  const GroupArgs ga{offsets, n_groups};
+#define MLOP_GEMV_G(RP, KW)                                                                        \
+  do {                                                                                             \
+    const int sets = spg * slots;                                                                  \
+    const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
+    gemv_kernel<M, RP, EPI, KW, U, false, true><<<blocks, 256, 0, st>>>(A, K, B, K, C, ldc, N, K,  \
+                                                                          RopeEpi{}, NormPro{}, ga); \
+  } while (0)
+  if (rp == 2) {
+    if (kw4) MLOP_GEMV_G(2, 4); else MLOP_GEMV_G(2, 1);
+  } else {
+    if (kw4) MLOP_GEMV_G(1, 4); else MLOP_GEMV_G(1, 1);
+  }
+#undef MLOP_GEMV_G
+}
+
+// MoE expert GEMMs at decode: M = routed rows in total (<= MLOP_GEMV_GROUPED_MAX_M, default 8)
+bool gemv_grouped_takes(int M, int N, int K, int epi) {
+  static const int max_m = std::min(8, env_int("MLOP_GEMV_GROUPED_MAX_M", 8));
+  return M >= 1 && M <= max_m && K % 8 == 0 && N % (epi == EPI_SILU_MUL ? 32 : 4) == 0 &&
+         (epi == EPI_NONE || epi == EPI_SILU_MUL);
+}
+
+void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,
+                         int K, int epi, hipStream_t st) {
+  auto* a = (const uint16_t*)A;
+  auto* b = (const uint16_t*)B;
+  auto* c = (uint16_t*)C;
+  const int ldc = epi == EPI_SILU_MUL ? N / 2 : N;
+#define MLOP_GG(MM)                                                                       \
+  case MM:                                                                                \
+    if (epi == EPI_SILU_MUL) run_gemv_grouped_m<MM, EPI_SILU_MUL>(a, b, c, ldc, N, K, offsets, n_groups, st); \
+    else run_gemv_grouped_m<MM, EPI_NONE>(a, b, c, ldc, N, K, offsets, n_groups, st);          \
+    break;
+  switch (M) {
+    MLOP_GG(1) MLOP_GG(2) MLOP_GG(3) MLOP_GG(4) MLOP_GG(5) MLOP_GG(6) MLOP_GG(7) MLOP_GG(8)
+    default: break;
+  }
+#undef MLOP_GG
 }
 
 // residual add + RMSNorm fused into the projection that consumes it (prologue NORM):

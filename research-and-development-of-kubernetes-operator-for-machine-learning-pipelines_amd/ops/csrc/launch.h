@@ -57,6 +57,9 @@ struct NormPro {
   float eps;
 };
 bool gemv_norm_takes(int M, int N, int K, int epi);
+bool gemv_grouped_takes(int M, int N, int K, int epi);
+void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,
+                         int K, int epi, hipStream_t st);
 void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M, int N, int K, int epi,
                       const RopeEpi& re, hipStream_t st);
 bool gemm_rope_supported(int M, int N, int K);

@@ -388,8 +388,31 @@ def test_grouped_gemm_large_groups(gpu, rows, epi):
         close(y[a:b], r)
 
 
-@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (77, 8, 2, 1024, 512), (512, 8, 2, 512, 256),
-                                       (300, 4, 1, 256, 256)])
+@pytest.mark.parametrize("counts", [[1, 0, 0, 0, 0, 0, 1, 0], [0, 3, 0, 2, 0, 0, 0, 3], [0, 0, 0, 0, 0, 0, 0, 1],
+                                    [1, 1, 1, 1, 1, 1, 1, 1]])
+@pytest.mark.parametrize("epi,N,K", [(1, 28672, 4096), (0, 4096, 14336), (1, 1024, 512), (0, 1024, 2048)])
+def test_grouped_gemv_decode(gpu, counts, epi, N, K):
+    """MoE decode (<= 8 routed rows): the grouped GEMV streams only the experts that got
+    rows (grid = min(E, rows) expert slots), empty experts in between; vs fp32 per expert."""
+    torch.manual_seed(sum(counts) * N)
+    E = len(counts)
+    off = torch.tensor([0] + list(np.cumsum(counts)), device=gpu, dtype=torch.int32)
+    M = int(off[-1])
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.03 * torch.randn(E, N, K, device=gpu)).to(bf)
+    y = ops.grouped_gemm(x, w, off, epi=epi)
+    for e in range(E):
+        a, b = int(off[e]), int(off[e + 1])
+        if a == b:
+            continue
+        r = (x[a:b].float() @ w[e].float().t()).to(bf)
+        if epi:
+            r = ref.silu_mul(ops.deinterleave_cols(r))
+        close(y[a:b], r, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (3, 8, 2, 4096, 14336), (77, 8, 2, 1024, 512),
+                                       (512, 8, 2, 512, 256), (300, 4, 1, 256, 256)])
 def test_moe_pipeline(gpu, T, E, k, H, I):
     torch.manual_seed(T)
     x = torch.randn(T, H, device=gpu, dtype=bf)
@@ -423,7 +446,8 @@ def test_moe_pipeline(gpu, T, E, k, H, I):
                 gu = (x[t].float() @ ops.deinterleave_rows(w13[e]).float().t()).to(bf)
                 h = ref.silu_mul(gu[None])[0].float() @ w2[e].float().t()
                 exp[t] += w[t, j] * h.to(bf).float()
-        close(out, exp, atol=3e-2, rtol=3e-2)
+        # bf16 rounding noise scales with the output magnitude (large I: |out| ~ 20)
+        close(out, exp, atol=3e-2 + 3e-3 * float(exp.abs().max()), rtol=3e-2)
         assert n == int(((idx >= e0) & (idx < e0 + nl)).sum())
 
 
