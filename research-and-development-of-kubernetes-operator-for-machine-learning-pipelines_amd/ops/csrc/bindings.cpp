@@ -396,10 +396,13 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
   check_i32(top_ks, "top_ks");
   TORCH_CHECK(top_ks.numel() == n, "top_ks");
   c10::DeviceGuard g(logits.device());
+  const long wsb = mlop::sample_workspace_bytes((int)n, (int)logits.size(1));
+  at::Tensor ws;  // candidate buffers from the caching allocator (graph-capture safe)
+  if (wsb > 0) ws = at::empty({wsb}, logits.options().dtype(at::kByte));
   mlop::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)n,
                       (int)logits.size(1), logits.stride(0), temps.data_ptr<float>(),
                       top_ks.data_ptr<int>(), top_ps.data_ptr<float>(), uniform.data_ptr<float>(),
-                      cur_stream());
+                      wsb > 0 ? ws.data_ptr() : nullptr, cur_stream());
 }
 
 

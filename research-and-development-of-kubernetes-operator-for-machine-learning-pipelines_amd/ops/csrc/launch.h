@@ -82,8 +82,11 @@ void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStr
 // bf16 greedy argmax; ws (>= argmax_splits(n, V) * n int64, or null) splits small batches' rows
 int argmax_splits(int n, int V);
 void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, void* ws, hipStream_t st);
+// temperature / top-k / top-p draw; small batches pre-select per-slice top-K candidates into ws
+// (sample_workspace_bytes(n, V) bytes, 0 = not needed)
+long sample_workspace_bytes(int n, int V);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
-                   const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st);
+                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, hipStream_t st);
 
 // K15 custom one-shot all-reduce (allreduce.hip); handles are opaque state pointers
 long car_create(int rank, int world, long max_bytes, int device);

@@ -170,10 +170,13 @@ __global__ void __launch_bounds__(64) argmax_keys_kernel(long* __restrict__ out,
   }
 }
 
+// idx_map (optional): the row holds pre-selected candidates (sample_presel_kernel) and
+// idx_map[row * ld + j] is candidate j's vocabulary index (-inf padding maps to 0x7fffffff)
 __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
     long* __restrict__ out, const float* __restrict__ logits, int V, long ld,
     const float* __restrict__ temps, const int* __restrict__ top_ks,
-    const float* __restrict__ top_ps, const float* __restrict__ uniform) {
+    const float* __restrict__ top_ps, const float* __restrict__ uniform,
+    const int* __restrict__ idx_map = nullptr) {
   __shared__ uint32_t hist[256];
   __shared__ float cv[kMaxCand];
   __shared__ int ci[kMaxCand];
@@ -189,6 +192,7 @@ __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
     float bv;
     int bi;
     block_argmax(row, V, sv, si, bv, bi);
+    if (idx_map && bi != 0x7fffffff) bi = idx_map[row_id * ld + bi];
     if (threadIdx.x == 0) out[row_id] = bi == 0x7fffffff ? 0 : bi;
     return;
   }
@@ -230,10 +234,10 @@ __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
     const uint32_t k = fkey(x);
     if (k > prefix) {
       const uint32_t p = atomicAdd(&s_cnt_gt, 1u);
-      if (p < n_gt) { cv[p] = x; ci[p] = j; }
+      if (p < n_gt) { cv[p] = x; ci[p] = idx_map ? idx_map[row_id * ld + j] : j; }
     } else if (k == prefix) {
       const uint32_t p = atomicAdd(&s_cnt_eq, 1u);
-      if (p < remaining) { cv[n_gt + p] = x; ci[n_gt + p] = j; }
+      if (p < remaining) { cv[n_gt + p] = x; ci[n_gt + p] = idx_map ? idx_map[row_id * ld + j] : j; }
     }
   }
   __syncthreads();
@@ -298,6 +302,83 @@ __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
   }
 }
 
+// Small batches: one workgroup per row makes sample_kernel a ~0.5 ms single-CU job over a
+// 128k vocabulary (5 dependent passes over 512 KB).  Stage 1 splits each row over S
+// workgroups: a workgroup stages its slice (<= kPreselSlice floats) in LDS once, radix-
+// selects the slice's own top-K (K = the row's top_k, capped at kMaxCand) and writes them as
+// kMaxCand (value, vocab index) candidates (-inf padding).  The row's global top-K is inside
+// the union of the slices' top-K, so stage 2 (sample_kernel over the S * kMaxCand candidates,
+// idx_map = their indices) draws from the same distribution with the same uniform.
+constexpr int kPreselSlice = 8192;
+
+__global__ void __launch_bounds__(kSampleThreads) sample_presel_kernel(
+    float* __restrict__ cand_v, int* __restrict__ cand_i, const float* __restrict__ logits, int V, long ld,
+    const float* __restrict__ temps, const int* __restrict__ top_ks, int per) {
+  __shared__ float sl[kPreselSlice];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_prefix, s_remaining, s_cnt_gt, s_cnt_eq;
+  const int s = blockIdx.x, row_id = blockIdx.y, S = gridDim.x;
+  const int j0 = s * per, len = max(0, min(per, V - j0));
+  const size_t base = ((size_t)row_id * S + s) * kMaxCand;
+  const float* row = logits + row_id * ld + j0;
+  for (int j = threadIdx.x; j < len; j += blockDim.x) sl[j] = row[j];
+  int K = top_ks[row_id];
+  if (K <= 0 || K > kMaxCand) K = kMaxCand;
+  if (temps[row_id] <= 0.f) K = 1;  // greedy row: its slice max is all stage 2 needs
+  if (K > len) K = len;
+  __syncthreads();
+  uint32_t prefix = 0, mask = 0, remaining = (uint32_t)K;
+  for (int shift = 24; shift >= 0 && K > 0; shift -= 8) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < len; j += blockDim.x) {
+      const uint32_t k = fkey(sl[j]);
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 0xff], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t above = 0;
+      int d = 255;
+      for (; d > 0; --d) {
+        if (above + hist[d] >= remaining) break;
+        above += hist[d];
+      }
+      s_prefix = prefix | ((uint32_t)d << shift);
+      s_remaining = remaining - above;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    remaining = s_remaining;
+    mask |= 0xffu << shift;
+  }
+  if (threadIdx.x == 0) { s_cnt_gt = 0; s_cnt_eq = 0; }
+  __syncthreads();
+  const uint32_t n_gt = K > 0 ? (uint32_t)K - remaining : 0;
+  for (int j = threadIdx.x; j < len && K > 0; j += blockDim.x) {
+    const float x = sl[j];
+    const uint32_t k = fkey(x);
+    if (k > prefix) {
+      const uint32_t p = atomicAdd(&s_cnt_gt, 1u);
+      if (p < n_gt) { cand_v[base + p] = x; cand_i[base + p] = j0 + j; }
+    } else if (k == prefix) {
+      const uint32_t p = atomicAdd(&s_cnt_eq, 1u);
+      if (p < remaining) { cand_v[base + n_gt + p] = x; cand_i[base + n_gt + p] = j0 + j; }
+    }
+  }
+  for (int j = max(K, 0) + threadIdx.x; j < kMaxCand; j += blockDim.x) {
+    cand_v[base + j] = -INFINITY;
+    cand_i[base + j] = 0x7fffffff;
+  }
+}
+
+// workgroups per row of the pre-selection (1 = sample_kernel alone over the full row)
+int sample_splits(int n, int V) {
+  if (n <= 0 || n >= 64) return 1;
+  const int need = (V + kPreselSlice - 1) / kPreselSlice;  // slices must fit LDS
+  const int S = std::max(need, std::min(16, (256 + n - 1) / n));
+  return S <= 1 ? 1 : S;
+}
+
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st) {
   if (n == 0) return;
   argmax_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld);
@@ -323,9 +404,24 @@ void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, vo
 }
 
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
-                   const int* top_ks, const float* top_ps, const float* uniform, hipStream_t st) {
+                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, hipStream_t st) {
   if (n == 0) return;
-  sample_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld, temps, top_ks, top_ps, uniform);
+  const int S = ws ? sample_splits(n, V) : 1;
+  if (S <= 1) {
+    sample_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld, temps, top_ks, top_ps, uniform);
+    return;
+  }
+  const int per = (V + S - 1) / S;
+  const long C = (long)S * kMaxCand;  // candidates per row
+  auto* cv = (float*)ws;
+  auto* ci = (int*)((char*)ws + (size_t)n * C * sizeof(float));
+  sample_presel_kernel<<<dim3(S, n), kSampleThreads, 0, st>>>(cv, ci, logits, V, ld, temps, top_ks, per);
+  sample_kernel<<<n, kSampleThreads, 0, st>>>(out, cv, (int)C, C, temps, top_ks, top_ps, uniform, ci);
+}
+
+long sample_workspace_bytes(int n, int V) {
+  const int S = sample_splits(n, V);
+  return S <= 1 ? 0 : (long)n * S * kMaxCand * (sizeof(float) + sizeof(int));
 }
 
 }  // namespace mlop

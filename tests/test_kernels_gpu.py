@@ -228,13 +228,15 @@ def test_argmax(gpu, n, V, dtype):
     assert torch.equal(ops.argmax(x).cpu(), x.float().argmax(-1).cpu())
 
 
-def test_sample_matches_reference(gpu):
+@pytest.mark.parametrize("n,V", [(16, 32000), (4, 128256), (64, 32000), (8, 1000)])
+def test_sample_matches_reference(gpu, n, V):
+    """n < 64: per-slice top-K pre-selection (16 workgroups per row) + the draw over the
+    candidates; n = 64: the single-stage kernel; same uniforms as the torch reference."""
     torch.manual_seed(1)
-    n, V = 16, 32000
     x = 3 * torch.randn(n, V, device=gpu)
-    temps = torch.tensor([0.0, 0.7, 1.0, 1.3] * 4, device=gpu)
-    ks = torch.tensor([0, 1, 50, 0] * 4, dtype=torch.int32, device=gpu)
-    ps = torch.tensor([1.0, 1.0, 0.9, 0.5] * 4, device=gpu)
+    temps = torch.tensor([0.0, 0.7, 1.0, 1.3] * (n // 4), device=gpu)
+    ks = torch.tensor([0, 1, 50, 0] * (n // 4), dtype=torch.int32, device=gpu)
+    ps = torch.tensor([1.0, 1.0, 0.9, 0.5] * (n // 4), device=gpu)
     u = torch.rand(n, device=gpu)
     got = ops.sample(x, temps, ks, ps, u).cpu()
     exp = ref_sample = None
