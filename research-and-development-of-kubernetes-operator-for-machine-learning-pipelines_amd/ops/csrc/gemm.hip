@@ -731,7 +731,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.splits = 1;
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
-  static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 320);
+  static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 256);  // run49: down -5..-15% at M 8-64
   if (!grouped && tiles < 160 && K >= 1024) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
