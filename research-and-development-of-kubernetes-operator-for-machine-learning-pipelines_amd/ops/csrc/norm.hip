@@ -71,9 +71,81 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ ou
   }
 }
 
+// Wave-per-row form for the many-row passes (H = 512 * VPL): each lane issues all
+// of its row's 16-B loads up front and the sum of squares is one wave reduction,
+// so there is no LDS and no barrier, and a CU keeps several rows per SIMD in
+// flight instead of one 8-wave row per quarter CU (the block form above waits on
+// one 32 KB row's round trip per workgroup).
+template <int VPL, bool ADD>
+__global__ void __launch_bounds__(256) rmsnorm_wave_kernel(uint16_t* __restrict__ out,
+                                                           uint16_t* __restrict__ residual,
+                                                           const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ w,
+                                                           float eps, int M, int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;  // whole wave; no barrier below
+  const size_t base = (size_t)row * H;
+  u32x4 a[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) a[i] = *reinterpret_cast<const u32x4*>(x + base + (lane + i * 64) * 8);
+  if constexpr (ADD) {
+    u32x4 r[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+      r[i] = *reinterpret_cast<const u32x4*>(residual + base + (lane + i * 64) * 8);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // bf16-rounded sum, as the residual stream stores it
+        a[i][j] = pack2(lo_bf(a[i][j]) + lo_bf(r[i][j]), hi_bf(a[i][j]) + hi_bf(r[i][j]));
+      *reinterpret_cast<u32x4*>(residual + base + (lane + i * 64) * 8) = a[i];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = lo_bf(a[i][j]), hi = hi_bf(a[i][j]);
+      ss += lo * lo + hi * hi;
+    }
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const u32x4 wv = *reinterpret_cast<const u32x4*>(w + (lane + i * 64) * 8);
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // HF LlamaRMSNorm: weight * bf16(x * inv)
+      o[j] = pack2(bf2f(f2bf(lo_bf(a[i][j]) * inv)) * lo_bf(wv[j]),
+                   bf2f(f2bf(hi_bf(a[i][j]) * inv)) * hi_bf(wv[j]));
+    *reinterpret_cast<u32x4*>(out + base + (lane + i * 64) * 8) = o;
+  }
+}
+
+constexpr int kWaveRowsMinM = 256;  // fewer rows: the block form's 8-wave fan-out per row wins
+
+template <bool ADD>
+static bool dispatch_wave(uint16_t* out, uint16_t* residual, const uint16_t* x, const uint16_t* w,
+                          float eps, int M, int H, hipStream_t st) {
+  static const bool on = !getenv("MLOP_NORM_WAVE") || atoi(getenv("MLOP_NORM_WAVE")) != 0;
+  if (!on || M < kWaveRowsMinM || H % 512) return false;
+  const int g = cdiv(M, 4);
+  switch (H / 512) {
+    case 1: rmsnorm_wave_kernel<1, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
+    case 2: rmsnorm_wave_kernel<2, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
+    case 4: rmsnorm_wave_kernel<4, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
+    case 8: rmsnorm_wave_kernel<8, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
+    case 16: rmsnorm_wave_kernel<16, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
+    default: return false;
+  }
+}
+
 template <bool ADD>
 static void dispatch(uint16_t* out, uint16_t* residual, const uint16_t* x, const uint16_t* w,
                      float eps, int M, int H, hipStream_t st) {
+  if (dispatch_wave<ADD>(out, residual, x, w, eps, M, H, st)) return;
   const int nvec = H / 8;
   int vpt = 1;
   while (vpt < 8 && nvec / vpt > 512) vpt <<= 1;

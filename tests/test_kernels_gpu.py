@@ -17,14 +17,15 @@ def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
 
-@pytest.mark.parametrize("M,H", [(1, 4096), (7, 4096), (33, 8192), (5, 1024), (3, 5120)])
+@pytest.mark.parametrize("M,H", [(1, 4096), (7, 4096), (33, 8192), (5, 1024), (3, 5120),
+                                 (1027, 4096), (300, 1024), (259, 8192), (400, 5120)])
 def test_rmsnorm(gpu, M, H):
     x = torch.randn(M, H, device=gpu, dtype=bf)
     w = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
     close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x, w, 1e-5))
 
 
-@pytest.mark.parametrize("M,H", [(1, 4096), (19, 4096), (4, 8192)])
+@pytest.mark.parametrize("M,H", [(1, 4096), (19, 4096), (4, 8192), (1030, 4096), (257, 2048), (300, 8192)])
 def test_add_rmsnorm(gpu, M, H):
     x = torch.randn(M, H, device=gpu, dtype=bf)
     r = torch.randn(M, H, device=gpu, dtype=bf)
