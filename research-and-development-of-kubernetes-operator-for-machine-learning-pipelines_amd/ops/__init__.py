@@ -112,6 +112,16 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0,
     return out
 
 
+_NO_SEM: dict = {}
+
+
+def _no_sem(device):
+    t = _NO_SEM.get(device)
+    if t is None:
+        t = _NO_SEM[device] = torch.empty(0, dtype=torch.int32, device=device)
+    return t
+
+
 def paged_attention(q, k_cache, v_cache, meta, out: torch.Tensor | None = None):
     """Ragged paged attention; ``meta`` is a ``mlopamd.runtime.attn_meta.AttnMeta``.
     Decode / short rows run on the 16-q-row tiles (``tile_*``), prompt chunks on
@@ -122,7 +132,10 @@ def paged_attention(q, k_cache, v_cache, meta, out: torch.Tensor | None = None):
     out = torch.empty_like(q) if out is None else out
     scale = 1.0 / math.sqrt(q.shape[-1])
     if meta.tile_seq.numel():
-        torch.ops.mlop.paged_attention(out, meta.part_o, meta.part_ml, q, k_cache, v_cache,
+        sem = getattr(meta, "part_sem", None)
+        if sem is None:
+            sem = _no_sem(q.device)
+        torch.ops.mlop.paged_attention(out, meta.part_o, meta.part_ml, sem, q, k_cache, v_cache,
                                        meta.block_tables, meta.tile_seq, meta.tile_q0, meta.q_start,
                                        meta.q_len, meta.ctx_len, scale, meta.part_tokens, meta.nparts)
     pts = getattr(meta, "ptile_seq", None)

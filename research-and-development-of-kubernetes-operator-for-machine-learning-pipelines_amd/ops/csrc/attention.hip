@@ -44,11 +44,12 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const int* __restrict__ tile_seq, const int* __restrict__ tile_q0,
     const int* __restrict__ q_start, const int* __restrict__ q_len,
     const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int part_tokens,
-    int nparts, int num_blocks) {
+    int nparts, int num_blocks, int* __restrict__ sem) {
   constexpr int QT = 16 / G;
   __shared__ float sm_o[4][16][kD + 4];
   __shared__ float sm_m[4][16];
   __shared__ float sm_l[4][16];
+  __shared__ int sm_last;
 
   const int tile = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -180,16 +181,19 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     for (int j = 0; j < 8; ++j) acc[j] += f * sm_o[w][rr][c + j];
   }
   const int qi2 = q0 + rr / G;
-  if (qi2 >= ql) return;
+  const bool row_valid = qi2 < ql;
   const int head2 = kvh * G + (rr % G);
   if (nparts == 1) {
+    if (!row_valid) return;
     const float inv = L > 0.f ? 1.f / L : 0.f;
     u32x4 ov;
 #pragma unroll
     for (int j = 0; j < 4; ++j) ov[j] = pack2(acc[2 * j] * inv, acc[2 * j + 1] * inv);
     *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + head2) * kD + c) = ov;
-  } else {
-    const size_t pbase = (((size_t)tile * Hkv + kvh) * nparts + part) * 16 + rr;
+    return;
+  }
+  const size_t pbase = (((size_t)tile * Hkv + kvh) * nparts + part) * 16 + rr;
+  if (row_valid) {
     float4* po = reinterpret_cast<float4*>(part_o + pbase * kD + c);
     po[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     po[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
@@ -198,6 +202,48 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       part_ml[pbase * 2 + 1] = L;
     }
   }
+  if (sem == nullptr) return;  // attn_reduce_kernel combines in a second launch
+  // In-launch combine (cdna_hip_programming.md §5 split-K item 2, counter form of the
+  // §6 Guideline 16 hand-off): publish the slab with ONE agent-scope release, draw a
+  // ticket; the partition that draws nvalid-1 acquires and reduces every slab, then
+  // re-arms the counter for the next launch (the buffer is zero-initialised once).
+  const int nvalid = min(nparts, (kv_end + part_tokens - 1) / part_tokens);
+  int* cnt = sem + (size_t)tile * Hkv + kvh;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm_last = (t == nvalid - 1);
+  }
+  __syncthreads();
+  if (!sm_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!row_valid) return;
+  const size_t base = ((size_t)tile * Hkv + kvh) * nparts;
+  float MM = kNegBig;
+  for (int p = 0; p < nvalid; ++p) MM = fmaxf(MM, part_ml[((base + p) * 16 + rr) * 2]);
+  float LL = 0.f, a2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < nvalid; ++p) {
+    const size_t pb = (base + p) * 16 + rr;
+    const float f = exp2f(part_ml[pb * 2] - MM);
+    LL += f * part_ml[pb * 2 + 1];
+    const float4* po = reinterpret_cast<const float4*>(part_o + pb * kD + c);
+    const float4 x0 = po[0], x1 = po[1];
+    a2[0] += f * x0.x; a2[1] += f * x0.y; a2[2] += f * x0.z; a2[3] += f * x0.w;
+    a2[4] += f * x1.x; a2[5] += f * x1.y; a2[6] += f * x1.z; a2[7] += f * x1.w;
+  }
+  const float inv = LL > 0.f ? 1.f / LL : 0.f;
+  u32x4 ov;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ov[j] = pack2(a2[2 * j] * inv, a2[2 * j + 1] * inv);
+  *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + head2) * kD + c) = ov;
 }
 
 template <int G>
@@ -243,13 +289,13 @@ static void launch_g(void* out, float* part_o, float* part_ml, const void* q, co
                      const void* vc, const int* bt, int bt_stride, const int* tile_seq,
                      const int* tile_q0, const int* q_start, const int* q_len, const int* ctx_len,
                      int num_tiles, int Hq, int Hkv, float scale_log2, int part_tokens, int nparts,
-                     int num_blocks, hipStream_t st) {
+                     int num_blocks, int* sem, hipStream_t st) {
   dim3 grid(num_tiles, Hkv, nparts);
   paged_attn_kernel<G><<<grid, 256, 0, st>>>((uint16_t*)out, part_o, part_ml, (const uint16_t*)q,
                                              (const uint16_t*)kc, (const uint16_t*)vc, bt,
                                              bt_stride, tile_seq, tile_q0, q_start, q_len, ctx_len,
-                                             Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks);
-  if (nparts > 1) {
+                                             Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, sem);
+  if (nparts > 1 && sem == nullptr) {
     attn_reduce_kernel<G><<<dim3(num_tiles, Hkv), 256, 0, st>>>(
         (uint16_t*)out, part_o, part_ml, tile_seq, tile_q0, q_start, q_len, ctx_len, Hq, Hkv,
         part_tokens, nparts);
@@ -261,13 +307,13 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
                             const int* tile_seq, const int* tile_q0, const int* q_start,
                             const int* q_len, const int* ctx_len, int num_tiles, int Hq, int Hkv,
                             float scale_log2, int part_tokens, int nparts, int num_blocks,
-                            hipStream_t st) {
+                            int* sem, hipStream_t st) {
   if (num_tiles == 0) return;
   const int G = Hq / Hkv;
 #define MLOP_ATTN_CASE(GG)                                                                        \
   case GG:                                                                                        \
     launch_g<GG>(out, part_o, part_ml, q, kc, vc, bt, bt_stride, tile_seq, tile_q0, q_start,     \
-                 q_len, ctx_len, num_tiles, Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, st);        \
+                 q_len, ctx_len, num_tiles, Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, sem, st);   \
     break;
   switch (G) {
     MLOP_ATTN_CASE(1)

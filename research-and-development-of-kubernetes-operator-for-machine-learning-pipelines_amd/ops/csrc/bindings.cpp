@@ -126,7 +126,7 @@ void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor 
                              (int)k_cache.size(0), cur_stream());
 }
 
-void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_cache,
+void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem, Tensor q, Tensor k_cache,
                      Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0,
                      Tensor q_start, Tensor q_len, Tensor ctx_len, double scale,
                      int64_t part_tokens, int64_t nparts) {
@@ -158,6 +158,18 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor
                     part_ml.numel() >= (int64_t)num_tiles * Hkv * nparts * 16 * 2,
                 "partial workspace too small");
   }
+  // part_sem: zero-initialised int32 tickets, one per (tile, kv head), re-armed by the
+  // kernel; empty -> the split-KV combine runs as a second launch
+  // Only for launches of few (tile, kv head) pairs: there the saved launch (~4.7 us in a
+  // graph) outweighs every partition's release fence (batch 1: 309.7 -> 316.7-318.6 tok/s;
+  // batch 8, 64 pairs: 1800 -> 1783, scripts/run52.sh)
+  static const int max_pairs = getenv("MLOP_ATTN_FUSED_MAX_PAIRS") ? atoi(getenv("MLOP_ATTN_FUSED_MAX_PAIRS")) : 32;
+  int* sem = nullptr;
+  if (nparts > 1 && part_sem.numel() > 0 && num_tiles * Hkv <= max_pairs) {
+    check_i32(part_sem, "part_sem");
+    TORCH_CHECK(part_sem.numel() >= (int64_t)num_tiles * Hkv, "part_sem too small");
+    sem = part_sem.data_ptr<int>();
+  }
   c10::DeviceGuard g(q.device());
   const float scale_log2 = (float)(scale * 1.4426950408889634);
   mlop::launch_paged_attention(
@@ -166,7 +178,7 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor
       v_cache.data_ptr(), block_tables.data_ptr<int>(), (int)block_tables.stride(0),
       tile_seq.data_ptr<int>(), tile_q0.data_ptr<int>(), q_start.data_ptr<int>(),
       q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), num_tiles, Hq, Hkv, scale_log2,
-      (int)part_tokens, (int)nparts, (int)k_cache.size(0), cur_stream());
+      (int)part_tokens, (int)nparts, (int)k_cache.size(0), sem, cur_stream());
 }
 
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
@@ -470,7 +482,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("embedding(Tensor(a!) out, Tensor table, Tensor ids, int vocab_start) -> ()");
   m.def("flash_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor ptile_seq, Tensor ptile_q0, Tensor q_start, Tensor q_len, Tensor ctx_len, float scale) -> ()");
-  m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor q, "
+  m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor(d!) part_sem, Tensor q, "
         "Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0, "
         "Tensor q_start, Tensor q_len, Tensor ctx_len, float scale, int part_tokens, "
         "int nparts) -> ()");

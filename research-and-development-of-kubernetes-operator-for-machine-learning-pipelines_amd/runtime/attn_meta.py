@@ -41,6 +41,9 @@ class AttnMeta:
     part_ml: torch.Tensor
     logits_idx: torch.Tensor  # int64 [n_logits]
     num_tokens: int
+    # int32 tickets (zero-initialised, re-armed by the kernel): the last partition of a
+    # split-KV (tile, kv head) combines the slabs in the same launch; None -> reduce launch
+    part_sem: torch.Tensor | None = None
 
 
 # 128-token partitions: one 32-token page pair per wave at batch 1 (256: 312 tok/s, 128: 322,
@@ -104,6 +107,8 @@ class MetaBuffers:
         self.wp_capacity = 4096
         self.part_o = torch.empty(self.wp_capacity * 16 * 128, dtype=torch.float32, device=self.device)
         self.part_ml = torch.empty(self.wp_capacity * 16 * 2, dtype=torch.float32, device=self.device)
+        self.part_sem = (torch.zeros(self.wp_capacity, dtype=torch.int32, device=self.device)
+                         if os.environ.get("MLOP_ATTN_FUSED_REDUCE", "1") != "0" else None)
         bt = self.view_h("block_tables").reshape(max_seqs, max_blocks_per_seq)
         self.bt_h = bt  # numpy view [max_seqs, mb]
 
@@ -134,7 +139,7 @@ class MetaBuffers:
             ptile_seq=self.view_d("ptile_seq", num_ptiles), ptile_q0=self.view_d("ptile_q0", num_ptiles),
             q_start=self.view_d("q_start"), q_len=self.view_d("q_len"), ctx_len=self.view_d("ctx_len"),
             part_tokens=part_tokens, nparts=nparts, part_o=self.part_o, part_ml=self.part_ml,
-            logits_idx=self.lidx_d[:n_logits], num_tokens=num_tokens)
+            logits_idx=self.lidx_d[:n_logits], num_tokens=num_tokens, part_sem=self.part_sem)
 
     def fill(self, rows, q_lens, ctx_lens, token_ids_per_seq, want_logits=None):
         """Fill host arrays for a ragged batch.

@@ -178,7 +178,7 @@ def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
-@pytest.mark.parametrize("case", ["decode", "prefill", "mixed", "split"])
+@pytest.mark.parametrize("case", ["decode", "prefill", "mixed", "split", "split_fused"])
 def test_paged_attention(gpu, Hq, Hkv, case):
     torch.manual_seed(0)
     np.random.seed(0)
@@ -195,11 +195,20 @@ def test_paged_attention(gpu, Hq, Hkv, case):
         q_lens, ctx_lens = [1, 1, 3], [1500, 33, 900]
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
-    kw = dict(part_tokens=256, nparts=6) if case == "split" else {}
+    kw = dict(part_tokens=256, nparts=6) if case.startswith("split") else {}
     m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, **kw)
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
-    out = ops.paged_attention(q, kc, vc, m)
     exp = ref.paged_attention(q, kc, vc, m)
+    if case == "split_fused":
+        # in-launch combine by the last-arriving partition; the tickets must come back
+        # re-armed (all zero) after every launch, so repeated launches stay correct
+        m.part_sem = torch.zeros(m.tile_seq.numel() * Hkv, dtype=torch.int32, device=gpu)
+        for _ in range(3):
+            out = ops.paged_attention(q, kc, vc, m)
+            close(out, exp, atol=2e-2, rtol=2e-2)
+            assert int(m.part_sem.abs().sum()) == 0
+        return
+    out = ops.paged_attention(q, kc, vc, m)
     close(out, exp, atol=2e-2, rtol=2e-2)
 
 
