@@ -284,6 +284,13 @@ int gemv_max_m() {
   return max_m;
 }
 
+// below this many row sets a workgroup's 4 waves share rows and split K (KW = 4): more loads
+// in flight per row for the small projections (MLOP_GEMV_KW4_SETS, default 2048)
+int gemv_kw4_sets() {
+  static const int v = env_int("MLOP_GEMV_KW4_SETS", 2048);
+  return v;
+}
+
 template <int M, int EPI, bool NORM>
 void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int N,
                 int K, const RopeEpi& re, const NormPro& np, hipStream_t st) {
@@ -292,7 +299,7 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
   const int pairs = N / 2;
   const int rp = (EPI != EPI_ROPE && pairs / 2 >= 2048) ? 2 : 1;
   const int sets = pairs / rp;
-  const bool kw4 = sets < 2048;
+  const bool kw4 = sets < gemv_kw4_sets();
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
