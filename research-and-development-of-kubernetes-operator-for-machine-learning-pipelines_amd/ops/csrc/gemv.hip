@@ -285,10 +285,13 @@ int gemv_max_m() {
 }
 
 // below this many row sets a workgroup's 4 waves share rows and split K (KW = 4): more loads
-// in flight per row for the small projections (MLOP_GEMV_KW4_SETS, default 2048)
-int gemv_kw4_sets() {
-  static const int v = env_int("MLOP_GEMV_KW4_SETS", 2048);
-  return v;
+// in flight per row.  Measured at batch-1/2/4 decode (scripts/run56.sh, run57.sh): at M <= 2
+// moving gate_up (7168 sets) to KW = 4 gives +3-4% tok/s at batch 1 and +1.5% at batch 2, at
+// M = 4 it loses 5% (the dot work per loaded byte grows with M), and o / qkv / down (2048-3072
+// sets) do not move.  MLOP_GEMV_KW4_SETS overrides both defaults.
+int gemv_kw4_sets(int M) {
+  static const int v = env_int("MLOP_GEMV_KW4_SETS", 0);
+  return v > 0 ? v : (M <= 2 ? 8192 : 2048);
 }
 
 template <int M, int EPI, bool NORM>
@@ -299,7 +302,7 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
   const int pairs = N / 2;
   const int rp = (EPI != EPI_ROPE && pairs / 2 >= 2048) ? 2 : 1;
   const int sets = pairs / rp;
-  const bool kw4 = sets < gemv_kw4_sets();
+  const bool kw4 = sets < gemv_kw4_sets(M);
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
