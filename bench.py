@@ -103,7 +103,7 @@ def main(argv=None):
     else:
         engine, ready_s, deploy_info = deploy_for_bench(
             model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank, engine_kwargs=ekw)
-    for k in ("model_build_ms", "kv_alloc_ms", "graph_capture_ms"):  # start-up breakdown
+    for k in ("model_build_ms", "kv_alloc_ms", "kv_malloc_ms", "kv_zero_ms", "graph_capture_ms"):  # start-up breakdown
         deploy_info[k] = engine.stats.get(k, 0)
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()

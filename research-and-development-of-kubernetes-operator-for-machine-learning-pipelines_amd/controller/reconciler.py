@@ -113,8 +113,11 @@ class MlflowModelReconciler:
             return None
         phase = status.get("phase")
         preds = []
-        versions = [(prev, 100 - int(status.get("canaryTraffic", 0))), (cur, int(status.get("canaryTraffic", 0)))] \
-            if phase == PH_CANARY and prev is not None else [(cur, 100)]
+        # PromotionFailed without rollback keeps the split the canary stopped at (reference
+        # mlflow_operator.py:347-349 leaves it); only Canary and PromotionFailed carry two predictors
+        split = phase in (PH_CANARY, PH_FAILED) and prev is not None
+        ct = int(status.get("canaryTraffic") or 0)
+        versions = [(prev, 100 - ct), (cur, ct)] if split else [(cur, 100)]
         for v, traffic in versions:
             uri, mv = await self._uri(spec, v)
             runtime, arch = self._runtime_of(spec, mv)
@@ -221,8 +224,9 @@ class MlflowModelReconciler:
             sd = await self._get_sd(ns, name)
             serving = seldon.traffic_of(sd)
             prev = cur if (cur is not None and serving.get(seldon.predictor_name(cur), 0) > 0) else None
-            if status.get("phase") == PH_CANARY and prev is not None:
-                # a newer version arrived mid-canary: keep the one with the most traffic as the baseline
+            if status.get("phase") in (PH_CANARY, PH_FAILED) and prev is not None:
+                # a newer version arrived mid-canary (or after a failed one left its split):
+                # keep the one with the most traffic as the baseline
                 old_prev = status.get("previousModelVersion")
                 if old_prev is not None and serving.get(seldon.predictor_name(old_prev), 0) >= serving.get(
                         seldon.predictor_name(cur), 0):

@@ -59,7 +59,18 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
   const int kv_end = last_q >= 0 ? ctx - ql + last_q + 1 : 0;
   const int p_begin = part * part_tokens;
   const int p_end = min(kv_end, p_begin + part_tokens);
-  if (p_begin >= p_end && nparts > 1) return;        // reducer skips empty partitions
+  if (p_begin >= p_end && nparts > 1) {              // reducer skips empty partitions
+    // kv_end == 0 (graph-bucket padding rows, ctx 0): no partition draws the last ticket of
+    // the in-launch combine, so partition 0 writes the zero row attn_reduce_kernel would
+    if (sem != nullptr && part == 0 && kv_end <= 0) {
+      const int rr = threadIdx.x >> 4, c = (threadIdx.x & 15) * 8;
+      const int qi2 = q0 + rr / G;
+      if (qi2 < ql)
+        *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + kvh * G + (rr % G)) * kD + c) =
+            u32x4{0u, 0u, 0u, 0u};
+    }
+    return;
+  }
 
   // this lane's q-row (B operand column) and its causal limit
   const int r = lane & 15, g4 = lane >> 4;

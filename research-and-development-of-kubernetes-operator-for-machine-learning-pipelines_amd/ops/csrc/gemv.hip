@@ -288,10 +288,11 @@ int gemv_max_m() {
 // in flight per row.  Measured at batch-1/2/4 decode (scripts/run56.sh, run57.sh): at M <= 2
 // moving gate_up (7168 sets) to KW = 4 gives +3-4% tok/s at batch 1 and +1.5% at batch 2, at
 // M = 4 it loses 5% (the dot work per loaded byte grows with M), and o / qkv / down (2048-3072
-// sets) do not move.  MLOP_GEMV_KW4_SETS overrides both defaults.
+// sets) do not move.  MLOP_GEMV_KW4_SETS, when set, overrides both defaults; an explicit 0
+// disables KW = 4 everywhere (no launch has fewer than 0 sets).
 int gemv_kw4_sets(int M) {
-  static const int v = env_int("MLOP_GEMV_KW4_SETS", 0);
-  return v > 0 ? v : (M <= 2 ? 8192 : 2048);
+  static const int v = env_int("MLOP_GEMV_KW4_SETS", -1);
+  return v >= 0 ? v : (M <= 2 ? 8192 : 2048);
 }
 
 template <int M, int EPI, bool NORM>

@@ -243,6 +243,7 @@ class Engine:
         self.graph_pool = None
         self.stats = collections.Counter()
         self.stats["kv_alloc_ms"] = kv_alloc_ms
+        self.stats.update(self.kv.timing_ms)
         self.tracer = StepTracer()
         self.profile_window = TorchProfileWindow()
         import os

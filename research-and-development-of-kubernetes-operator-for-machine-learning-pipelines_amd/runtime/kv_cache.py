@@ -9,9 +9,16 @@ Host side: ``BlockAllocator`` hands out page ids (free-list, O(1) alloc/free).
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 BLOCK_SIZE = 16
+
+
+def _sync(device) -> None:
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 class KVCache:
@@ -19,10 +26,17 @@ class KVCache:
                  device, dtype=torch.bfloat16):
         self.num_layers, self.num_blocks = num_layers, num_blocks
         self.num_kv_heads, self.head_dim = num_kv_heads, head_dim
-        self.k_all = torch.zeros(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
+        t0 = time.perf_counter()
+        self.k_all = torch.empty(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
                                  device=device, dtype=dtype)
-        self.v_all = torch.zeros(num_layers, num_blocks, num_kv_heads, head_dim, BLOCK_SIZE,
+        self.v_all = torch.empty(num_layers, num_blocks, num_kv_heads, head_dim, BLOCK_SIZE,
                                  device=device, dtype=dtype)
+        _sync(device)
+        t1 = time.perf_counter()
+        self.k_all.zero_()
+        self.v_all.zero_()
+        _sync(device)
+        self.timing_ms = {"kv_malloc_ms": int(1e3 * (t1 - t0)), "kv_zero_ms": int(1e3 * (time.perf_counter() - t1))}
         self.k = [self.k_all[i] for i in range(num_layers)]
         self.v = [self.v_all[i] for i in range(num_layers)]
 

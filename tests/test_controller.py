@@ -215,6 +215,11 @@ def test_reference_mode_no_rollback_leaves_split():
         env.reg.set_alias("m", "champion", env.version())
         assert await env.run_until(lambda: _phase(env, "PromotionFailed"), 3000)
         assert seldon.traffic_of(await env.sd()) == {"v1": 90, "v2": 10}
+        # level-triggered ticks after the failure must keep that split (not hand v2 100 %)
+        for _ in range(4):
+            await env.clock.sleep(40.0)
+            assert seldon.traffic_of(await env.sd()) == {"v1": 90, "v2": 10}
+            assert await _phase(env, "PromotionFailed")
         assert "RollbackComplete" not in env.reasons()
         await env.stop()
     run(go())

@@ -212,6 +212,33 @@ def test_paged_attention(gpu, Hq, Hkv, case):
     close(out, exp, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_paged_attention_padded_bucket(gpu, fused):
+    """Graph-bucket padding rows (q_len 1, ctx 0) under forced split-KV: both combine
+    paths (second-launch reduce and in-launch last-ticket combine) must write a zero
+    row there, not leave the buffer's old contents (NaN here) for o_proj / MoE routing."""
+    torch.manual_seed(0)
+    np.random.seed(0)
+    Hq, Hkv, NB = 32, 8, 400
+    q_lens, ctx_lens = [1, 1, 3, 1, 1], [1500, 33, 900, 0, 0]
+    kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, Hq // Hkv, NB, part_tokens=256, nparts=6,
+                     shuffle_rows=False)
+    if fused:
+        m.part_sem = torch.zeros(m.tile_seq.numel() * Hkv, dtype=torch.int32, device=gpu)
+    q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
+    exp = ref.paged_attention(q, kc, vc, m)
+    for _ in range(2):
+        out = torch.full_like(q, float("nan"))
+        ops.paged_attention(q, kc, vc, m, out=out)
+        assert torch.isfinite(out).all()
+        assert (out[-2:] == 0).all()
+        close(out, exp, atol=2e-2, rtol=2e-2)
+        if fused:
+            assert int(m.part_sem.abs().sum()) == 0
+
+
 def test_attention_spike_rescale(gpu):
     """Force the online-softmax rescale branch: a late key dominates."""
     Hq, Hkv = 32, 8
