@@ -181,6 +181,8 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem,
       (int)part_tokens, (int)nparts, (int)k_cache.size(0), sem, cur_stream());
 }
 
+int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
+
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, (int)epi);
 }
@@ -453,6 +455,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
+  m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
   m.def("gemm_rope_supported(int M, int N, int K) -> bool", &gemm_rope_supported);
   m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");

@@ -35,6 +35,7 @@
 // B = W[e] ([E, N, K]); blockIdx.y enumerates (expert, m-tile) pairs on device.
 #include "common.h"
 #include "launch.h"
+#include "rope_epi.h"
 
 namespace mlop {
 
@@ -48,90 +49,6 @@ constexpr int kStages = 3;
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 
-
-// RoPE / paged-cache stores of `nheads` consecutive 128-wide heads of a staged 256-row
-// C tile (EPI_ROPE).  `at(r, c)` returns the bf16-rounded projection output of tile row r,
-// column c (column 0 = first column of head `head0`), so the math is rope_cache_kernel's
-// on the same bf16 inputs.  Latency-shaped: every per-row index (position, slot) and the
-// cos/sin values a thread needs are loaded up front in one batch (the accumulators are
-// dead by now, so the registers are free), then the heads are rotated and stored; rows
-// >= `rows` are skipped.
-template <int NT, typename At>
-__device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nheads, int m0, int rows,
-                                                const RopeEpi& re, int tid) {
-  constexpr int D = 128, HALF = 64, BM = 256;
-  constexpr int QK = BM * (HALF / 8) / NT;  // (row, 8-column) items per thread, q/k heads
-  // v heads: lane -> row, so one store instruction writes a dim of 64 consecutive rows
-  // (a prefill chunk's consecutive slots: 16 tokens = one contiguous 32-B run of the
-  // dim-major [NB, Hkv, D, BS] page instead of 64 scattered 2-B writes)
-  constexpr int VD = D / (NT / BM);          // dims per thread
-  const int cq = (tid & 7) * 8, rq = tid >> 3;       // q/k item k: row rq + k * NT/8
-  const int rv = tid % BM, dv0 = (tid / BM) * VD;
-  const int n_rope = re.Hq + re.Hkv, n_all = re.Hq + 2 * re.Hkv;
-  const bool any_rope = head0 < n_rope, any_k = head0 + nheads > re.Hq && head0 < n_rope;
-  const bool any_v = head0 + nheads > n_rope;
-  int slot_q[QK], slot_v = -1;
-  float4 cs[QK][4];
-  if (any_rope) {
-    int p[QK];
-#pragma unroll
-    for (int k = 0; k < QK; ++k) {
-      const int r = rq + k * (NT / 8);
-      p[k] = r < rows ? re.pos[m0 + r] : 0;
-      slot_q[k] = (any_k && r < rows) ? re.slots[m0 + r] : -1;
-    }
-#pragma unroll
-    for (int k = 0; k < QK; ++k) {
-      const float4* row = reinterpret_cast<const float4*>(re.cos_sin + (size_t)p[k] * D);
-      cs[k][0] = row[cq / 4];
-      cs[k][1] = row[cq / 4 + 1];
-      cs[k][2] = row[(HALF + cq) / 4];
-      cs[k][3] = row[(HALF + cq) / 4 + 1];
-    }
-  }
-  if (any_v && rv < rows) slot_v = re.slots[m0 + rv];
-  for (int hh = 0; hh < nheads; ++hh) {
-    const int head = head0 + hh;
-    if (head >= n_all) break;
-    if (head < n_rope) {
-#pragma unroll
-      for (int k = 0; k < QK; ++k) {
-        const int r = rq + k * (NT / 8);
-        if (r >= rows) continue;
-        uint16_t* dst;
-        if (head < re.Hq) {
-          dst = re.q_out + ((size_t)(m0 + r) * re.Hq + head) * D;
-        } else {
-          const int slot = slot_q[k];
-          if (slot < 0) continue;
-          dst = re.k_cache + (((size_t)(slot / re.BS) * re.Hkv + (head - re.Hq)) * re.BS + slot % re.BS) * D;
-        }
-        const float cc[8] = {cs[k][0].x, cs[k][0].y, cs[k][0].z, cs[k][0].w,
-                             cs[k][1].x, cs[k][1].y, cs[k][1].z, cs[k][1].w};
-        const float ss[8] = {cs[k][2].x, cs[k][2].y, cs[k][2].z, cs[k][2].w,
-                             cs[k][3].x, cs[k][3].y, cs[k][3].z, cs[k][3].w};
-        u32x4 oa, ob;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float x0 = at(r, hh * D + cq + 2 * j), x1 = at(r, hh * D + cq + 2 * j + 1);
-          const float y0 = at(r, hh * D + HALF + cq + 2 * j), y1 = at(r, hh * D + HALF + cq + 2 * j + 1);
-          oa[j] = pack2(x0 * cc[2 * j] - y0 * ss[2 * j], x1 * cc[2 * j + 1] - y1 * ss[2 * j + 1]);
-          ob[j] = pack2(y0 * cc[2 * j] + x0 * ss[2 * j], y1 * cc[2 * j + 1] + x1 * ss[2 * j + 1]);
-        }
-        *reinterpret_cast<u32x4*>(dst + cq) = oa;
-        *reinterpret_cast<u32x4*>(dst + HALF + cq) = ob;
-      }
-    } else {
-      const int kh = head - n_rope;
-      if (slot_v >= 0) {
-        uint16_t* dst = re.v_cache + (((size_t)(slot_v / re.BS) * re.Hkv + kh) * D + dv0) * re.BS +
-                        slot_v % re.BS;
-#pragma unroll 16
-        for (int j = 0; j < VD; ++j) dst[j * re.BS] = f2bf(at(rv, hh * D + dv0 + j));
-      }
-    }
-  }
-}
 
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES = 3, bool SETPRIO = false>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
@@ -446,6 +363,14 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// large-M kernel choice (plan() variants below); MLOP_GEMM_BIG_VARIANT at load, and
+// settable at run time (gemm_big_variant op) so A/B microbenches run in one process
+static int g_big_variant = env_int("MLOP_GEMM_BIG_VARIANT", 3);
+int gemm_big_variant(int set) {
+  if (set >= 0) g_big_variant = set;
+  return g_big_variant;
+}
+
 // ---------------------------------------------------------------------------
 // Ping-pong 256x256 GEMM (cdna_hip_programming.md "The 256^2 8-phase template"):
 // 8 waves = 2 wave GROUPS (A halves) x 4 column strips, 128x64 outputs per wave.
@@ -699,7 +624,8 @@ struct Plan {
 //   batch in one tile (weights read once), BN by how many N tiles fill the chip;
 //   large M: variant 0 = 256x128 (3-stage ring), 1 = 256x256 (2-stage, 128x64 per
 //   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs,
-//   3 (default) = 256x256 two-group ping-pong (gemm_pp_kernel).
+//   3 (default) = 256x256 two-group ping-pong (gemm_pp_kernel).  (A four-wave 128x128-per-wave
+//   variant was measured 10-20% slower: profiles/r02_gemm_fourwave_rejected.md.)
 static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {
   Plan p{};
   p.variant = 0;
@@ -714,13 +640,14 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     p.BM = 256;
     p.BN = ((N + 127) / 128 >= bn_min_tiles) ? 128 : 64;
   } else {
-    static const int big = env_int("MLOP_GEMM_BIG_VARIANT", 3);
+    const int big = g_big_variant;
     static const int big_min_m = env_int("MLOP_GEMM_BIG_MIN_M", 1024);
     p.BM = 256;
     p.BN = 128;
     static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 192);
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    if (big && mrows >= big_min_m && !grouped && (big != 3 || (K % kBK == 0 && t256 >= pp_min_tiles))) {
+    const bool pp_ok = K % kBK == 0 && t256 >= pp_min_tiles;
+    if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
       p.BN = 256;
       p.variant = big;
     }

@@ -42,6 +42,9 @@ struct RopeEpi {
   int Hq, Hkv, BS;
 };
 long gemm_workspace_floats(int M, int N, int K, int epi);
+// large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
+// 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
+int gemm_big_variant(int set);
 // K2 skinny GEMV (gemv.hip): decode projections at M <= 8 (epi 0 none, 1 silu-mul, 3 rope)
 bool gemv_takes(int M, int N, int K, int epi);
 void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,

@@ -1,5 +1,5 @@
 """Run one GEMM shape repeatedly (for rocprofv3 counter collection).
-env: SHAPE=M,N,K  EPI=0|1  ITERS=n  BACKEND=mlop|hipblaslt"""
+env: SHAPE=M,N,K  EPI=0|1  ITERS=n  BACKEND=mlop|hipblaslt  BIG_VARIANT=3|4 (large-M kernel)"""
 import os
 import sys
 
@@ -16,6 +16,8 @@ be = os.environ.get("BACKEND", "mlop")
 x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
 w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
 ops.GEMM_BACKEND = "mlop"
+if os.environ.get("BIG_VARIANT"):
+    torch.ops.mlop.gemm_big_variant(int(os.environ["BIG_VARIANT"]))
 for _ in range(iters):
     if be == "mlop":
         ops.gemm(x, w, epi=epi)
