@@ -512,7 +512,19 @@ def deploy_and_wait(model: str = "llama3-8b", device="cuda", seed: int = 0, engi
 
         async def ready():
             o = await kube.get(GROUP, VERSION, namespace, PLURAL, model)
-            return (o.get("status") or {}).get("ready") == "True" and o
+            if (o.get("status") or {}).get("ready") == "True":
+                return o
+            # a predictor that cannot start (e.g. GPU OOM at weight load) fails the deploy
+            # now instead of at the timeout
+            try:
+                sd = await kube.get(SELDON_GROUP, SELDON_VERSION, namespace, SELDON_PLURAL, model)
+            except ApiError:
+                return False
+            for p in sd["spec"]["predictors"]:
+                _, failed, reason = seldon.predictor_health(sd, p["name"])
+                if failed:
+                    raise RuntimeError(f"predictor {p['name']} failed to start: {reason}")
+            return False
 
         obj = await wait_for(ready, timeout_s)
         ready_s = time.perf_counter() - t0

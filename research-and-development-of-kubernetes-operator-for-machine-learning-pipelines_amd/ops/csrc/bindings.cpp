@@ -181,6 +181,36 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem,
       (int)part_tokens, (int)nparts, (int)k_cache.size(0), sem, cur_stream());
 }
 
+// ---- lazily backed KV arenas (vmm.hip)
+bool vmm_supported(int64_t device) { return mlop::vmm_supported((int)device); }
+int64_t vmm_granularity(int64_t device) { return mlop::vmm_granularity((int)device); }
+
+// flat uint8 tensor over a reserved (unbacked) device range; its storage owns the arena
+Tensor vmm_arena(int64_t bytes, int64_t device) {
+  void* base = nullptr;
+  long reserved = 0;
+  std::shared_ptr<void> owner = mlop::vmm_reserve((long)bytes, (int)device, &base, &reserved);
+  TORCH_CHECK(owner != nullptr, "hipMemAddressReserve failed");
+  const at::Device dev(at::kCUDA, (int)device);
+  // target_device: the range is not backed yet, so the pointer's device cannot be queried
+  return at::for_blob(base, {(int64_t)reserved})
+      .deleter([owner, base](void*) mutable {
+        mlop::vmm_forget(base);
+        owner.reset();
+      })
+      .options(at::TensorOptions().dtype(at::kByte).device(dev))
+      .target_device(dev)
+      .make_tensor();
+}
+
+bool vmm_map_chunks(Tensor flat, int64_t region_stride, int64_t n_regions, int64_t chunk_bytes, int64_t first,
+                    int64_t count, bool async) {
+  return mlop::vmm_map_chunks(flat.data_ptr(), (long)region_stride, (int)n_regions, (long)chunk_bytes,
+                              (long)first, (long)count, async);
+}
+int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_ptr()); }
+int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
+
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
 
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
@@ -456,6 +486,13 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
+  m.def("vmm_supported(int device) -> bool", &vmm_supported);
+  m.def("vmm_granularity(int device) -> int", &vmm_granularity);
+  m.def("vmm_arena(int bytes, int device) -> Tensor", &vmm_arena);
+  m.def("vmm_map_chunks(Tensor flat, int region_stride, int n_regions, int chunk_bytes, int first, "
+        "int count, bool async_) -> bool", &vmm_map_chunks);
+  m.def("vmm_chunks_ready(Tensor flat) -> int", &vmm_chunks_ready);
+  m.def("vmm_error(Tensor flat) -> int", &vmm_error);
   m.def("gemm_rope_supported(int M, int N, int K) -> bool", &gemm_rope_supported);
   m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <memory>
 
 namespace mlop {
 
@@ -90,6 +91,17 @@ void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, vo
 long sample_workspace_bytes(int n, int V);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
                    const int* top_ks, const float* top_ps, const float* uniform, void* ws, hipStream_t st);
+
+// lazily backed KV arenas (vmm.hip): reserve VA, back chunks synchronously or on a native
+// worker thread; the returned owner must outlive every use of the range
+bool vmm_supported(int device);
+long vmm_granularity(int device);
+std::shared_ptr<void> vmm_reserve(long bytes, int device, void** base_out, long* reserved_out);
+void vmm_forget(void* base);
+bool vmm_map_chunks(void* base, long region_stride, int n_regions, long chunk_bytes, long first, long count,
+                    bool async);
+long vmm_chunks_ready(void* base);
+int vmm_error(void* base);
 
 // K15 custom one-shot all-reduce (allreduce.hip); handles are opaque state pointers
 long car_create(int rank, int world, long max_bytes, int device);

@@ -205,11 +205,13 @@ class Engine:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=tp.handle)
             nb = int(t.item())
         t_kv = time.perf_counter()
-        self.kv = KVCache(mc.num_layers, nb, model.n_kv, mc.head_dim, self.device, model.dtype)
+        # TP ranks must all hold every page id the leader hands out: eager backing there
+        self.kv = KVCache(mc.num_layers, nb, model.n_kv, mc.head_dim, self.device, model.dtype,
+                          lazy=False if tp.size > 1 else None)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         kv_alloc_ms = int(1e3 * (time.perf_counter() - t_kv))
-        self.alloc = BlockAllocator(nb)
+        self.alloc = BlockAllocator(nb, available=self.kv.ready_blocks())
         self.max_blocks_per_seq = blocks_needed(self.max_model_len)
         self.buckets = sorted(b for b in cfg.graph_buckets if b <= cfg.max_num_seqs) or [cfg.max_num_seqs]
         if self.buckets[-1] < cfg.max_num_seqs:
@@ -251,6 +253,8 @@ class Engine:
         tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS") == "1"
         if cfg.use_graphs and self.device.type == "cuda" and tp_graphs:
             self.capture_graphs()
+        self.kv.start_background_fill()  # after capture: the rest of a lazy KV arena
+        self.stats["kv_ready_blocks_at_start"] = self.alloc.available
 
     # ----------------------------------------------------------- sizing --
     def _auto_blocks(self) -> int:
@@ -379,6 +383,8 @@ class Engine:
         return out
 
     def _step(self):
+        if self.alloc.available < self.alloc.num_blocks:  # lazily backed KV chunks became ready
+            self.alloc.grow(self.kv.ready_blocks())
         if self._want_prefill():
             if self.running and self.cfg.mixed_prefill:
                 kind, out = "mixed", self._mixed_step()

@@ -3,17 +3,32 @@
 Device side: one K and one V tensor per layer, pages of 16 tokens:
   k[layer] : [num_blocks, Hkv, 16, D]   (token-major: A operand of S^T = K.Q^T)
   v[layer] : [num_blocks, Hkv, D, 16]   (dim-major:  A operand of O^T = V^T.P^T)
-allocated ZEROED once (the attention kernel relies on finite unused slots).
+zeroed before first use (the attention kernel relies on finite unused slots).
+
+Two ways to back it:
+
+* eager: two ``torch.empty`` + ``zero_`` (CPU, TP ranks, ``MLOP_KV_LAZY=0``);
+* lazy (default on one GPU): ``ops/csrc/vmm.hip`` reserves the whole virtual range, backs
+  and zeroes the first chunk of pages before the engine reports ready, and a native worker
+  thread backs the rest while it serves.  A 134 GB hipMalloc waits 0.7-4.8 s for the
+  driver to scrub memory another process just freed (profiles/r02_kv_lazy_map.md); backing
+  4 GB first takes that wait off the CR -> ready path.  ``ready_blocks()`` says how many
+  page ids are backed; the engine grows its ``BlockAllocator`` to it, so no page of an
+  unbacked chunk is ever handed out.
 
 Host side: ``BlockAllocator`` hands out page ids (free-list, O(1) alloc/free).
 """
 from __future__ import annotations
 
+import math
+import os
 import time
 
 import torch
 
 BLOCK_SIZE = 16
+CHUNK_BYTES_PER_REGION = 64 << 20   # lazy backing unit: 64 MB of each K / V layer tensor
+INITIAL_BYTES = 4 << 30             # backed before ready (all layers, K and V)
 
 
 def _sync(device) -> None:
@@ -21,24 +36,88 @@ def _sync(device) -> None:
         torch.cuda.synchronize(device)
 
 
+def _lazy_default(device) -> bool:
+    if torch.device(device).type != "cuda" or os.environ.get("MLOP_KV_LAZY", "1") == "0":
+        return False
+    from .. import ops
+
+    ops.load()
+    idx = torch.device(device).index
+    return bool(torch.ops.mlop.vmm_supported(torch.cuda.current_device() if idx is None else idx))
+
+
 class KVCache:
     def __init__(self, num_layers: int, num_blocks: int, num_kv_heads: int, head_dim: int,
-                 device, dtype=torch.bfloat16):
+                 device, dtype=torch.bfloat16, lazy: bool | None = None, initial_blocks: int | None = None):
         self.num_layers, self.num_blocks = num_layers, num_blocks
         self.num_kv_heads, self.head_dim = num_kv_heads, head_dim
+        self.device, self.dtype = torch.device(device), dtype
+        self.lazy = _lazy_default(device) if lazy is None else lazy
+        self._flat = None
         t0 = time.perf_counter()
-        self.k_all = torch.empty(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
-                                 device=device, dtype=dtype)
-        self.v_all = torch.empty(num_layers, num_blocks, num_kv_heads, head_dim, BLOCK_SIZE,
-                                 device=device, dtype=dtype)
-        _sync(device)
-        t1 = time.perf_counter()
-        self.k_all.zero_()
-        self.v_all.zero_()
-        _sync(device)
-        self.timing_ms = {"kv_malloc_ms": int(1e3 * (t1 - t0)), "kv_zero_ms": int(1e3 * (time.perf_counter() - t1))}
+        if self.lazy:
+            self._init_lazy(initial_blocks)
+            self.timing_ms = {"kv_malloc_ms": int(1e3 * (time.perf_counter() - t0)), "kv_zero_ms": 0}
+        else:
+            self.k_all = torch.empty(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
+                                     device=device, dtype=dtype)
+            self.v_all = torch.empty(num_layers, num_blocks, num_kv_heads, head_dim, BLOCK_SIZE,
+                                     device=device, dtype=dtype)
+            _sync(device)
+            t1 = time.perf_counter()
+            self.k_all.zero_()
+            self.v_all.zero_()
+            _sync(device)
+            self.timing_ms = {"kv_malloc_ms": int(1e3 * (t1 - t0)), "kv_zero_ms": int(1e3 * (time.perf_counter() - t1))}
         self.k = [self.k_all[i] for i in range(num_layers)]
         self.v = [self.v_all[i] for i in range(num_layers)]
+
+    def _init_lazy(self, initial_blocks):
+        L, Hkv, D = self.num_layers, self.num_kv_heads, self.head_dim
+        esz = torch.empty(0, dtype=self.dtype).element_size()
+        page = Hkv * BLOCK_SIZE * D                      # elements of one page in one layer tensor
+        page_bytes = page * esz
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        gran = int(torch.ops.mlop.vmm_granularity(idx))
+        unit = gran // math.gcd(gran, page_bytes)          # pages per granule-aligned step
+        cb = max(unit, (CHUNK_BYTES_PER_REGION // page_bytes) // unit * unit)
+        self.chunk_blocks = cb
+        self.n_chunks = -(-self.num_blocks // cb)
+        chunk_bytes = cb * page_bytes
+        region = self.n_chunks * chunk_bytes               # bytes of one layer's K (or V) tensor
+        n_regions = 2 * L
+        self._flat = torch.ops.mlop.vmm_arena(n_regions * region, idx)
+        base = self._flat.view(self.dtype)
+        rs = region // esz
+        self.k_all = base.as_strided((L, self.num_blocks, Hkv, BLOCK_SIZE, D), (rs, page, BLOCK_SIZE * D, D, 1), 0)
+        self.v_all = base.as_strided((L, self.num_blocks, Hkv, D, BLOCK_SIZE), (rs, page, D * BLOCK_SIZE, BLOCK_SIZE, 1),
+                                     L * rs)
+        if initial_blocks is None:
+            initial_blocks = max(2, INITIAL_BYTES // (n_regions * page_bytes))
+        first = min(self.n_chunks, max(1, -(-initial_blocks // cb)))
+        self._map_args = (region, n_regions, chunk_bytes)
+        self._first = first
+        self._filling = False
+        if not torch.ops.mlop.vmm_map_chunks(self._flat, *self._map_args, 0, first, False):
+            raise RuntimeError("KV arena: backing the first chunk failed")
+
+    def start_background_fill(self) -> None:
+        """Back the remaining chunks on a native worker thread.  Call it after any hipGraph
+        capture: VMM calls from another thread would invalidate a global-mode capture."""
+        if not self.lazy or self._filling or self._first >= self.n_chunks:
+            return
+        if not torch.ops.mlop.vmm_map_chunks(self._flat, *self._map_args, self._first,
+                                             self.n_chunks - self._first, True):
+            raise RuntimeError("KV arena: could not start the background backing thread")
+        self._filling = True
+
+    def ready_blocks(self) -> int:
+        """Page ids [0, ready_blocks()) are backed and zeroed (all of them when eager)."""
+        if not self.lazy:
+            return self.num_blocks
+        if torch.ops.mlop.vmm_error(self._flat):
+            raise RuntimeError("KV arena: backing a chunk failed (device out of memory?)")
+        return min(self.num_blocks, int(torch.ops.mlop.vmm_chunks_ready(self._flat)) * self.chunk_blocks)
 
     @staticmethod
     def bytes_per_block(num_layers, num_kv_heads, head_dim, dtype_bytes=2) -> int:
@@ -46,7 +125,8 @@ class KVCache:
 
     @property
     def nbytes(self) -> int:
-        return (self.k_all.numel() + self.v_all.numel()) * self.k_all.element_size()
+        return 2 * self.num_layers * self.num_blocks * self.num_kv_heads * BLOCK_SIZE * self.head_dim * \
+            self.k_all.element_size()
 
 
 def blocks_for_budget(budget_bytes: int, num_layers, num_kv_heads, head_dim, dtype_bytes=2) -> int:
@@ -55,13 +135,27 @@ def blocks_for_budget(budget_bytes: int, num_layers, num_kv_heads, head_dim, dty
 
 class BlockAllocator:
     """Free-list page allocator.  Block 0 is reserved as the always-valid
-    'null page' that padded block-table entries point at."""
+    'null page' that padded block-table entries point at.  ``available`` page
+    ids (a prefix of [0, num_blocks)) may grow over time (``grow``: pages of a
+    lazily backed KV arena becoming ready)."""
 
-    def __init__(self, num_blocks: int):
+    def __init__(self, num_blocks: int, available: int | None = None):
         if num_blocks < 2:
             raise ValueError("need at least 2 KV blocks")
         self.num_blocks = num_blocks
-        self._free = list(range(num_blocks - 1, 0, -1))  # pop() yields 1, 2, ...
+        self.available = num_blocks if available is None else max(2, min(available, num_blocks))
+        self._free = list(range(self.available - 1, 0, -1))  # pop() yields 1, 2, ...
+
+    def grow(self, available: int) -> int:
+        """Make page ids [self.available, available) allocatable; returns how many were added."""
+        available = min(available, self.num_blocks)
+        if available <= self.available:
+            return 0
+        new = list(range(available - 1, self.available - 1, -1))
+        self._free[:0] = new  # below the existing free ids: older pages are reused first
+        added = available - self.available
+        self.available = available
+        return added
 
     @property
     def num_free(self) -> int:
@@ -81,7 +175,7 @@ class BlockAllocator:
         self._free.extend(reversed(list(blocks)))
 
     def usage(self) -> float:
-        return 1.0 - len(self._free) / (self.num_blocks - 1)
+        return 1.0 - len(self._free) / (self.available - 1)
 
 
 def blocks_needed(num_tokens: int) -> int:

@@ -46,3 +46,20 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 16 and d["value"] > 0
     # whole-job aggregate over ranks = per-GPU value x N
     assert abs(d["served_tokens_per_sec_per_gpu"] * 2 - d["value"]) < 1e-3 * d["value"] + 0.02
+
+
+def test_deploy_fails_fast_when_predictor_cannot_start():
+    """A predictor whose start-up raises (here: a 1-page KV cache) fails the bench's
+    operator deploy at once, not after the 900 s readiness timeout."""
+    import time
+
+    import pytest
+
+    sys.path.insert(0, ROOT)
+    from mlopamd.controller.local import deploy_and_wait
+
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="failed to start"):
+        deploy_and_wait(model="tiny-llama", device="cpu", timeout_s=120.0,
+                        engine_kwargs=dict(num_kv_blocks=1, use_graphs=False))
+    assert time.time() - t0 < 60

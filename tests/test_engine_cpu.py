@@ -183,3 +183,17 @@ def test_decode_forward_with_norm_fusion(tiny, cfg):
         ops.NORM_FUSION = False
     for p, o in zip(prompts, outs):
         assert o == greedy_ref(model, p, 5)
+
+
+def test_block_allocator_grow():
+    """Lazily backed KV: only ids below ``available`` are handed out until grow()."""
+    a = BlockAllocator(100, available=10)
+    assert a.num_free == 9 and a.usage() == 0.0
+    x = a.allocate(9)
+    assert max(x) < 10 and not a.can_allocate(1)
+    assert a.grow(40) == 30 and a.available == 40 and a.num_free == 30
+    y = a.allocate(30)
+    assert set(y) == set(range(10, 40))
+    assert a.grow(5) == 0 and a.grow(1000) == 60 and a.available == 100
+    a.free(x + y)
+    assert a.num_free == 99 and a.usage() == 0.0
