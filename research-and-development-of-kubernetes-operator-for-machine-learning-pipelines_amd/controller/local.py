@@ -498,7 +498,8 @@ def deploy_and_wait(model: str = "llama3-8b", device="cuda", seed: int = 0, engi
 
             if torch.device(device).type == "cuda":
                 torch.cuda.set_device(device)  # worker thread: HIP's current device is per-thread
-            eng = build_engine(env.get("MLOP_ARCHITECTURE", model), device=device, seed=seed, **engine_kwargs)
+            eng = build_engine(env.get("MLOP_ARCHITECTURE", model), device=device, seed=seed,
+                               model_uri=env.get("MLOP_MODEL_URI"), **engine_kwargs)
             built["engine"] = eng
             return eng
 

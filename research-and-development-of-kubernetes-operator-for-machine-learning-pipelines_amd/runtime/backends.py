@@ -36,6 +36,30 @@ class ByteTokenizer:
         return bytes(max(0, min(255, i - self.offset)) for i in ids if i >= self.offset).decode("utf-8", "replace")
 
 
+class HFTokenizer:
+    """A checkpoint's ``tokenizer.json`` (Hugging Face ``tokenizers``, no network)."""
+
+    def __init__(self, path):
+        from tokenizers import Tokenizer
+
+        self._tok = Tokenizer.from_file(str(path))
+
+    def encode(self, text: str) -> list[int]:
+        return self._tok.encode(text).ids
+
+    def decode(self, ids) -> str:
+        return self._tok.decode(list(ids), skip_special_tokens=True)
+
+
+def load_tokenizer(checkpoint_dir):
+    """The checkpoint's own tokenizer when it ships one, else the byte tokenizer."""
+    if checkpoint_dir is not None:
+        p = Path(checkpoint_dir) / "tokenizer.json"
+        if p.is_file():
+            return HFTokenizer(p)
+    return ByteTokenizer()
+
+
 class _Req:
     __slots__ = ("prompt", "params", "loop", "future", "queue", "tokens", "t0", "t_first", "seq")
 

@@ -17,14 +17,23 @@ from .engine import Engine, EngineConfig
 
 
 def build_engine(model: str = "llama3-8b", device="cuda", seed: int = 0, tp_state=None,
-                 dtype=torch.bfloat16, **engine_kwargs) -> Engine:
+                 dtype=torch.bfloat16, model_uri: str | None = None, **engine_kwargs) -> Engine:
+    """Weights from the predictor's artifact when it is a local HF checkpoint
+    (``models.loader.resolve_model_dir``), else random-init ``model`` (the benchmark)."""
+    from ..models.loader import load_pretrained, resolve_model_dir
+
     t0 = time.perf_counter()
-    m = build_model(model, device=device, dtype=dtype, pstate=tp_state, seed=seed)
+    ckpt = resolve_model_dir(model_uri)
+    if ckpt is not None:
+        m = load_pretrained(ckpt, device=device, dtype=dtype, pstate=tp_state)
+    else:
+        m = build_model(model, device=device, dtype=dtype, pstate=tp_state, seed=seed)
     if torch.device(device).type == "cuda":
         torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     eng = Engine(m, EngineConfig(**engine_kwargs))
     eng.stats["model_build_ms"] = int(1e3 * (t1 - t0))
+    eng.checkpoint_dir = ckpt  # None: random-init weights
     return eng
 
 

@@ -191,6 +191,7 @@ class StepBatch:
 class Engine:
     def __init__(self, model, cfg: EngineConfig | None = None):
         self.model = model
+        self.checkpoint_dir = None  # set by deploy.build_engine when the weights came from a checkpoint
         self.cfg = cfg = cfg or EngineConfig()
         self.device = model.device
         mc = model.cfg

@@ -13,7 +13,9 @@ code, which is what the operator's canary gate queries.
 
 ``python -m mlopamd.runtime.server --runtime mlop-llm --architecture llama3-8b``
 starts it; configuration also comes from the env the SeldonDeployment sets
-(MLOP_RUNTIME, MLOP_MODEL_URI, MLOP_ARCHITECTURE, MLOP_ENGINE_*).
+(MLOP_RUNTIME, MLOP_MODEL_URI, MLOP_ARCHITECTURE, MLOP_ENGINE_*, MLOP_DTYPE).  A model URI that
+resolves to a local Hugging Face checkpoint (models/loader.py) is served with its weights and
+``tokenizer.json``; otherwise the architecture is random-initialised (the benchmark setup).
 Fault injection for canary tests: MLOP_INJECT_LATENCY_S, MLOP_INJECT_ERROR_RATE,
 MLOP_INJECT_START_ERROR (fail at start-up, e.g. a GPU OOM message), MLOP_INJECT_CRASH_AFTER_S
 (exit with status 139 after serving that long).
@@ -205,13 +207,18 @@ def build_backend(runtime: str, model_uri: str | None, architecture: str | None,
     from .backends import LLMBackend
     from .deploy import build_engine
 
+    from .backends import load_tokenizer
+
+    import torch
+
     t0 = time.perf_counter()
+    dtype = {"float32": torch.float32, "bfloat16": torch.bfloat16}[os.environ.get("MLOP_DTYPE", "bfloat16")]
     eng = build_engine(architecture or "llama3-8b", device=device, seed=seed, tp_state=tp_state,
-                       **(engine_kwargs or {}))
+                       model_uri=model_uri, dtype=dtype, **(engine_kwargs or {}))
     if metrics is not None:
         metrics.load_seconds.labels(**metrics.labels).set(time.perf_counter() - t0)
         metrics.ready.labels(**metrics.labels).set(1)
-    return LLMBackend(eng, metrics, name=name).start()
+    return LLMBackend(eng, metrics, tokenizer=load_tokenizer(eng.checkpoint_dir), name=name).start()
 
 
 def engine_kwargs_from_env() -> dict:
