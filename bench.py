@@ -59,6 +59,10 @@ def parse(argv=None):
     ap.add_argument("--no-operator", action="store_true", help="skip the CR->SeldonDeployment deploy path")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--shared-prefix", type=int, default=0,
+                    help="the first N prompt tokens are the same for every request (a system prompt): "
+                         "exercises the prefix cache; 0 = fully random prompts (the headline)")
+    ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--save-gemm-table", default=None,
                     help="after the run, write the per-shape GEMM backend choices measured here to this JSON")
     ap.add_argument("--tp", type=int, default=1,
@@ -84,7 +88,8 @@ def main(argv=None):
     ekw = dict(max_num_seqs=a.batch, max_num_batched_tokens=a.max_batched_tokens,
                max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
                prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
-               mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk)
+               mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk,
+               enable_prefix_caching=not a.no_prefix_cache)
     t0 = time.perf_counter()
     leader = True
     if a.tp > 1:
@@ -115,9 +120,11 @@ def main(argv=None):
     V = engine.model.cfg.vocab_size
     P, O = a.prompt_len, a.output_len
 
+    lo = min(1000, V // 4)
+    shared = rng.integers(lo, V - lo, size=min(a.shared_prefix, P)).tolist()
+
     def new_request(max_tokens):
-        lo = min(1000, V // 4)
-        prompt = rng.integers(lo, V - lo, size=P).tolist()
+        prompt = shared + rng.integers(lo, V - lo, size=P - len(shared)).tolist()
         engine.add_request(prompt, SamplingParams(max_tokens=int(max_tokens), temperature=a.temperature,
                                                   top_k=50 if a.temperature > 0 else 0, ignore_eos=True))
 
@@ -195,7 +202,8 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
                        "prompt_len": a.prompt_len, "output_len": a.output_len,
                        "parallelism": f"dp{world // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
                        "graphs": not a.no_graphs, "mixed_prefill": not a.no_mixed,
-                       "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap},
+                       "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap,
+                       "shared_prefix": a.shared_prefix, "prefix_cache": not a.no_prefix_cache},
             "p50_cr_ready_s": round(p50_ready, 3),
             "served_tokens_per_sec_per_gpu": round(value / world, 2),
             "prefill_tokens_per_sec": round(total_prefill / max_t, 2),

@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from .attn_meta import MetaBuffers, plan_partitions
-from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, blocks_needed
+from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, blocks_needed, prefix_hashes
 from .sampler import Sampler, SamplingParams
 from .tracing import StepTracer, TorchProfileWindow
 
@@ -98,6 +98,8 @@ class Sequence:
     first_token_time: float | None = None
     finish_time: float | None = None
     finish_reason: str | None = None
+    hashes: list = field(default_factory=list)  # prefix hashes of this sequence's full pages
+    n_reg: int = 0                              # leading pages matched in / registered to the prefix cache
 
     @property
     def length(self) -> int:
@@ -133,6 +135,7 @@ class EngineConfig:
     mixed_prefill: bool = True    # prefill chunks ride in the decode step (one forward)
     mixed_min_chunk: int = 64     # below this many free token slots, decode alone
     seed: int = 0
+    enable_prefix_caching: bool = True  # share computed prompt pages between requests (same prefix)
 
 
 @dataclass
@@ -326,6 +329,7 @@ class Engine:
         if seq.blocks:
             self.alloc.free(seq.blocks)
             seq.blocks = []
+        seq.n_reg = 0
         if seq.row >= 0:
             self.r_nblk[seq.row] = 0
             self.free_rows.append(seq.row)
@@ -415,11 +419,12 @@ class Engine:
             budget -= n
         while budget > 0 and self.waiting and self.free_rows:
             seq = self.waiting[0]
-            n = min(seq.length, budget)
             seq.row = self.free_rows.pop()
-            if not self._ensure_blocks(seq, n):
-                self.free_rows.append(seq.row)
-                seq.row = -1
+            if self.cfg.enable_prefix_caching:
+                self._match_prefix(seq)
+            n = min(seq.length - seq.num_cached, budget)
+            if not self._ensure_blocks(seq, seq.num_cached + n):
+                self._release(seq)  # matched prefix pages back to the cache, row freed
                 break
             self.waiting.popleft()
             seq.status = Status.PREFILL
@@ -429,11 +434,50 @@ class Engine:
             budget -= n
         return batch, chunks
 
+    def _match_prefix(self, seq: Sequence) -> None:
+        """Reuse cached pages of this sequence's longest cached prefix (never the page
+        holding its last token: that one is computed to get the next-token logits)."""
+        nfull = (seq.length - 1) // BLOCK_SIZE
+        self.stats["prefix_query_tokens"] += seq.length
+        if nfull <= 0:
+            return
+        if len(seq.hashes) < nfull:
+            prev = seq.hashes[-1] if seq.hashes else 0
+            seq.hashes += prefix_hashes(seq.tokens(0, nfull * BLOCK_SIZE), nfull, len(seq.hashes), prev)
+        m = 0
+        for h in seq.hashes[:nfull]:
+            b = self.alloc.lookup(h)
+            if b is None:
+                break
+            self.alloc.take(b)
+            seq.blocks.append(b)
+            m += 1
+        if m:
+            self.meta.bt_h[seq.row, :m] = seq.blocks
+            self.r_nblk[seq.row] = m
+            seq.num_cached = m * BLOCK_SIZE
+            seq.n_reg = m
+            self.stats["prefix_hit_tokens"] += m * BLOCK_SIZE
+
+    def _register_prefix(self, seq: Sequence, ctx: int) -> None:
+        """Publish the pages this prefill filled (full pages of computed tokens)."""
+        full = ctx // BLOCK_SIZE
+        if full <= seq.n_reg:
+            return
+        if len(seq.hashes) < full:
+            prev = seq.hashes[-1] if seq.hashes else 0
+            seq.hashes += prefix_hashes(seq.tokens(0, full * BLOCK_SIZE), full, len(seq.hashes), prev)
+        for i in range(seq.n_reg, full):
+            self.alloc.register(seq.blocks[i], seq.hashes[i])
+        seq.n_reg = full
+
     def _prefill_finish(self, batch, ctx, done, tokens) -> list:
         outs = []
         ti = 0
         for s, c, d in zip(batch, ctx, done):
             s.num_cached = c
+            if self.cfg.enable_prefix_caching:
+                self._register_prefix(s, c)
             if d:
                 self.prefilling.remove(s)
                 s.status = Status.RUNNING

@@ -20,10 +20,12 @@ Host side: ``BlockAllocator`` hands out page ids (free-list, O(1) alloc/free).
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import time
 
+import numpy as np
 import torch
 
 BLOCK_SIZE = 16
@@ -134,48 +136,111 @@ def blocks_for_budget(budget_bytes: int, num_layers, num_kv_heads, head_dim, dty
 
 
 class BlockAllocator:
-    """Free-list page allocator.  Block 0 is reserved as the always-valid
-    'null page' that padded block-table entries point at.  ``available`` page
-    ids (a prefix of [0, num_blocks)) may grow over time (``grow``: pages of a
-    lazily backed KV arena becoming ready)."""
+    """Page allocator with reference counts and a prefix cache.
+
+    Block 0 is reserved as the always-valid 'null page' that padded block-table
+    entries point at.  ``available`` page ids (a prefix of [0, num_blocks)) may grow
+    over time (``grow``: pages of a lazily backed KV arena becoming ready).
+
+    Prefix caching (vLLM-style automatic prefix caching): a FULL page of computed
+    tokens can be ``register``-ed under the hash of its token prefix; a later request
+    with the same prefix ``take``-s it instead of recomputing it (reference count +1).
+    A page whose count drops to 0 stays cached but allocatable: uncached free pages are
+    handed out first (a plain stack, sliced: the per-step decode path allocates and frees
+    hundreds of pages), cached ones after them in least-recently-freed order (evicted).
+    """
 
     def __init__(self, num_blocks: int, available: int | None = None):
         if num_blocks < 2:
             raise ValueError("need at least 2 KV blocks")
         self.num_blocks = num_blocks
         self.available = num_blocks if available is None else max(2, min(available, num_blocks))
-        self._free = list(range(self.available - 1, 0, -1))  # pop() yields 1, 2, ...
+        self._ref = [0] * num_blocks        # plain lists: per-page Python ops beat numpy's per-call
+        self._hashed = bytearray(num_blocks)  # overhead at the few pages a step touches
+        self._free = list(range(self.available - 1, 0, -1))  # uncached free pages; pop() yields 1, 2, ...
+        self._cached_free: collections.OrderedDict[int, None] = collections.OrderedDict()  # LRU first
+        self._hash_of: dict[int, int] = {}
+        self._by_hash: dict[int, int] = {}
 
     def grow(self, available: int) -> int:
         """Make page ids [self.available, available) allocatable; returns how many were added."""
         available = min(available, self.num_blocks)
         if available <= self.available:
             return 0
-        new = list(range(available - 1, self.available - 1, -1))
-        self._free[:0] = new  # below the existing free ids: older pages are reused first
+        self._free[:0] = range(available - 1, self.available - 1, -1)  # below the older free ids
         added = available - self.available
         self.available = available
         return added
 
     @property
     def num_free(self) -> int:
-        return len(self._free)
+        return len(self._free) + len(self._cached_free)
+
+    @property
+    def num_cached(self) -> int:
+        return len(self._by_hash)
 
     def can_allocate(self, n: int) -> bool:
-        return n <= len(self._free)
+        return n <= self.num_free
 
     def allocate(self, n: int) -> list[int]:
-        if n > len(self._free):
-            raise MemoryError(f"KV cache exhausted: want {n}, free {len(self._free)}")
-        out = self._free[-n:] if n else []
-        del self._free[len(self._free) - n:]
-        return out[::-1]
+        if n > self.num_free:
+            raise MemoryError(f"KV cache exhausted: want {n}, free {self.num_free}")
+        k = min(n, len(self._free))
+        out = self._free[-k:][::-1] if k else []
+        del self._free[len(self._free) - k:]
+        for _ in range(n - k):  # evict least recently freed cached pages
+            b, _ = self._cached_free.popitem(last=False)
+            del self._by_hash[self._hash_of.pop(b)]
+            self._hashed[b] = 0
+            out.append(b)
+        ref = self._ref
+        for b in out:
+            ref[b] = 1
+        return out
 
     def free(self, blocks) -> None:
-        self._free.extend(reversed(list(blocks)))
+        ref, hashed, plain = self._ref, self._hashed, []
+        for b in reversed(blocks):  # a sequence holds each of its pages once
+            r = ref[b] - 1
+            ref[b] = r
+            if r == 0:
+                if hashed[b]:
+                    self._cached_free[b] = None
+                else:
+                    plain.append(b)
+        self._free.extend(plain)
+
+    # ----------------------------------------------------------- prefix cache --
+    def lookup(self, h: int) -> int | None:
+        return self._by_hash.get(h)
+
+    def take(self, b: int) -> None:
+        """One more reference to cached page ``b`` (a prefix hit)."""
+        if self._ref[b] == 0:
+            del self._cached_free[b]
+        self._ref[b] += 1
+
+    def register(self, b: int, h: int) -> None:
+        """Page ``b`` (held, count >= 1) now holds the computed full page of prefix hash ``h``."""
+        if h not in self._by_hash and not self._hashed[b]:
+            self._by_hash[h] = b
+            self._hash_of[b] = h
+            self._hashed[b] = 1
 
     def usage(self) -> float:
-        return 1.0 - len(self._free) / (self.available - 1)
+        return 1.0 - self.num_free / (self.available - 1)
+
+
+def prefix_hashes(tokens, n_blocks: int, start: int = 0, prev: int = 0) -> list[int]:
+    """Chained hashes of full pages [start, n_blocks) of ``tokens`` (page i's hash covers
+    every token of pages 0..i, so equal hashes mean equal prefixes)."""
+    out = []
+    h = prev
+    for i in range(start, n_blocks):
+        h = hash((h, tuple(tokens[i * BLOCK_SIZE:(i + 1) * BLOCK_SIZE])))
+        out.append(h)
+    return out
 
 
 def blocks_needed(num_tokens: int) -> int:

@@ -197,3 +197,66 @@ def test_block_allocator_grow():
     assert a.grow(5) == 0 and a.grow(1000) == 60 and a.available == 100
     a.free(x + y)
     assert a.num_free == 99 and a.usage() == 0.0
+
+
+def test_allocator_prefix_cache_lru():
+    a = BlockAllocator(8)
+    x = a.allocate(3)
+    for b, h in zip(x, (11, 22, 33)):
+        a.register(b, h)
+    assert a.num_cached == 3 and a.lookup(22) == x[1]
+    a.free(x)  # cached pages stay cached while free
+    assert a.num_free == 7 and a.num_cached == 3
+    a.take(x[0])  # a prefix hit on a free cached page
+    assert a.num_free == 6
+    y = a.allocate(4)  # uncached pages first, no eviction
+    assert not set(y) & set(x) and a.num_cached == 3
+    z = a.allocate(1)  # then the least recently freed cached page is evicted
+    assert z[0] in x[1:] and a.num_cached == 2 and a.lookup(22 if z[0] == x[1] else 33) is None
+    with pytest.raises(MemoryError):
+        a.allocate(2)
+    a.free([x[0]])
+    assert a.num_free == 2
+
+
+def _shared_prefix_prompts(n, prefix_len=70, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    prefix = torch.randint(2, 500, (prefix_len,), generator=g).tolist()
+    return [prefix + torch.randint(2, 500, (5 + 7 * i,), generator=g).tolist() for i in range(n)]
+
+
+@pytest.mark.parametrize("mixed", [True, False])
+def test_prefix_caching_matches_uncached(mixed):
+    """Requests sharing a 70-token prefix: with the prefix cache the later ones skip the
+    shared pages' prefill (hits counted), and every greedy output equals the
+    no-cache engine's (and the dense oracle's)."""
+    m = build_model(TINY_LLAMA, device="cpu", dtype=torch.float32, seed=4)
+    prompts = _shared_prefix_prompts(6)
+    outs = {}
+    for cache in (True, False):
+        eng = Engine(m, EngineConfig(max_num_seqs=4, max_num_batched_tokens=96, max_model_len=256, num_kv_blocks=64,
+                                     use_graphs=False, enable_prefix_caching=cache, mixed_prefill=mixed))
+        first = eng.generate(prompts[:1], SamplingParams(max_tokens=5, ignore_eos=True))
+        rest = eng.generate(prompts[1:], SamplingParams(max_tokens=5, ignore_eos=True))
+        outs[cache] = first + rest
+        if cache:
+            assert eng.stats["prefix_hit_tokens"] >= 5 * 64  # 4 full shared pages per later request
+        else:
+            assert eng.stats["prefix_hit_tokens"] == 0
+    assert outs[True] == outs[False]
+    for p, o in zip(prompts[:2], outs[True][:2]):
+        assert o == greedy_ref(m, p, 5)
+
+
+def test_prefix_cache_survives_preemption():
+    """A tiny KV pool forces preemptions; re-admitted sequences re-match their own cached
+    pages and the outputs still equal the dense oracle."""
+    m = build_model(TINY_LLAMA, device="cpu", dtype=torch.float32, seed=6)
+    prompts = _shared_prefix_prompts(5, prefix_len=40, seed=9)
+    eng = Engine(m, EngineConfig(max_num_seqs=5, max_num_batched_tokens=64, max_model_len=256, num_kv_blocks=13,
+                                 use_graphs=False))
+    outs = eng.generate(prompts, SamplingParams(max_tokens=40, ignore_eos=True))
+    assert eng.stats["preemptions"] > 0 and eng.stats["prefix_hit_tokens"] > 0
+    for p, o in zip(prompts, outs):
+        assert o == greedy_ref(m, p, 40)
+    assert eng.alloc.num_free == eng.alloc.available - 1  # every reference returned

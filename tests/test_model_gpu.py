@@ -69,3 +69,21 @@ def test_engine_staggered_arrivals(gpu, mixed):
         eng.step()
     assert (eng.stats["mixed_steps"] > 0) == mixed
     _check_greedy(model, prompts, [s.output for s in seqs])
+
+
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_MIXTRAL], ids=["llama", "mixtral"])
+def test_prefix_caching_gpu(gpu, cfg):
+    """Requests sharing a 100-token prefix on the GPU engine (graphs, mixed steps): the
+    later ones reuse the cached pages (hits counted) and still decode the dense oracle's
+    greedy tokens."""
+    torch.manual_seed(0)
+    model = build_model(cfg, device=gpu, seed=7)
+    g = torch.Generator().manual_seed(1)
+    prefix = torch.randint(2, 500, (100,), generator=g).tolist()
+    prompts = [prefix + torch.randint(2, 500, (3 + 11 * i,), generator=g).tolist() for i in range(5)]
+    eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+                                     num_kv_blocks=128, graph_buckets=(1, 2, 4, 8)))
+    outs = eng.generate(prompts[:1], SamplingParams(max_tokens=8, ignore_eos=True))
+    outs += eng.generate(prompts[1:], SamplingParams(max_tokens=8, ignore_eos=True))
+    assert eng.stats["prefix_hit_tokens"] >= 4 * 96  # 6 full shared pages per later request
+    _check_greedy(model, prompts, outs)
