@@ -54,6 +54,14 @@ class MixtralModel(LlamaModel):
         return self.mlp(i, x), residual
 
     def mlp_add_norm(self, i, x, residual, next_norm, eps):
+        """TP = EP = 1: MoE block + the next residual add / norm (decode-size dispatch in one
+        launch, combine fused into the norm: parallel.moe.moe_forward_add_norm)."""
+        if self.ps.ep.size == 1:
+            from ..parallel.moe import moe_forward_add_norm
+
+            L = self.layers[i]
+            return moe_forward_add_norm(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.expert_start,
+                                        self.n_local_experts, residual, next_norm, eps)
         return ops.add_rmsnorm(self.mlp(i, x), residual, next_norm, eps)
 
     def forward(self, ids, meta, kv):

@@ -534,6 +534,37 @@ def moe_permute(x, topi, e0: int, n_local: int):
     return xp, offsets, src, inv
 
 
+def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int):
+    """Decode-size MoE dispatch in ONE launch (router GEMV + route + sort + gather, moe.hip):
+    returns (topw, topi, xp, offsets, src, inv) or None when the shape is not on this path
+    (more than 16 tokens, CPU tensors)."""
+    if not x.is_cuda or x.shape[0] > 16:
+        return None
+    _need_gpu()
+    T, H = x.shape
+    dev = x.device
+    topw = torch.empty(T, top_k, dtype=torch.float32, device=dev)
+    topi = torch.empty(T, top_k, dtype=torch.int32, device=dev)
+    xp = torch.empty(T * top_k, H, dtype=x.dtype, device=dev)
+    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
+    src = torch.empty(T * top_k, dtype=torch.int32, device=dev)
+    inv = torch.empty(T * top_k, dtype=torch.int32, device=dev)
+    if not torch.ops.mlop.moe_dispatch_small(topw, topi, xp, offsets, src, inv, x.contiguous(), router_w,
+                                             e0, n_local):
+        return None
+    return topw, topi, xp, offsets, src, inv
+
+
+def moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps: float):
+    """residual <- residual + combine(y); returns rmsnorm(residual) * norm_w (one launch on GPU)."""
+    if y.is_cuda:
+        _need_gpu()
+        out = torch.empty_like(residual)
+        if torch.ops.mlop.moe_combine_add_rmsnorm(out, residual, y, inv, topw, norm_w, eps):
+            return out
+    return add_rmsnorm(moe_combine(y, inv, topw), residual, norm_w, eps)
+
+
 def moe_combine(y, inv, topw):
     """out[t] = sum_j topw[t,j] * y[inv[t*k+j]] (inv < 0 skipped), fp32 accumulate."""
     if not y.is_cuda:

@@ -391,6 +391,41 @@ void moe_permute(Tensor xp, Tensor offsets, Tensor src, Tensor inv, Tensor x, Te
                            (int)H, (int)e0, (int)n_local, cur_stream());
 }
 
+// decode-size dispatch (T <= 16): router GEMV + route + sort + gather in one launch; false = not taken
+bool moe_dispatch_small(Tensor topw, Tensor topi, Tensor xp, Tensor offsets, Tensor src, Tensor inv, Tensor x,
+                        Tensor router_w, int64_t e0, int64_t n_local) {
+  check_bf16(xp, "xp"); check_bf16(x, "x"); check_bf16(router_w, "router_w"); check_i32(topi, "topi");
+  check_i32(offsets, "offsets"); check_i32(src, "src"); check_i32(inv, "inv");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous(), "topw f32");
+  const int64_t T = x.size(0), H = x.size(1), E = router_w.size(0), k = topi.size(1);
+  if (!mlop::moe_dispatch_small_takes((int)T, (int)E, (int)k, (int)H)) return false;
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && router_w.size(1) == H, "x [T, H], router_w [E, H]");
+  TORCH_CHECK(topi.size(0) == T && topw.numel() == T * k && xp.size(0) == T * k && xp.size(1) == H,
+              "topi/topw [T, k], xp [T*k, H]");
+  TORCH_CHECK(n_local >= 1 && n_local <= 64 && offsets.numel() == n_local + 1 && src.numel() == T * k &&
+                  inv.numel() == T * k, "offsets / src / inv");
+  c10::DeviceGuard g(x.device());
+  mlop::launch_moe_dispatch_small(topw.data_ptr<float>(), topi.data_ptr<int>(), xp.data_ptr(),
+                                  offsets.data_ptr<int>(), src.data_ptr<int>(), inv.data_ptr<int>(), x.data_ptr(),
+                                  router_w.data_ptr(), (int)T, (int)E, (int)k, (int)H, (int)e0, (int)n_local,
+                                  cur_stream());
+  return true;
+}
+
+bool moe_combine_add_rmsnorm(Tensor out, Tensor residual, Tensor y, Tensor inv, Tensor topw, Tensor norm_w,
+                             double eps) {
+  check_bf16(out, "out"); check_bf16(residual, "residual"); check_bf16(y, "y"); check_bf16(norm_w, "norm_w");
+  check_i32(inv, "inv");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.dim() == 2, "topw");
+  const int64_t T = topw.size(0), k = topw.size(1), H = y.size(1);
+  TORCH_CHECK(out.numel() == T * H && residual.numel() == T * H && inv.numel() == T * k && norm_w.numel() == H,
+              "combine + norm shapes");
+  c10::DeviceGuard g(y.device());
+  return mlop::launch_moe_combine_add_rmsnorm(out.data_ptr(), residual.data_ptr(), y.data_ptr(),
+                                              inv.data_ptr<int>(), topw.data_ptr<float>(), norm_w.data_ptr(),
+                                              (float)eps, (int)T, (int)k, (int)H, cur_stream());
+}
+
 void moe_combine(Tensor out, Tensor y, Tensor inv, Tensor topw) {
   check_bf16(out, "out"); check_bf16(y, "y"); check_i32(inv, "inv");
   TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.dim() == 2, "topw");
@@ -511,6 +546,10 @@ TORCH_LIBRARY(mlop, m) {
   m.def("moe_permute(Tensor(a!) xp, Tensor(b!) offsets, Tensor(c!) src, Tensor(d!) inv, Tensor x, "
         "Tensor topi, int e0, int n_local) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor inv, Tensor topw) -> ()");
+  m.def("moe_dispatch_small(Tensor(a!) topw, Tensor(b!) topi, Tensor(c!) xp, Tensor(d!) offsets, Tensor(e!) src, "
+        "Tensor(f!) inv, Tensor x, Tensor router_w, int e0, int n_local) -> bool");
+  m.def("moe_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor y, Tensor inv, Tensor topw, "
+        "Tensor norm_w, float eps) -> bool");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, "
         "Tensor uniform) -> ()");
@@ -543,6 +582,8 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("gemm_norm", &gemm_norm);
   m.impl("gemm_norm_rope", &gemm_norm_rope);
   m.impl("moe_route", &moe_route);
+  m.impl("moe_dispatch_small", &moe_dispatch_small);
+  m.impl("moe_combine_add_rmsnorm", &moe_combine_add_rmsnorm);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);
   m.impl("argmax", &argmax);

@@ -82,6 +82,13 @@ void launch_moe_permute(void* xp, int* offsets, int* src, int* inv, const void* 
                         int T, int k, int H, int e0, int n_local, hipStream_t st);
 void launch_moe_combine(void* out, const void* y, const int* inv, const float* topw, int T, int k,
                         int H, hipStream_t st);
+// decode-size MoE dispatch in one launch: router GEMV + route + sort + gather (moe.hip)
+bool moe_dispatch_small_takes(int T, int E, int k, int H);
+void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, int* src, int* inv, const void* x,
+                               const void* wr, int T, int E, int k, int H, int e0, int n_local, hipStream_t st);
+// combine + residual add + RMSNorm in one launch; false = hidden size not instantiated
+bool launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, const int* inv, const float* topw,
+                                    const void* w, float eps, int T, int k, int H, hipStream_t st);
 void launch_argmax(long* out, const float* logits, int n, int V, long ld, hipStream_t st);
 // bf16 greedy argmax; ws (>= argmax_splits(n, V) * n int64, or null) splits small batches' rows
 int argmax_splits(int n, int V);

@@ -126,6 +126,188 @@ __global__ void __launch_bounds__(256) moe_combine_kernel(uint16_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode-size MoE dispatch in ONE launch (T <= kSmallT tokens): router GEMV (bf16-rounded
+// logits, as the separate router projection stores them), softmax / top-k / renormalise,
+// counting sort by local expert and the row gather.  At batch 1-16 each of the four
+// separate launches (router GEMV, route, sort, gather) is a ~5 us graph node doing <1 us of
+// work (profiles/r02_mixtral_b1.md); one workgroup does all four back to back.
+// Wave w computes the logits of experts w, w+8, ...: the expert's router row is loaded once
+// (all of a lane's chunks in flight together) while the wave walks the T activation rows.
+constexpr int kSmallT = 16, kMaxE = 64, kDispWaves = 8;
+
+template <int CH>  // 16-B chunks per lane per row: H = CH * 512
+__global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_small_kernel(
+    float* __restrict__ topw, int* __restrict__ topi, uint16_t* __restrict__ xp, int* __restrict__ offsets,
+    int* __restrict__ src, int* __restrict__ inv, const uint16_t* __restrict__ x,
+    const uint16_t* __restrict__ wr, int T, int E, int k, int H, int e0, int n_local) {
+  __shared__ float lg[kSmallT][kMaxE];
+  __shared__ int s_topi[kSmallT * 8];
+  __shared__ int cnt[kMaxE + 1];
+  __shared__ int base[kMaxE + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // 1. router logits: lg[t][e] = bf16(x[t] . wr[e])
+  for (int e = wv; e < E; e += kDispWaves) {
+    const uint16_t* we = wr + (size_t)e * H + lane * 8;
+    u32x4 b[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const u32x4*>(we + i * 512);
+    for (int t = 0; t < T; ++t) {
+      const uint16_t* xt = x + (size_t)t * H + lane * 8;
+      u32x4 a[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) a[i] = *reinterpret_cast<const u32x4*>(xt + i * 512);
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc += lo_bf(a[i][q]) * lo_bf(b[i][q]) + hi_bf(a[i][q]) * hi_bf(b[i][q]);
+      acc = wave_sum(acc);
+      if (lane == 0) lg[t][e] = bf2f(f2bf(acc));
+    }
+  }
+  for (int e = threadIdx.x; e <= n_local; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  // 2. softmax -> top-k -> renormalise (moe_route_kernel's math), one thread per token
+  if (threadIdx.x < T) {
+    const int t = threadIdx.x;
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[t][e]);
+    float sum = 0.f;
+    for (int e = 0; e < E; ++e) sum += __expf(lg[t][e] - mx);
+    const float rinv = 1.f / sum;
+    float picked = 0.f, wsel[8];
+    int isel[8];
+    unsigned long long used = 0ull;
+    for (int j = 0; j < k; ++j) {
+      int best = 0;
+      float bv = -1.f;
+      for (int e = 0; e < E; ++e) {
+        const float v = __expf(lg[t][e] - mx);
+        if (!((used >> e) & 1ull) && v > bv) { bv = v; best = e; }
+      }
+      used |= 1ull << best;
+      isel[j] = best;
+      wsel[j] = bv * rinv;
+      picked += bv * rinv;
+    }
+    const float rn = picked > 0.f ? 1.f / picked : 0.f;
+    for (int j = 0; j < k; ++j) {
+      topi[t * k + j] = isel[j];
+      topw[t * k + j] = wsel[j] * rn;
+      s_topi[t * k + j] = isel[j];
+    }
+  }
+  __syncthreads();
+  // 3. counting sort of the T*k slots by local expert (moe_sort_kernel), slot order kept
+  const int n_slots = T * k;
+  if (threadIdx.x == 0) {
+    for (int s = 0; s < n_slots; ++s) {
+      const int e = s_topi[s] - e0;
+      if (e >= 0 && e < n_local) ++cnt[e];
+    }
+    int acc = 0;
+    for (int e = 0; e < n_local; ++e) {
+      base[e] = acc;
+      offsets[e] = acc;
+      acc += cnt[e];
+      cnt[e] = 0;
+    }
+    offsets[n_local] = acc;
+    for (int s = 0; s < n_slots; ++s) {
+      const int e = s_topi[s] - e0;
+      if (e >= 0 && e < n_local) {
+        const int row = base[e] + cnt[e]++;
+        inv[s] = row;
+        src[row] = s;
+        s_topi[s] = row;  // reused: slot -> row for the gather below
+      } else {
+        inv[s] = -1;
+        s_topi[s] = -1;
+      }
+    }
+  }
+  __syncthreads();
+  // 4. gather: xp[row(s)] = x[s / k]
+  const int vpr = H / 8;
+  for (int i = threadIdx.x; i < n_slots * vpr; i += blockDim.x) {
+    const int s = i / vpr, c = (i % vpr) * 8;
+    const int row = s_topi[s];
+    if (row >= 0)
+      *reinterpret_cast<u32x4*>(xp + (size_t)row * H + c) =
+          *reinterpret_cast<const u32x4*>(x + (size_t)(s / k) * H + c);
+  }
+}
+
+bool moe_dispatch_small_takes(int T, int E, int k, int H) {
+  return T >= 1 && T <= kSmallT && E <= kMaxE && k <= 8 && (H == 1024 || H == 2048 || H == 4096 || H == 8192);
+}
+
+void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, int* src, int* inv, const void* x,
+                               const void* wr, int T, int E, int k, int H, int e0, int n_local, hipStream_t st) {
+#define MLOP_DISP(CH)                                                                                       \
+  moe_dispatch_small_kernel<CH><<<1, 64 * kDispWaves, 0, st>>>(topw, topi, (uint16_t*)xp, offsets, src, inv, \
+                                                               (const uint16_t*)x, (const uint16_t*)wr, T, E, k, \
+                                                               H, e0, n_local)
+  switch (H) {
+    case 1024: MLOP_DISP(2); break;
+    case 2048: MLOP_DISP(4); break;
+    case 4096: MLOP_DISP(8); break;
+    default: MLOP_DISP(16); break;
+  }
+#undef MLOP_DISP
+}
+
+// combine fused with the decoder's residual add + RMSNorm (one workgroup per token row, 8
+// elements per thread: at decode sizes every row's reads are in flight at once):
+//   m = bf16(sum_j topw[t, j] * y[inv[t*k + j]])   (moe_combine_kernel's rounding)
+//   residual[t] = bf16(residual[t] + m);  out[t] = bf16(bf16(residual[t] * rsqrt(mean sq + eps)) * w)
+__global__ void __launch_bounds__(1024) moe_combine_add_rmsnorm_kernel(
+    uint16_t* __restrict__ out, uint16_t* __restrict__ residual, const uint16_t* __restrict__ y,
+    const int* __restrict__ inv, const float* __restrict__ topw, const uint16_t* __restrict__ w, float eps,
+    int k, int H) {
+  __shared__ float scratch[16];
+  const int t = blockIdx.x, c = threadIdx.x * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const int row = inv[t * k + j];
+    if (row < 0) continue;
+    const float wt = topw[t * k + j];
+    const u32x4 v = *reinterpret_cast<const u32x4*>(y + (size_t)row * H + c);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[2 * q] += wt * lo_bf(v[q]);
+      acc[2 * q + 1] += wt * hi_bf(v[q]);
+    }
+  }
+  const u32x4 res = *reinterpret_cast<const u32x4*>(residual + (size_t)t * H + c);
+  const u32x4 wv = *reinterpret_cast<const u32x4*>(w + c);
+  u32x4 r;
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t m = pack2(acc[2 * q], acc[2 * q + 1]);
+    r[q] = pack2(lo_bf(m) + lo_bf(res[q]), hi_bf(m) + hi_bf(res[q]));
+    ss += lo_bf(r[q]) * lo_bf(r[q]) + hi_bf(r[q]) * hi_bf(r[q]);
+  }
+  *reinterpret_cast<u32x4*>(residual + (size_t)t * H + c) = r;
+  const float rs = rsqrtf(block_sum(ss, scratch) / (float)H + eps);
+  u32x4 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = pack2(bf2f(f2bf(lo_bf(r[q]) * rs)) * lo_bf(wv[q]), bf2f(f2bf(hi_bf(r[q]) * rs)) * hi_bf(wv[q]));
+  *reinterpret_cast<u32x4*>(out + (size_t)t * H + c) = o;
+}
+
+bool launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, const int* inv, const float* topw,
+                                    const void* w, float eps, int T, int k, int H, hipStream_t st) {
+  if (T == 0) return true;
+  if (H % 512 || H > 8192) return false;  // whole 64-thread waves, <= 1024 threads
+  moe_combine_add_rmsnorm_kernel<<<T, H / 8, 0, st>>>((uint16_t*)out, (uint16_t*)residual, (const uint16_t*)y,
+                                                      inv, topw, (const uint16_t*)w, eps, k, H);
+  return true;
+}
+
 void launch_moe_route(float* topw, int* topi, const void* logits, int T, int E, int k,
                       hipStream_t st) {
   if (T == 0) return;

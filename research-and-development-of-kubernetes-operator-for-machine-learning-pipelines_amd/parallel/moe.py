@@ -27,17 +27,36 @@ def route(x: torch.Tensor, router_w: torch.Tensor, top_k: int):
     return ops.moe_route(logits, top_k)
 
 
-def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int):
+def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None, combine: bool = True):
     """Sum over the top-k slots whose expert is in [e0, e0+n_local) of w * expert(x).
 
     permute (K12) -> grouped gate_up GEMM with fused SiLU-mul (K13, w13 rows
-    gate/up-interleaved) -> grouped down GEMM (K13) -> weighted gather (K14)."""
+    gate/up-interleaved) -> grouped down GEMM (K13) -> weighted gather (K14).
+    ``dispatched``: (xp, offsets, inv) from ops.moe_dispatch_small; ``combine=False``
+    returns (y, inv) so the caller can fuse the weighted gather into its next kernel."""
     T, k = topi.shape
-    xp, offsets, src, inv = ops.moe_permute(x, topi, e0, n_local)
+    if dispatched is None:
+        xp, offsets, src, inv = ops.moe_permute(x, topi, e0, n_local)
+    else:
+        xp, offsets, inv = dispatched
     avg = max(1, (T * k) // max(1, n_local))
     a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg)
     y = ops.grouped_gemm(a, w2, offsets, avg_rows=avg)
-    return ops.moe_combine(y, inv, topw)
+    return ops.moe_combine(y, inv, topw) if combine else (y, inv)
+
+
+def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int, residual, norm_w, eps: float):
+    """Single-rank MoE block followed by the decoder's residual add + RMSNorm.  At decode
+    sizes the router GEMV, routing, sort and gather are ONE launch (moe_dispatch_small) and
+    the weighted combine rides in the add + RMSNorm launch: 6 MoE glue launches -> 2."""
+    d = ops.moe_dispatch_small(x, router_w, top_k, e0, n_local)
+    if d is None:
+        topw, topi = route(x, router_w, top_k)
+        y, inv = local_experts(x, topw, topi, w13, w2, e0, n_local, combine=False)
+    else:
+        topw, topi, xp, offsets, _src, inv = d
+        y, inv = local_experts(x, topw, topi, w13, w2, e0, n_local, dispatched=(xp, offsets, inv), combine=False)
+    return ops.moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps)
 
 
 def moe_forward(x, router_w, w13, w2, top_k: int, ep, e0: int, n_local: int, mode: str = "allreduce"):

@@ -30,7 +30,7 @@ span = (win[-1][1] - win[0][0]) / 1e6
 busy = sum(r[1] - r[0] for r in win) / 1e6
 agg = collections.defaultdict(lambda: [0, 0.0])
 for s, e, n, g, wg in win:
-    short = n.split("(")[0].replace("void ", "")[:70]
+    short = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:70]
     k = (short, g[0] // wg, g[1], g[2])
     agg[k][0] += 1
     agg[k][1] += (e - s) / 1e3

@@ -450,6 +450,48 @@ def test_grouped_gemv_decode(gpu, counts, epi, N, K):
         close(y[a:b], r, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (4, 8, 2, 4096), (16, 8, 2, 1024), (7, 4, 1, 8192),
+                                     (5, 64, 8, 2048)])
+def test_moe_dispatch_small(gpu, T, E, k, H):
+    """One-launch decode dispatch (router GEMV + route + sort + gather) against the
+    separate router projection + moe_route + moe_permute, for the full and a partial
+    (expert-parallel) local expert range."""
+    torch.manual_seed(T * E)
+    x = torch.randn(T, H, device=gpu, dtype=bf)
+    wr = (0.05 * torch.randn(E, H, device=gpu)).to(bf)
+    logits = (x.float() @ wr.float().t()).to(bf)
+    p = torch.softmax(logits.float(), -1)
+    for e0, nl in [(0, E), (E // 2, E - E // 2)]:
+        topw, topi, xp, off, src, inv = ops.moe_dispatch_small(x, wr, k, e0, nl)
+        w_ref, i_ref = ops.moe_route(logits, k)
+        # bf16 logits tie often: compare the chosen probabilities, then the weights
+        close(p.gather(1, topi.long()), p.gather(1, i_ref.long()), atol=1e-3, rtol=1e-3)
+        close(topw, w_ref, atol=2e-3, rtol=2e-3)
+        xp_r, off_r, _, inv_r = ops.moe_permute(x, topi, e0, nl)
+        assert torch.equal(off.cpu(), off_r.cpu()) and torch.equal(inv.cpu(), inv_r.cpu())
+        n = int(off[-1])
+        close(xp[:n], xp_r[:n], atol=0, rtol=0)
+        sel = torch.nonzero(inv >= 0).flatten()
+        assert torch.equal(src[inv[sel].long()].cpu(), sel.to(torch.int32).cpu())
+
+
+@pytest.mark.parametrize("T,k,H", [(1, 2, 4096), (9, 2, 4096), (3, 1, 8192), (16, 8, 2048)])
+def test_moe_combine_add_rmsnorm(gpu, T, k, H):
+    torch.manual_seed(H + T)
+    rows = T * k
+    y = torch.randn(rows, H, device=gpu, dtype=bf)
+    inv = torch.randperm(rows, device=gpu).to(torch.int32)
+    inv[0] = -1  # a slot routed to another rank's expert
+    topw = torch.rand(T, k, device=gpu)
+    res = torch.randn(T, H, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    exp_out, exp_res = ref.add_rmsnorm(ops.moe_combine(y, inv, topw), res, nw, 1e-5)
+    r2 = res.clone()
+    out = ops.moe_combine_add_rmsnorm(y, inv, topw, r2, nw, 1e-5)
+    close(r2, exp_res, atol=0, rtol=0)
+    close(out, exp_out, atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 4096, 1024), (3, 8, 2, 4096, 14336), (77, 8, 2, 1024, 512),
                                        (512, 8, 2, 512, 256), (300, 4, 1, 256, 256)])
 def test_moe_pipeline(gpu, T, E, k, H, I):

@@ -87,3 +87,24 @@ def test_prefix_caching_gpu(gpu, cfg):
     outs += eng.generate(prompts[1:], SamplingParams(max_tokens=8, ignore_eos=True))
     assert eng.stats["prefix_hit_tokens"] >= 4 * 96  # 6 full shared pages per later request
     _check_greedy(model, prompts, outs)
+
+
+def test_mixtral_decode_fused_moe_glue(gpu):
+    """hidden 1024: the decode steps take the one-launch MoE dispatch (router GEMV + route +
+    sort + gather) and the combine fused into the residual add + RMSNorm; greedy tokens
+    still follow the dense oracle."""
+    from dataclasses import replace
+
+    cfg = replace(TINY_MIXTRAL, hidden_size=1024, intermediate_size=512)
+    torch.manual_seed(0)
+    model = build_model(cfg, device=gpu, seed=4)
+    x = torch.randn(3, 1024, device=gpu, dtype=torch.bfloat16)
+    from mlopamd import ops
+
+    assert ops.moe_dispatch_small(x, model.layers[0]["router"], 2, 0, cfg.num_experts) is not None
+    eng = Engine(model, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, max_model_len=512,
+                                     num_kv_blocks=64, graph_buckets=(1, 2, 4)))
+    prompts = [torch.randint(2, 500, (n,)).tolist() for n in (5, 33, 70)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=8, ignore_eos=True))
+    assert eng.stats["graph_steps"] > 0
+    _check_greedy(model, prompts, outs)
