@@ -475,6 +475,26 @@ def test_moe_dispatch_small(gpu, T, E, k, H):
         assert torch.equal(src[inv[sel].long()].cpu(), sel.to(torch.int32).cpu())
 
 
+@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (4, 8, 2, 4096), (16, 8, 2, 1024), (3, 8, 2, 8192)])
+def test_moe_dispatch_small_prologue(gpu, T, E, k, H):
+    """Dispatch with the residual add + RMSNorm prologue == add_rmsnorm, then dispatch."""
+    torch.manual_seed(T + H)
+    o = torch.randn(T, H, device=gpu, dtype=bf)
+    res = torch.randn(T, H, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    wr = (0.05 * torch.randn(E, H, device=gpu)).to(bf)
+    x_ref, res_ref = ref.add_rmsnorm(o, res, nw, 1e-5)
+    r2 = res.clone()
+    topw, topi, xp, off, src, inv = ops.moe_dispatch_small(o, wr, k, 0, E, pro=(o, r2, nw, 1e-5))
+    close(r2, res_ref, atol=0, rtol=0)
+    p = torch.softmax(x_ref.float() @ wr.float().t(), -1)
+    w_ref, i_ref = ops.moe_route((x_ref.float() @ wr.float().t()).to(bf), k)
+    close(p.gather(1, topi.long()), p.gather(1, i_ref.long()), atol=2e-3, rtol=2e-3)
+    xp_r, off_r, _, inv_r = ops.moe_permute(x_ref, topi, 0, E)
+    assert torch.equal(off.cpu(), off_r.cpu()) and torch.equal(inv.cpu(), inv_r.cpu())
+    close(xp[:T * k], xp_r[:T * k], atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("T,k,H", [(1, 2, 4096), (9, 2, 4096), (3, 1, 8192), (16, 8, 2048)])
 def test_moe_combine_add_rmsnorm(gpu, T, k, H):
     torch.manual_seed(H + T)
