@@ -195,7 +195,17 @@ _GEMM_CHOICE: dict = {}
 GEMM_BACKEND = os.environ.get("MLOP_GEMM_BACKEND", "auto")  # auto | mlop | hipblaslt
 
 
+_POW2_BUCKETS = os.environ.get("MLOP_GEMM_MBUCKET") == "pow2"  # A/B against the old keys
+
+
 def _mbucket(M: int) -> int:
+    """Autotune key for the row count: powers of two up to 256 (GEMV / narrow-tile
+    regimes), then every 256 rows: above one tile row the winner flips with how the
+    256-row tiles fill the 256 CUs (e.g. QKV at M=2040 is 192 tiles = 3/4 of the chip
+    for the fused RoPE kernel, while hipBLASLt's stream-K does not care), so
+    power-of-two buckets let the first M seen in [1025, 2048] decide for all of them."""
+    if M > 256 and not _POW2_BUCKETS:
+        return (M + 255) // 256 * 256
     b = 1
     while b < M:
         b <<= 1
@@ -216,30 +226,35 @@ def _flush_caches(dev) -> None:
     buf.fill_(1)
 
 
-def _time_candidates(cands, M: int, dev, reps: int = 3) -> dict:
-    """Mean ms per candidate; cold caches before every rep when M is decode-sized."""
+def _time_candidates(cands, M: int, dev, reps: int = 5, rounds: int = 3) -> dict:
+    """ms per call per candidate: cold caches before every rep when M is decode-sized;
+    otherwise the best of ``rounds`` interleaved rounds of ``reps`` back-to-back calls
+    (one 3-call sample per candidate mis-picked QKV at M=2048 by 20-30%: clocks and
+    heuristic warm-up drift between the two candidates' samples)."""
     cold = M <= COLD_TUNE_MAX_M
-    times = {}
+    times = {name: float("inf") for name, _ in cands}
     for name, fn in cands:
         fn()  # warm (kernel selection, lazy init)
-        tot = 0.0
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if cold:
-            for _ in range(reps):
-                _flush_caches(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(1 if cold else rounds):
+        for name, fn in cands:
+            tot = 0.0
+            if cold:
+                for _ in range(reps):
+                    _flush_caches(dev)
+                    s.record()
+                    fn()
+                    e.record()
+                    e.synchronize()
+                    tot += s.elapsed_time(e)
+            else:
                 s.record()
-                fn()
+                for _ in range(reps):
+                    fn()
                 e.record()
                 e.synchronize()
-                tot += s.elapsed_time(e)
-        else:
-            s.record()
-            for _ in range(reps):
-                fn()
-            e.record()
-            e.synchronize()
-            tot = s.elapsed_time(e)
-        times[name] = tot / reps
+                tot = s.elapsed_time(e)
+            times[name] = min(times[name], tot / reps)
     return times
 
 
@@ -534,10 +549,12 @@ def moe_permute(x, topi, e0: int, n_local: int):
     return xp, offsets, src, inv
 
 
-def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int):
+def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int, pro=None):
     """Decode-size MoE dispatch in ONE launch (router GEMV + route + sort + gather, moe.hip):
     returns (topw, topi, xp, offsets, src, inv) or None when the shape is not on this path
-    (more than 16 tokens, CPU tensors)."""
+    (more than 16 tokens, CPU tensors).  ``pro=(y, residual, norm_w, eps)``: x is not given
+    (pass y); the launch first does residual += y, x = rmsnorm(residual) * norm_w.  On None
+    nothing was written."""
     if not x.is_cuda or x.shape[0] > 16:
         return None
     _need_gpu()
@@ -549,8 +566,12 @@ def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int):
     offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
     src = torch.empty(T * top_k, dtype=torch.int32, device=dev)
     inv = torch.empty(T * top_k, dtype=torch.int32, device=dev)
-    if not torch.ops.mlop.moe_dispatch_small(topw, topi, xp, offsets, src, inv, x.contiguous(), router_w,
-                                             e0, n_local):
+    if pro is None:
+        args = (x.contiguous(), router_w, e0, n_local)
+    else:  # x (= y) is only the shape carrier; the kernel writes the normed rows to xn
+        y, residual, norm_w, eps = pro
+        args = (torch.empty_like(y), router_w, e0, n_local, y.contiguous(), residual, norm_w, float(eps))
+    if not torch.ops.mlop.moe_dispatch_small(topw, topi, xp, offsets, src, inv, *args):
         return None
     return topw, topi, xp, offsets, src, inv
 
