@@ -112,6 +112,12 @@ class LlamaModel:
         act = ops.gemm(x, L["gate_up"], epi=ops.EPI_SILU_MUL)
         return ops.gemm_add_rmsnorm(act, L["down"], residual, next_norm, eps)
 
+    def attn_out_mlp(self, i, a, residual, next_norm, eps):
+        """TP=1: O projection with the residual add + post-attention norm in its reduce
+        pass, then the MLP block with the next add + norm in the down projection's."""
+        x = ops.gemm_add_rmsnorm(a, self.layers[i]["o"], residual, self.layers[i]["post_norm"], eps)
+        return self.mlp_add_norm(i, x, residual, next_norm, eps)
+
     # ------------------------------------------------------------ forward --
     def weight_tensors(self):
         yield self.embed
@@ -175,9 +181,7 @@ class LlamaModel:
             a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
             if tp.size == 1:
-                # O projection with the residual add + post-attention norm in its reduce pass
-                x = ops.gemm_add_rmsnorm(a.view(a.shape[0], -1), L["o"], residual, L["post_norm"], eps)
-                x = self.mlp_add_norm(i, x, residual, nxt, eps)
+                x = self.attn_out_mlp(i, a.view(a.shape[0], -1), residual, nxt, eps)
                 continue
             o = linear(a.view(a.shape[0], -1), L["o"])
             tp.all_reduce(o)

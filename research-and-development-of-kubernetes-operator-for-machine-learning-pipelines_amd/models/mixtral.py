@@ -64,6 +64,19 @@ class MixtralModel(LlamaModel):
                                         self.n_local_experts, residual, next_norm, eps)
         return ops.add_rmsnorm(self.mlp(i, x), residual, next_norm, eps)
 
+    def attn_out_mlp(self, i, a, residual, next_norm, eps):
+        """TP = EP = 1 decode sizes: O projection GEMV, then ONE launch for residual add +
+        post-attention RMSNorm + router + route + sort + gather (moe_dispatch_small's
+        prologue), the two grouped GEMMs, and the combine fused into the next add + norm."""
+        if self.ps.ep.size == 1 and a.is_cuda and a.shape[0] <= 16:
+            from ..parallel.moe import moe_forward_add_norm
+
+            L = self.layers[i]
+            o = linear(a, L["o"])
+            return moe_forward_add_norm(None, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.expert_start,
+                                        self.n_local_experts, residual, next_norm, eps, pre=(o, L["post_norm"]))
+        return super().attn_out_mlp(i, a, residual, next_norm, eps)
+
     def forward(self, ids, meta, kv):
         # MoE output is already complete per token (EP combine) -> no TP all-reduce
         # when attention runs TP=1 inside an EP group; the base forward all-reduces

@@ -393,7 +393,8 @@ void moe_permute(Tensor xp, Tensor offsets, Tensor src, Tensor inv, Tensor x, Te
 
 // decode-size dispatch (T <= 16): router GEMV + route + sort + gather in one launch; false = not taken
 bool moe_dispatch_small(Tensor topw, Tensor topi, Tensor xp, Tensor offsets, Tensor src, Tensor inv, Tensor x,
-                        Tensor router_w, int64_t e0, int64_t n_local) {
+                        Tensor router_w, int64_t e0, int64_t n_local, std::optional<Tensor> pro_y,
+                        std::optional<Tensor> pro_res, std::optional<Tensor> pro_w, double pro_eps) {
   check_bf16(xp, "xp"); check_bf16(x, "x"); check_bf16(router_w, "router_w"); check_i32(topi, "topi");
   check_i32(offsets, "offsets"); check_i32(src, "src"); check_i32(inv, "inv");
   TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous(), "topw f32");
@@ -404,10 +405,18 @@ bool moe_dispatch_small(Tensor topw, Tensor topi, Tensor xp, Tensor offsets, Ten
               "topi/topw [T, k], xp [T*k, H]");
   TORCH_CHECK(n_local >= 1 && n_local <= 64 && offsets.numel() == n_local + 1 && src.numel() == T * k &&
                   inv.numel() == T * k, "offsets / src / inv");
+  const bool pro = pro_y.has_value();
+  if (pro) {  // x is the OUTPUT of the prologue here
+    check_bf16(*pro_y, "pro_y"); check_bf16(*pro_res, "pro_res"); check_bf16(*pro_w, "pro_w");
+    TORCH_CHECK(pro_y->numel() == T * H && pro_res->numel() == T * H && pro_w->numel() == H && H <= 8192,
+                "prologue y / residual [T, H], w [H]");
+  }
   c10::DeviceGuard g(x.device());
   mlop::launch_moe_dispatch_small(topw.data_ptr<float>(), topi.data_ptr<int>(), xp.data_ptr(),
                                   offsets.data_ptr<int>(), src.data_ptr<int>(), inv.data_ptr<int>(), x.data_ptr(),
                                   router_w.data_ptr(), (int)T, (int)E, (int)k, (int)H, (int)e0, (int)n_local,
+                                  pro ? pro_y->data_ptr() : nullptr, pro ? pro_res->data_ptr() : nullptr,
+                                  pro ? pro_w->data_ptr() : nullptr, (float)pro_eps, pro ? x.data_ptr() : nullptr,
                                   cur_stream());
   return true;
 }
@@ -547,7 +556,8 @@ TORCH_LIBRARY(mlop, m) {
         "Tensor topi, int e0, int n_local) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor inv, Tensor topw) -> ()");
   m.def("moe_dispatch_small(Tensor(a!) topw, Tensor(b!) topi, Tensor(c!) xp, Tensor(d!) offsets, Tensor(e!) src, "
-        "Tensor(f!) inv, Tensor x, Tensor router_w, int e0, int n_local) -> bool");
+        "Tensor(f!) inv, Tensor(g!) x, Tensor router_w, int e0, int n_local, Tensor? pro_y=None, "
+        "Tensor(h!)? pro_res=None, Tensor? pro_w=None, float pro_eps=0.0) -> bool");
   m.def("moe_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor y, Tensor inv, Tensor topw, "
         "Tensor norm_w, float eps) -> bool");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");

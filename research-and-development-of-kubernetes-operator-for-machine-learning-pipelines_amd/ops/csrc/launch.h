@@ -84,8 +84,10 @@ void launch_moe_combine(void* out, const void* y, const int* inv, const float* t
                         int H, hipStream_t st);
 // decode-size MoE dispatch in one launch: router GEMV + route + sort + gather (moe.hip)
 bool moe_dispatch_small_takes(int T, int E, int k, int H);
+// pro_y != nullptr: prologue residual += pro_y, x = rmsnorm(residual) * pro_w (written to pro_xn)
 void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, int* src, int* inv, const void* x,
-                               const void* wr, int T, int E, int k, int H, int e0, int n_local, hipStream_t st);
+                               const void* wr, int T, int E, int k, int H, int e0, int n_local, const void* pro_y,
+                               void* pro_res, const void* pro_w, float pro_eps, void* pro_xn, hipStream_t st);
 // combine + residual add + RMSNorm in one launch; false = hidden size not instantiated
 bool launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, const int* inv, const float* topw,
                                     const void* w, float eps, int T, int k, int H, hipStream_t st);

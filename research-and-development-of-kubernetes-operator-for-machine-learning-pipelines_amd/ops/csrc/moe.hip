@@ -127,6 +127,16 @@ __global__ void __launch_bounds__(256) moe_combine_kernel(uint16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Optional prologue (MoePro): the post-attention residual add + RMSNorm that produces x, so
+// the O projection's output goes straight into the MoE block (one more launch saved).
+struct MoePro {
+  const uint16_t* y;   // [T, H] O projection output (nullptr: no prologue, x given)
+  uint16_t* residual;  // [T, H] in / out
+  const uint16_t* w;   // [H] post-attention norm weight
+  float eps;
+  uint16_t* xn;        // [T, H] normed x (written)
+};
+
 // Decode-size MoE dispatch in ONE launch (T <= kSmallT tokens): router GEMV (bf16-rounded
 // logits, as the separate router projection stores them), softmax / top-k / renormalise,
 // counting sort by local expert and the row gather.  At batch 1-16 each of the four
@@ -140,12 +150,47 @@ template <int CH>  // 16-B chunks per lane per row: H = CH * 512
 __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_small_kernel(
     float* __restrict__ topw, int* __restrict__ topi, uint16_t* __restrict__ xp, int* __restrict__ offsets,
     int* __restrict__ src, int* __restrict__ inv, const uint16_t* __restrict__ x,
-    const uint16_t* __restrict__ wr, int T, int E, int k, int H, int e0, int n_local) {
+    const uint16_t* __restrict__ wr, int T, int E, int k, int H, int e0, int n_local, MoePro pro) {
   __shared__ float lg[kSmallT][kMaxE];
   __shared__ int s_topi[kSmallT * 8];
   __shared__ int cnt[kMaxE + 1];
   __shared__ int base[kMaxE + 1];
+  __shared__ float red[16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (pro.y != nullptr) {
+    // 0. prologue: residual += y; x = rmsnorm(residual) * w (norm.hip's rounding), x -> pro.xn
+    for (int t = 0; t < T; ++t) {
+      u32x4 r[2];  // H <= 8192: at most two 8-element chunks per thread
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = (threadIdx.x + i * 64 * kDispWaves) * 8;
+        if (c >= H) continue;
+        const u32x4 a = *reinterpret_cast<const u32x4*>(pro.y + (size_t)t * H + c);
+        const u32x4 b = *reinterpret_cast<const u32x4*>(pro.residual + (size_t)t * H + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          r[i][q] = pack2(lo_bf(a[q]) + lo_bf(b[q]), hi_bf(a[q]) + hi_bf(b[q]));
+          ss += lo_bf(r[i][q]) * lo_bf(r[i][q]) + hi_bf(r[i][q]) * hi_bf(r[i][q]);
+        }
+        *reinterpret_cast<u32x4*>(pro.residual + (size_t)t * H + c) = r[i];
+      }
+      const float rs = rsqrtf(block_sum(ss, red) / (float)H + pro.eps);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = (threadIdx.x + i * 64 * kDispWaves) * 8;
+        if (c >= H) continue;
+        const u32x4 wv8 = *reinterpret_cast<const u32x4*>(pro.w + c);
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = pack2(bf2f(f2bf(lo_bf(r[i][q]) * rs)) * lo_bf(wv8[q]), bf2f(f2bf(hi_bf(r[i][q]) * rs)) * hi_bf(wv8[q]));
+        *reinterpret_cast<u32x4*>(pro.xn + (size_t)t * H + c) = o;
+      }
+    }
+    __syncthreads();  // x is read back below by other threads of this workgroup
+    x = pro.xn;
+  }
   // 1. router logits: lg[t][e] = bf16(x[t] . wr[e])
   for (int e = wv; e < E; e += kDispWaves) {
     const uint16_t* we = wr + (size_t)e * H + lane * 8;
@@ -244,11 +289,13 @@ bool moe_dispatch_small_takes(int T, int E, int k, int H) {
 }
 
 void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, int* src, int* inv, const void* x,
-                               const void* wr, int T, int E, int k, int H, int e0, int n_local, hipStream_t st) {
+                               const void* wr, int T, int E, int k, int H, int e0, int n_local, const void* pro_y,
+                               void* pro_res, const void* pro_w, float pro_eps, void* pro_xn, hipStream_t st) {
+  const MoePro pro{(const uint16_t*)pro_y, (uint16_t*)pro_res, (const uint16_t*)pro_w, pro_eps, (uint16_t*)pro_xn};
 #define MLOP_DISP(CH)                                                                                       \
   moe_dispatch_small_kernel<CH><<<1, 64 * kDispWaves, 0, st>>>(topw, topi, (uint16_t*)xp, offsets, src, inv, \
                                                                (const uint16_t*)x, (const uint16_t*)wr, T, E, k, \
-                                                               H, e0, n_local)
+                                                               H, e0, n_local, pro)
   switch (H) {
     case 1024: MLOP_DISP(2); break;
     case 2048: MLOP_DISP(4); break;

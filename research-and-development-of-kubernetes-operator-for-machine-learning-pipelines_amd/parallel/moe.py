@@ -45,11 +45,20 @@ def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None
     return ops.moe_combine(y, inv, topw) if combine else (y, inv)
 
 
-def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int, residual, norm_w, eps: float):
+def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int, residual, norm_w, eps: float,
+                         pre=None):
     """Single-rank MoE block followed by the decoder's residual add + RMSNorm.  At decode
     sizes the router GEMV, routing, sort and gather are ONE launch (moe_dispatch_small) and
-    the weighted combine rides in the add + RMSNorm launch: 6 MoE glue launches -> 2."""
-    d = ops.moe_dispatch_small(x, router_w, top_k, e0, n_local)
+    the weighted combine rides in the add + RMSNorm launch: 6 MoE glue launches -> 2.
+    ``pre=(o, pre_norm_w)``: x is not formed yet; the block's own input add + RMSNorm
+    (residual += o, x = rmsnorm(residual)) becomes the dispatch launch's prologue."""
+    if pre is not None:
+        o, pre_w = pre
+        d = ops.moe_dispatch_small(o, router_w, top_k, e0, n_local, pro=(o, residual, pre_w, eps))
+        if d is None:
+            x = ops.add_rmsnorm(o, residual, pre_w, eps)
+    else:
+        d = ops.moe_dispatch_small(x, router_w, top_k, e0, n_local)
     if d is None:
         topw, topi = route(x, router_w, top_k)
         y, inv = local_experts(x, topw, topi, w13, w2, e0, n_local, combine=False)
