@@ -48,6 +48,21 @@ def _need_gpu():
         load()
 
 
+_SK_READY: set = set()
+
+
+def _sk_reserve(dev) -> None:
+    """Stream-K tail buffers of the ping-pong GEMM (128 MB partials + counters) on this
+    device: allocated once, on the first eager GEMM (never inside a graph capture; until
+    they exist the kernel runs its plain data-parallel grid)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i in _SK_READY or torch.cuda.is_current_stream_capturing():
+        return
+    with torch.cuda.device(i):
+        torch.ops.mlop.gemm_sk_reserve()
+    _SK_READY.add(i)
+
+
 def library_path() -> str:
     return str(_LIB)
 
@@ -175,6 +190,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, epi:
 
 
 def _gemm_mlop(x2, w, o2, epi):
+    _sk_reserve(x2.device)
     M, K = x2.shape
     nws = torch.ops.mlop.gemm_workspace(M, w.shape[0], K, epi)
     ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x2.device) if nws else _EMPTY.get(x2.device)
@@ -343,6 +359,8 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
     M, K = x2.shape
     N = w.shape[0]
     q_out = torch.empty(T, n_q_heads, D, dtype=x.dtype, device=x.device) if q_out is None else q_out
+
+    _sk_reserve(x.device)
 
     def fused():
         if not torch.ops.mlop.gemm_rope_cache(q_out, k_cache, v_cache, x2, w, positions, cos_sin, slots):

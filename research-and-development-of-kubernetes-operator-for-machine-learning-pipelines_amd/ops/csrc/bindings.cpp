@@ -212,6 +212,9 @@ int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_
 int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
+int64_t gemm_sk_mode(int64_t set) { return mlop::gemm_sk_mode((int)set); }
+bool gemm_sk_reserve() { return mlop::gemm_sk_reserve(); }
+int64_t gemm_sk_workgroups(int64_t M, int64_t N, int64_t K) { return mlop::gemm_sk_workgroups((int)M, (int)N, (int)K); }
 
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, (int)epi);
@@ -530,6 +533,9 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
+  m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);
+  m.def("gemm_sk_reserve() -> bool", &gemm_sk_reserve);
+  m.def("gemm_sk_workgroups(int M, int N, int K) -> int", &gemm_sk_workgroups);
   m.def("vmm_supported(int device) -> bool", &vmm_supported);
   m.def("vmm_granularity(int device) -> int", &vmm_granularity);
   m.def("vmm_arena(int bytes, int device) -> Tensor", &vmm_arena);

@@ -392,205 +392,417 @@ int gemm_big_variant(int set) {
 // GROUPED (MoE K13 at >= 512 rows per expert): the (expert, m-tile) slot is the fast
 // tile index (empty slots of the worst-case grid spread over all XCDs), B = W[e] and
 // rows stop at offsets[e+1]; everything else is the dense schedule.
-template <int EPI, bool GROUPED = false>
+// Stream-K tail (plain, non-grouped launches): the T tiles are T / C full rounds on the C
+// CUs plus r = T % C tail tiles, and a tail of r < C whole tiles leaves C - r CUs idle for
+// a whole tile time (gate_up at M = 2040: 896 tiles = 3.5 rounds, 12.5 % of the kernel).
+// The first T - r tiles stay data-parallel (one per workgroup); the r tail tiles' K-tiles
+// are dealt as contiguous ranges of `ipw` K-tiles to n_sk more workgroups.  A workgroup
+// whose range covers only part of a tile writes its fp32 accumulators to its own slot
+// (2 per workgroup: the piece its range starts in, the piece it ends in), releases at
+// agent scope and takes a ticket on the tile's counter; the LAST contributor acquires,
+// adds the other slots and runs the normal epilogue, then resets the counter for the next
+// launch.  Nobody waits on anybody (placement-independent, MI355X_MICROARCH.md
+// "Correctness boundaries": dispatch order and co-residency are not assumed).
+struct SkArgs {
+  int n_dp;     // data-parallel workgroups = tiles before the tail (blockIdx < n_dp)
+  int t0;       // first tail tile (logical tile index)
+  int ipw;      // K-tiles per stream-K workgroup
+  int n_iters;  // r * nk: K-tiles of the whole tail
+  float* ws;    // 2 slots x 256 x 256 fp32 per stream-K workgroup
+  int* cnt;     // one ticket counter per tail tile, zero between launches
+};
+
+// Stream-K workgroup Lb (of n_sk starting at block n0) -> its range index, XCD-contiguous:
+// blocks are dealt to the 8 XCDs round-robin (block & 7), so consecutive ranges -- which walk
+// consecutive tiles and share their A / B panels -- must sit on ONE XCD's L2.  Dealing them
+// round-robin made every XCD fetch nearly all of A and B (QKV at M = 2304: 2x slower).
+__device__ __forceinline__ int sk_index(int Lb, int n0, int n_sk) {
+  const int x = Lb & 7;
+  int before = 0;
+  for (int y = 0; y < x; ++y) {
+    const int first = (y - n0) & 7;  // offset of XCD y's first block in the region
+    before += first < n_sk ? (n_sk - first + 7) / 8 : 0;
+  }
+  return before + (Lb - n0) / 8;
+}
+
+template <int EPI, bool GROUPED = false, bool SK = false>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m,
-    RopeEpi re, const int* __restrict__ offsets, int n_groups) {
+    RopeEpi re, const int* __restrict__ offsets, int n_groups, SkArgs sk) {
   constexpr int BM = 256, BN = 256;
   constexpr int BUF = (BM + BN) * kBK;  // bf16 per K-tile buffer (64 KB)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wid >> 2, wc = wid & 3;
-  const int G = gridDim.x, Lb = blockIdx.x;
-  const int q = G >> 3, rr = G & 7, xcd = Lb & 7, slot = Lb >> 3;
-  const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
-  // tile order inside an XCD's contiguous range: bands of group_m m-tiles, m fastest
-  // within a band (a B panel is reused by group_m consecutive tiles while L2-resident)
-  int m0, n0, m_end = M;
-  if constexpr (GROUPED) {
-    int t = lid % m_tiles, e = 0;
-    n0 = (lid / m_tiles) * BN;
-    for (; e < n_groups; ++e) {
-      const int tiles = (offsets[e + 1] - offsets[e] + BM - 1) / BM;
-      if (t < tiles) break;
-      t -= tiles;
-    }
-    if (e >= n_groups) return;  // whole workgroup, before any barrier
-    m0 = offsets[e] + t * BM;
-    m_end = offsets[e + 1];
-    B += (size_t)e * N * ldb;
-  } else {
+  const int Lb = blockIdx.x;
+  const int nk = K / kBK;
+  const bool dp = !SK || Lb < sk.n_dp;  // SK = false: every workgroup one whole tile
+
+  // tile (logical index) -> origin; bands of group_m m-tiles, m fastest within a band (a B
+  // panel is reused by group_m consecutive tiles while L2-resident)
+  auto tile_origin = [&](int lid, int& m0, int& n0) {
     const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
     const int gm_here = min(group_m, m_tiles - band * group_m);
     m0 = (band * group_m + in_band % gm_here) * BM;
     n0 = (in_band / gm_here) * BN;
+  };
+  // iteration range of this workgroup in K-tiles of the logical tile space
+  int it, it_end;
+  const uint16_t* Bg = B;
+  int m_end = M, m0g = 0, n0g = 0;
+  if (dp) {
+    // XCD-aware remap of the data-parallel part: each XCD a contiguous range of tiles
+    const int G = GROUPED ? (int)gridDim.x : sk.n_dp;
+    const int q = G >> 3, rr = G & 7, xcd = Lb & 7, slot = Lb >> 3;
+    const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+    if constexpr (GROUPED) {
+      int t = lid % m_tiles, e = 0;
+      n0g = (lid / m_tiles) * BN;
+      for (; e < n_groups; ++e) {
+        const int tiles = (offsets[e + 1] - offsets[e] + BM - 1) / BM;
+        if (t < tiles) break;
+        t -= tiles;
+      }
+      if (e >= n_groups) return;  // whole workgroup, before any barrier
+      m0g = offsets[e] + t * BM;
+      m_end = offsets[e + 1];
+      Bg = B + (size_t)e * N * ldb;
+    } else {
+      tile_origin(lid, m0g, n0g);
+    }
+    it = lid * nk;
+    it_end = it + nk;
+  } else {
+    const int s = sk_index(Lb, sk.n_dp, gridDim.x - sk.n_dp);
+    it = sk.t0 * nk + s * sk.ipw;
+    it_end = sk.t0 * nk + min((s + 1) * sk.ipw, sk.n_iters);
   }
-  const int nk = K / kBK;
-
-  // DMA sources: half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127,
-  // 3 B rows 128-255) = 16 pieces of 8 rows x 128 B; wave w moves pieces w, w+8
-  const int prow = lane >> 3;
-  const uint16_t* src[4][2];
-#pragma unroll
-  for (int h = 0; h < 4; ++h)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row inside the 256-row operand tile
-      const int ch = (lane & 7) ^ swz(r);
-      src[h][i] = h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda + ch * 8
-                        : B + (size_t)min(n0 + r, N - 1) * ldb + ch * 8;
-    }
-  auto issue_half = [&](int buf, int h, int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + ((h & 1) * 128 + (wid + 8 * i) * 8) * kBK;
-      __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
-    }
-  };
-  auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
-    const uint16_t* sA = smem + buf * BUF;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = grp * 128 + mi * 64 + i * 16 + (lane & 15);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int ch = kk * 4 + (lane >> 4);
-        fa[i][kk] = *reinterpret_cast<const bf16x8*>(sA + r * kBK + ((ch ^ swz(r)) << 3));
-      }
-    }
-  };
-  auto read_b = [&](int buf, int nj, bf16x8 (&fb)[2][2]) {
-    const uint16_t* sB = smem + buf * BUF + BM * kBK;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = wc * 64 + nj * 32 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int ch = kk * 4 + (lane >> 4);
-        fb[j][kk] = *reinterpret_cast<const bf16x8*>(sB + r * kBK + ((ch ^ swz(r)) << 3));
-      }
-    }
-  };
 
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
-    raw_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    raw_barrier();
-  };
+  const int prow = lane >> 3;
+  bool first_piece = true;
+  do {
+    const int tile = SK ? it / nk : 0;
+    const int k0 = SK ? it - tile * nk : 0, k1 = SK ? min(nk, k0 + (it_end - it)) : nk;
+    it += k1 - k0;
+    int m0 = m0g, n0 = n0g;
+    if (SK && !dp) tile_origin(tile, m0, n0);
+    if (SK && !first_piece) __syncthreads();  // the previous piece's epilogue is done with the LDS
+    first_piece = false;
+    const int nkp = k1 - k0;
 
-  // LDS-DMA schedule (barriers numbered along group 0; group 1 runs one behind):
-  //   A(t+1) -> buffer (t+1)&1 in phase 1 of t   (after the last A reads of t-1 retired)
-  //   B(t+2) -> buffer t&1     in phase 3 of t   (after B1(t), the last B read of t, retired)
-  //   retire B(t+1) in phase 2 of t (vmcnt(4): A(t+1) stays in flight), read B0(t+1) in
-  //   phase 3 of t into the other B0 register set; retire A(t+1) in phase 3 (vmcnt(4):
-  //   B(t+2) stays in flight), read it from phase 0 of t+1.  Every read happens at least
-  //   one barrier after the slower group's retirement; every DMA is issued at least one
-  //   barrier after the last read of its destination retired.  Per phase a wave issues
-  //   8 / 4+4 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
+    // DMA sources: half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127,
+    // 3 B rows 128-255) = 16 pieces of 8 rows x 128 B; wave w moves pieces w, w+8
+    const uint16_t* src[4][2];
 #pragma unroll
-  for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
-  if (nk > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
-  if (nk > 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
-  raw_barrier();
-  bf16x8 fa[4][2], fb1[2][2], fbA[2][2], fbB[2][2];
-  read_b(0, 0, fbA);
-  if (grp == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row inside the 256-row operand tile
+        const int ch = (lane & 7) ^ swz(r);
+        src[h][i] = (h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda
+                           : Bg + (size_t)min(n0 + r, N - 1) * ldb) + k0 * kBK + ch * 8;
+      }
+    auto issue_half = [&](int buf, int h, int kt) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + ((h & 1) * 128 + (wid + 8 * i) * 8) * kBK;
+        __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
+      }
+    };
+    auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
+      const uint16_t* sA = smem + buf * BUF;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = grp * 128 + mi * 64 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int ch = kk * 4 + (lane >> 4);
+          fa[i][kk] = *reinterpret_cast<const bf16x8*>(sA + r * kBK + ((ch ^ swz(r)) << 3));
+        }
+      }
+    };
+    auto read_b = [&](int buf, int nj, bf16x8 (&fb)[2][2]) {
+      const uint16_t* sB = smem + buf * BUF + BM * kBK;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 64 + nj * 32 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int ch = kk * 4 + (lane >> 4);
+          fb[j][kk] = *reinterpret_cast<const bf16x8*>(sB + r * kBK + ((ch ^ swz(r)) << 3));
+        }
+      }
+    };
 
-  auto ktile = [&](int t, bf16x8 (&fb0)[2][2], bf16x8 (&fb0n)[2][2]) {
-    const int cur = t & 1, nxt = cur ^ 1;
-    const bool m1 = t + 1 < nk, m2 = t + 2 < nk;
-    read_a(cur, 0, fa);                                  // phase 0: quadrant (0,0)
-    phase_mma(0, 0, fa, fb0);
-    read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
-    if (m1) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
-    phase_mma(0, 1, fa, fb1);
-    read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
-    if (m1) wait_vmcnt<4>();
-    phase_mma(1, 1, fa, fb1);
-    if (m1) read_b(nxt, 0, fb0n);                        // phase 3: quadrant (1,0)
-    if (m2) {
-      issue_half(cur, 2, t + 2);
-      issue_half(cur, 3, t + 2);
-      wait_vmcnt<4>();
-    } else {
-      wait_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+      raw_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+    };
+
+    // LDS-DMA schedule (barriers numbered along group 0; group 1 runs one behind):
+    //   A(t+1) -> buffer (t+1)&1 in phase 1 of t   (after the last A reads of t-1 retired)
+    //   B(t+2) -> buffer t&1     in phase 3 of t   (after B1(t), the last B read of t, retired)
+    //   retire B(t+1) in phase 2 of t (vmcnt(4): A(t+1) stays in flight), read B0(t+1) in
+    //   phase 3 of t into the other B0 register set; retire A(t+1) in phase 3 (vmcnt(4):
+    //   B(t+2) stays in flight), read it from phase 0 of t+1.  Every read happens at least
+    //   one barrier after the slower group's retirement; every DMA is issued at least one
+    //   barrier after the last read of its destination retired.  Per phase a wave issues
+    //   8 / 4+4 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
+    if (nkp > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
+    if (nkp > 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
+    raw_barrier();
+    bf16x8 fa[4][2], fb1[2][2], fbA[2][2], fbB[2][2];
+    read_b(0, 0, fbA);
+    if (grp == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
+
+    auto ktile = [&](int t, bf16x8 (&fb0)[2][2], bf16x8 (&fb0n)[2][2]) {
+      const int cur = t & 1, nxt = cur ^ 1;
+      const bool m1 = t + 1 < nkp, m2 = t + 2 < nkp;
+      read_a(cur, 0, fa);                                  // phase 0: quadrant (0,0)
+      phase_mma(0, 0, fa, fb0);
+      read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
+      if (m1) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
+      phase_mma(0, 1, fa, fb1);
+      read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
+      if (m1) wait_vmcnt<4>();
+      phase_mma(1, 1, fa, fb1);
+      if (m1) read_b(nxt, 0, fb0n);                        // phase 3: quadrant (1,0)
+      if (m2) {
+        issue_half(cur, 2, t + 2);
+        issue_half(cur, 3, t + 2);
+        wait_vmcnt<4>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      phase_mma(1, 0, fa, fb0);
+    };
+    for (int t = 0; t < nkp; t += 2) {
+      ktile(t, fbA, fbB);
+      if (t + 1 < nkp) ktile(t + 1, fbB, fbA);
     }
-    phase_mma(1, 0, fa, fb0);
-  };
-  for (int t = 0; t < nk; t += 2) {
-    ktile(t, fbA, fbB);
-    if (t + 1 < nk) ktile(t + 1, fbB, fbA);
-  }
-  if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
-  __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
+    if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
+    __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
 
-  if constexpr (EPI == EPI_ROPE) {
-    // stage the whole 256 x 256 bf16 tile (two heads), then rotate / scatter per head
-    constexpr int LDR = BN + 8;
+    if (SK && k1 - k0 != nk) {
+      // stream-K partial tile: slot, ticket, and (last contributor only) the fixup
+      const int s = sk_index(Lb, sk.n_dp, gridDim.x - sk.n_dp), base = sk.t0 * nk;
+      auto slot_of = [&](int w) { return 2 * w + (tile == (base + w * sk.ipw) / nk ? 0 : 1); };
+      const int first_w = (tile * nk - base) / sk.ipw, last_w = (tile * nk + nk - 1 - base) / sk.ipw;
+      // hand-off (MI355X_MICROARCH.md "Valid forms", first table row): 16-B sc1 (write-through)
+      // stores, every storing wave's vmcnt(0), a barrier, ONE lane's agent-scope ticket add;
+      // the workgroup whose add came last loads the other slots with 16-B sc1 loads after a
+      // barrier.  No L2 write-back / invalidate: an agent release here (buffer_wbl2) writes
+      // back every dirty line of the XCD's L2 -- the C tiles of the other workgroups too.
+      constexpr int kSlotBytes = BM * BN * 4;
+      auto slot_rsrc = [&](int w) {
+        return __builtin_amdgcn_make_buffer_rsrc(sk.ws + (size_t)slot_of(w) * (BM * BN), 0, kSlotBytes, 0x00020000);
+      };
+      {
+        const auto rs = slot_rsrc(s);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, tid * 16,
+                                                   (i * 4 + j) * 512 * 16, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        const int t = __hip_atomic_fetch_add(sk.cnt + (tile - sk.t0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == last_w - first_w;
+        if (last) __hip_atomic_store(sk.cnt + (tile - sk.t0), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = last;
+      }
+      __syncthreads();
+      const int last = flag[0];
+      __syncthreads();  // flag read everywhere before the epilogue reuses the LDS
+      if (!last) continue;
+      // deterministic sum: with 2 contributors own + other is exact whichever arrives last;
+      // with 3+ the last one re-reads its own slot and sums every slot in contributor order
+      const bool reload = last_w - first_w >= 2;
+      if (reload) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      for (int w = first_w; w <= last_w; ++w) {
+        if (w == s && !reload) continue;
+        const auto rs = slot_rsrc(w);
+        // 16 loads in flight per batch: one load -> wait -> add at a time is ~1.5 us per
+        // round trip, 48 us per slot (the compiler keeps these loads in program order)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          f32x4 v[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            v[q] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, (g * 16 + q) * 512 * 16, 16 /* sc1 */));
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[(g * 16 + q) / 4][q % 4] += v[q];
+        }
+      }
+    }
+
+    if constexpr (EPI == EPI_ROPE) {
+      // stage the whole 256 x 256 bf16 tile (two heads), then rotate / scatter per head
+      constexpr int LDR = BN + 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = grp * 128 + i * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) smem[row * LDR + wc * 64 + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+        }
+      __syncthreads();
+      const int rows = min(BM, m_end - m0);
+      auto at = [&](int r, int c) { return bf2f(smem[r * LDR + c]); };
+      rope_tile_store<512>(at, n0 / 128, 2, m0, rows, re, tid);
+      continue;
+    }
+    // epilogue: each wave stages its 128 x 64 (or 128 x 32 after SiLU.mul) bf16 tile
+    constexpr int OW = EPI == EPI_NONE ? 64 : 32;
+    constexpr int LD = OW + 8;
+    uint16_t* sC = smem + wid * 128 * LD;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = grp * 128 + i * 16 + 4 * (lane >> 4) + r;
+        const int row = i * 16 + 4 * (lane >> 4) + r;
+        if constexpr (EPI == EPI_NONE) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) smem[row * LDR + wc * 64 + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
-      }
-    __syncthreads();
-    const int rows = min(BM, m_end - m0);
-    auto at = [&](int r, int c) { return bf2f(smem[r * LDR + c]); };
-    rope_tile_store<512>(at, n0 / 128, 2, m0, rows, re, tid);
-    return;
-  }
-  // epilogue: each wave stages its 128 x 64 (or 128 x 32 after SiLU.mul) bf16 tile
-  constexpr int OW = EPI == EPI_NONE ? 64 : 32;
-  constexpr int LD = OW + 8;
-  uint16_t* sC = smem + wid * 128 * LD;
+          for (int j = 0; j < 4; ++j) sC[row * LD + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+        } else {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = i * 16 + 4 * (lane >> 4) + r;
-      if constexpr (EPI == EPI_NONE) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sC[row * LD + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
-      } else {
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
-          sC[row * LD + jp * 16 + (lane & 15)] = f2bf(silu_bf(g) * bf2f(f2bf(u)));
+          for (int jp = 0; jp < 2; ++jp) {
+            const float g = acc[i][2 * jp][r], u = acc[i][2 * jp + 1][r];
+            sC[row * LD + jp * 16 + (lane & 15)] = f2bf(silu_bf(g) * bf2f(f2bf(u)));
+          }
         }
       }
-    }
-  __syncthreads();
-  constexpr int CPR = OW / 8;  // 16-B chunks per staged row
-  const int out_col0 = EPI == EPI_NONE ? n0 + wc * 64 : (n0 + wc * 64) / 2;
-  const int out_n = EPI == EPI_NONE ? N : N / 2;
+    __syncthreads();
+    constexpr int CPR = OW / 8;  // 16-B chunks per staged row
+    const int out_col0 = EPI == EPI_NONE ? n0 + wc * 64 : (n0 + wc * 64) / 2;
+    const int out_n = EPI == EPI_NONE ? N : N / 2;
 #pragma unroll
-  for (int it = 0; it < 128 * CPR / 64; ++it) {
-    const int c = it * 64 + lane;
-    const int row = c / CPR, cc = (c % CPR) * 8;
-    const int gm = m0 + grp * 128 + row, gn = out_col0 + cc;
-    if (gm < m_end && gn < out_n)
-      *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
+    for (int i2 = 0; i2 < 128 * CPR / 64; ++i2) {
+      const int c = i2 * 64 + lane;
+      const int row = c / CPR, cc = (c % CPR) * 8;
+      const int gm = m0 + grp * 128 + row, gn = out_col0 + cc;
+      if (gm < m_end && gn < out_n)
+        *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
+    }
+  } while (SK && it < it_end);
+}
+
+// Stream-K buffers (per device, allocated once outside graph capture by gemm_sk_reserve):
+// 2 partial slots per stream-K workgroup and kCntRegions rotating sets of tail-tile counters,
+// so back-to-back launches never share a counter set while one may still be resetting.
+constexpr int kSkMaxWg = 256, kCntRegions = 64;
+struct SkBuf {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  int next = 0, cus = 0;
+};
+static SkBuf g_sk[16];
+static int g_sk_mode = env_int("MLOP_GEMM_SK", 1);
+static const int g_sk_min_iters = env_int("MLOP_GEMM_SK_MIN_ITERS", 16);
+
+int gemm_sk_mode(int set) {
+  if (set >= 0) g_sk_mode = set;
+  return g_sk_mode;
+}
+
+bool gemm_sk_reserve() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return false;
+  SkBuf& b = g_sk[dev];
+  if (b.ws) return true;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return false;
+  b.cus = std::min(cus, kSkMaxWg);
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  if (hipMalloc((void**)&ws, (size_t)2 * kSkMaxWg * 256 * 256 * sizeof(float)) != hipSuccess) return false;
+  if (hipMalloc((void**)&cnt, (size_t)kCntRegions * kSkMaxWg * sizeof(int)) != hipSuccess) {
+    (void)hipFree(ws);
+    return false;
   }
+  if (hipMemset(cnt, 0, (size_t)kCntRegions * kSkMaxWg * sizeof(int)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(ws);
+    (void)hipFree(cnt);
+    return false;
+  }
+  b.ws = ws;
+  b.cnt = cnt;
+  return true;
+}
+
+// Split of a plain launch's T tiles: n_dp data-parallel workgroups + a stream-K tail
+// (n_sk = 0: no tail).  The r = T % C tail tiles are each cut into d equal K-ranges (d | nk,
+// so no range straddles two tiles), one per extra workgroup, d <= C / r, when the cost model
+// (in K-tile times, calibrated on scripts/bench_proj.py) beats the tail round's nk:
+//   ipw                      the range itself
+//   max(2, w * 0.04)         256 KB fp32 partial per workgroup, HBM-bound when all write
+//   (d - 1 or d) * 2         the last contributor's slot reads (one CU, ~3 us per slot)
+//   1                        a second pipeline fill + ticket
+// Ranges that straddle tiles (general stream-K) were measured slower than the data-parallel
+// grid whenever the tail exceeds half the chip: twice the partial traffic, two fills.
+static SkArgs sk_plan(int T, int nk, int& n_sk) {
+  SkArgs a{T, T, 1, 0, nullptr, nullptr};
+  n_sk = 0;
+  int dev = 0;
+  if (!g_sk_mode || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return a;
+  SkBuf& b = g_sk[dev];
+  if (!b.ws || b.cus <= 0) return a;
+  const int r = T % b.cus;
+  if (r == 0) return a;
+  double best = 0.9 * nk;  // require a 10 % gain on the tail round
+  int best_d = 0;
+  for (int d = 2; d <= std::min(32, b.cus / r); ++d) {
+    if (nk % d || nk / d < std::max(1, g_sk_min_iters / 2)) continue;
+    const int w = r * d;
+    const double cost = nk / d + std::max(2.0, 0.04 * w) + 2.0 * (d >= 3 ? d : d - 1) + 1.0;
+    if (cost < best) {
+      best = cost;
+      best_d = d;
+    }
+  }
+  if (!best_d) return a;
+  a.n_dp = T - r;
+  a.t0 = T - r;
+  a.ipw = nk / best_d;
+  a.n_iters = r * nk;
+  a.ws = b.ws;
+  a.cnt = b.cnt + (size_t)(b.next++ % kCntRegions) * kSkMaxWg;
+  n_sk = r * best_d;
+  return a;
 }
 
 template <int EPI, bool GROUPED = false>
@@ -611,7 +823,21 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   const int gx = (N + 255) / 256, gy = (M + 255) / 256 + (GROUPED ? n_groups : 0);
   static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
   const int gm = std::max(1, std::min(group_m, gy));
-  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups);
+  int n_sk = 0;
+  const SkArgs sk = GROUPED ? SkArgs{gx * gy, gx * gy, 1, 0, nullptr, nullptr} : sk_plan(gx * gy, K / kBK, n_sk);
+  if constexpr (!GROUPED) {
+    if (n_sk > 0) {
+      auto ksk = gemm_pp_kernel<EPI, false, true>;
+      static bool attr_sk = false;
+      if (!attr_sk) {
+        hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_sk = true;
+      }
+      ksk<<<sk.n_dp + n_sk, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
+      return;
+    }
+  }
+  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
 }
 
 struct Plan {
@@ -693,6 +919,16 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
   }
 #undef MLOP_GEMM
+}
+
+// stream-K workgroups a plain launch of this shape would add (0: data-parallel grid only)
+int gemm_sk_workgroups(int M, int N, int K) {
+  if (M <= 0 || gemv_takes(M, N, K, EPI_NONE)) return 0;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  if (p.variant != 3 || p.BN != 256 || p.splits != 1) return 0;
+  int n_sk = 0;
+  sk_plan(((M + 255) / 256) * ((N + 255) / 256), K / kBK, n_sk);
+  return n_sk;
 }
 
 // EPI_ROPE: the plain (no split-K) plan must stage whole heads: BN >= 128, i.e. M > 256

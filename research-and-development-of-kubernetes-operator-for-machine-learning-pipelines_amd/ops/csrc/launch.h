@@ -46,6 +46,11 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
+// stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the
+// per-device partial / counter buffers (allocate once, outside graph capture)
+int gemm_sk_mode(int set);
+bool gemm_sk_reserve();
+int gemm_sk_workgroups(int M, int N, int K);
 // K2 skinny GEMV (gemv.hip): decode projections at M <= 8 (epi 0 none, 1 silu-mul, 3 rope)
 bool gemv_takes(int M, int N, int K, int epi);
 void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,

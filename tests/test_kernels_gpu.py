@@ -82,6 +82,7 @@ def test_qkv_rope_cache_fused(gpu, M, Hq, Hkv):
     D, K, BS = 128, 4096, 16
     N = (Hq + 2 * Hkv) * D
     NB = M // BS + 8
+    ops._sk_reserve(torch.device(gpu))  # M = 2048 / 3000: stream-K tail (192 / 288 tiles)
     cs = rope_table(D, 8192, 5e5, device=gpu)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
@@ -303,6 +304,39 @@ def test_gemm(gpu, M, N, K):
         ops.GEMM_BACKEND = "auto"
     exp = (x.float() @ w.float().t())
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [
+    (2040, 28672, 4096, 1),   # 896 tiles: 768 data-parallel + 128 tail tiles in 2 halves (gate_up, SiLU)
+    (4352, 4096, 14336, 0),   # 272 tiles: 16 tail tiles x 224 K-tiles in 8 ranges (re-read sum path)
+    (3072, 6144, 4096, 0),    # 288 tiles: 32 tail tiles in 4 ranges of 16 K-tiles
+    (2100, 8320, 2048, 0),    # ragged M and N: 297 tiles, 41 tail tiles in 2 halves
+])
+def test_gemm_stream_k(gpu, M, N, K, epi):
+    """Stream-K tail of the ping-pong GEMM (partial tiles through fp32 slots, ticket
+    counters, last-arriver fixup + epilogue): vs fp32 matmul, three launches in a row
+    (the counters re-arm), and against the data-parallel grid of the same kernel."""
+    torch.manual_seed(M + K)
+    ops._sk_reserve(torch.device(gpu))
+    assert torch.ops.mlop.gemm_sk_workgroups(M, N, K) > 0
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
+    exp = x.float() @ w.float().t()
+    if epi:
+        exp = ref.silu_mul(ops.deinterleave_cols(exp.to(bf)))
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        outs = [ops.gemm(x, w, epi=epi) for _ in range(3)]
+        prev = torch.ops.mlop.gemm_sk_mode(-1)
+        torch.ops.mlop.gemm_sk_mode(0)
+        dp = ops.gemm(x, w, epi=epi)
+        torch.ops.mlop.gemm_sk_mode(prev)
+    finally:
+        ops.GEMM_BACKEND = "auto"
+    tol = 3e-2 * exp.abs().max().item() / 10 + 1e-2
+    for y in outs + [dp]:
+        close(y, exp, atol=tol, rtol=2e-2)
+    close(outs[0], outs[2], atol=0, rtol=0)  # deterministic: fixed slot order in the fixup
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8])
