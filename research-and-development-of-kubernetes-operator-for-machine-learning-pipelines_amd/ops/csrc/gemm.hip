@@ -774,34 +774,45 @@ bool gemm_sk_reserve() {
 //   1                        a second pipeline fill + ticket
 // Ranges that straddle tiles (general stream-K) were measured slower than the data-parallel
 // grid whenever the tail exceeds half the chip: twice the partial traffic, two fills.
-static SkArgs sk_plan(int T, int nk, int& n_sk) {
-  SkArgs a{T, T, 1, 0, nullptr, nullptr};
-  n_sk = 0;
-  int dev = 0;
-  if (!g_sk_mode || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return a;
-  SkBuf& b = g_sk[dev];
-  if (!b.ws || b.cus <= 0) return a;
-  const int r = T % b.cus;
-  if (r == 0) return a;
+// d for the r tail tiles of a T-tile launch on `cus` CUs (0: keep the data-parallel grid)
+static int sk_choose_d(int T, int nk, int cus) {
+  const int r = T % cus;
+  if (r == 0) return 0;
   double best = 0.9 * nk;  // require a 10 % gain on the tail round
   int best_d = 0;
-  for (int d = 2; d <= std::min(32, b.cus / r); ++d) {
+  for (int d = 2; d <= std::min(32, cus / r); ++d) {
     if (nk % d || nk / d < std::max(1, g_sk_min_iters / 2)) continue;
-    const int w = r * d;
-    const double cost = nk / d + std::max(2.0, 0.04 * w) + 2.0 * (d >= 3 ? d : d - 1) + 1.0;
+    const double cost = nk / d + std::max(2.0, 0.04 * r * d) + 2.0 * (d >= 3 ? d : d - 1) + 1.0;
     if (cost < best) {
       best = cost;
       best_d = d;
     }
   }
-  if (!best_d) return a;
+  return best_d;
+}
+
+static SkBuf* sk_buf() {
+  int dev = 0;
+  if (!g_sk_mode || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  SkBuf& b = g_sk[dev];
+  return b.ws && b.cus > 0 ? &b : nullptr;
+}
+
+static SkArgs sk_plan(int T, int nk, int& n_sk) {
+  SkArgs a{T, T, 1, 0, nullptr, nullptr};
+  n_sk = 0;
+  SkBuf* b = sk_buf();
+  if (!b) return a;
+  const int d = sk_choose_d(T, nk, b->cus);
+  if (!d) return a;
+  const int r = T % b->cus;
   a.n_dp = T - r;
   a.t0 = T - r;
-  a.ipw = nk / best_d;
+  a.ipw = nk / d;
   a.n_iters = r * nk;
-  a.ws = b.ws;
-  a.cnt = b.cnt + (size_t)(b.next++ % kCntRegions) * kSkMaxWg;
-  n_sk = r * best_d;
+  a.ws = b->ws;
+  a.cnt = b->cnt + (size_t)(b->next++ % kCntRegions) * kSkMaxWg;
+  n_sk = r * d;
   return a;
 }
 
@@ -852,6 +863,12 @@ struct Plan {
 //   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs,
 //   3 (default) = 256x256 two-group ping-pong (gemm_pp_kernel).  (A four-wave 128x128-per-wave
 //   variant was measured 10-20% slower: profiles/r02_gemm_fourwave_rejected.md.)
+// true when the stream-K tail is available here and splits ALL T (<= C / 2) tiles
+static bool sk_halves_ok(long T, int nk) {
+  const SkBuf* b = sk_buf();
+  return b && T * 2 <= b->cus && sk_choose_d((int)T, nk, b->cus) >= 2;
+}
+
 static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {
   Plan p{};
   p.variant = 0;
@@ -872,7 +889,9 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     p.BN = 128;
     static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 192);
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    const bool pp_ok = K % kBK == 0 && t256 >= pp_min_tiles;
+    // below pp_min_tiles the 256x256 grid leaves CUs idle, unless the stream-K tail can cut
+    // every tile in two (T <= C / 2): o / down at M = 2040 (128 tiles)
+    const bool pp_ok = K % kBK == 0 && (t256 >= pp_min_tiles || sk_halves_ok(t256, K / kBK));
     if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
       p.BN = 256;
       p.variant = big;
@@ -885,7 +904,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
   static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 256);  // run49: down -5..-15% at M 8-64
-  if (!grouped && tiles < 160 && K >= 1024) {
+  if (!grouped && tiles < 160 && K >= 1024 && p.variant != 3) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
