@@ -626,5 +626,6 @@ def grouped_gemm(xp, w, offsets, epi: int = EPI_NONE, avg_rows: int | None = Non
     if xp.shape[0] == 0:
         return out
     rows = avg_rows if avg_rows is not None else max(1, xp.shape[0] // max(1, w.shape[0]))
+    _sk_reserve(xp.device)
     torch.ops.mlop.grouped_gemm(out, xp, w, offsets, rows, epi)
     return out

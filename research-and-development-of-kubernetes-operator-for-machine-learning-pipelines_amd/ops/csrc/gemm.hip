@@ -410,7 +410,38 @@ struct SkArgs {
   int n_iters;  // r * nk: K-tiles of the whole tail
   float* ws;    // 2 slots x 256 x 256 fp32 per stream-K workgroup
   int* cnt;     // one ticket counter per tail tile, zero between launches
+  int n_base;   // first stream-K block (grouped: the worst-case tile count of the grid)
+  int cus;      // CUs the split was planned for
+  int min_half; // shortest K-range (K-tiles) the planner may cut
+  int skip_dead;  // 1: quadrants past the last row issue no MFMAs (MLOP_GEMM_SKIP_DEAD=0: A/B)
 };
+
+// d for the r = T % cus tail tiles of a T-tile launch: each is cut into d equal K-ranges
+// (d | nk, so no range straddles two tiles), one per extra workgroup, d <= cus / r, when the
+// cost model (in K-tile times, calibrated on scripts/bench_proj.py) beats the tail round's nk:
+//   nk / d                   the range itself
+//   max(2, 0.04 * r * d)     256 KB fp32 partial per workgroup, HBM-bound when all write
+//   2 * (d - 1, or d)        the last contributor's slot reads (one CU, ~3 us per slot)
+//   1                        a second pipeline fill + ticket
+// 0: keep the data-parallel grid.  Host (plain launches) and device (grouped launches, whose
+// tile count depends on the routing) evaluate the same function.
+__host__ __device__ inline int sk_choose_d(int T, int nk, int cus, int min_half) {
+  const int r = T % cus;
+  if (r == 0) return 0;
+  float best = 0.9f * nk;  // require a 10 % gain on the tail round
+  int best_d = 0;
+  const int dmax = cus / r < 32 ? cus / r : 32;
+  for (int d = 2; d <= dmax; ++d) {
+    if (nk % d || nk / d < min_half) continue;
+    const float w = 0.04f * r * d;
+    const float cost = nk / d + (w > 2.f ? w : 2.f) + 2.f * (d >= 3 ? d : d - 1) + 1.f;
+    if (cost < best) {
+      best = cost;
+      best_d = d;
+    }
+  }
+  return best_d;
+}
 
 // Stream-K workgroup Lb (of n_sk starting at block n0) -> its range index, XCD-contiguous:
 // blocks are dealt to the 8 XCDs round-robin (block & 7), so consecutive ranges -- which walk
@@ -439,46 +470,71 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
   const int grp = wid >> 2, wc = wid & 3;
   const int Lb = blockIdx.x;
   const int nk = K / kBK;
-  const bool dp = !SK || Lb < sk.n_dp;  // SK = false: every workgroup one whole tile
-
-  // tile (logical index) -> origin; bands of group_m m-tiles, m fastest within a band (a B
-  // panel is reused by group_m consecutive tiles while L2-resident)
-  auto tile_origin = [&](int lid, int& m0, int& n0) {
-    const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
-    const int gm_here = min(group_m, m_tiles - band * group_m);
-    m0 = (band * group_m + in_band % gm_here) * BM;
-    n0 = (in_band / gm_here) * BN;
-  };
-  // iteration range of this workgroup in K-tiles of the logical tile space
-  int it, it_end;
-  const uint16_t* Bg = B;
-  int m_end = M, m0g = 0, n0g = 0;
-  if (dp) {
-    // XCD-aware remap of the data-parallel part: each XCD a contiguous range of tiles
-    const int G = GROUPED ? (int)gridDim.x : sk.n_dp;
-    const int q = G >> 3, rr = G & 7, xcd = Lb & 7, slot = Lb >> 3;
-    const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
-    if constexpr (GROUPED) {
-      int t = lid % m_tiles, e = 0;
-      n0g = (lid / m_tiles) * BN;
-      for (; e < n_groups; ++e) {
-        const int tiles = (offsets[e + 1] - offsets[e] + BM - 1) / BM;
-        if (t < tiles) break;
-        t -= tiles;
+  // launch geometry: data-parallel tiles [0, n_dp) on blocks [0, n_base), stream-K ranges
+  // over the tail tiles [t0, T) on blocks [n_base, n_base + n_sk)
+  int n_dp = sk.n_dp, t0 = sk.t0, ipw = sk.ipw, n_iters = sk.n_iters, n_sk = (int)gridDim.x - sk.n_base;
+  int S = 0;  // grouped: (expert, m-tile) slots the routing actually filled
+  if constexpr (GROUPED) {
+    for (int e = 0; e < n_groups; ++e) S += (offsets[e + 1] - offsets[e] + BM - 1) / BM;
+    const int T = S * n_tiles_x;
+    n_dp = T;
+    t0 = T;
+    ipw = 1;
+    n_iters = 0;
+    n_sk = 0;
+    if constexpr (SK) {
+      const int d = sk_choose_d(T, nk, sk.cus, sk.min_half);
+      if (d) {
+        const int r = T % sk.cus;
+        n_dp = t0 = T - r;
+        ipw = nk / d;
+        n_iters = r * nk;
+        n_sk = r * d;
       }
-      if (e >= n_groups) return;  // whole workgroup, before any barrier
-      m0g = offsets[e] + t * BM;
+    }
+  }
+  const bool dp = !SK || Lb < sk.n_base;
+  if (dp ? Lb >= n_dp : Lb - sk.n_base >= n_sk) return;  // whole workgroup, before any barrier
+
+  // tile (logical index) -> origin.  Plain: bands of group_m m-tiles, m fastest within a band
+  // (a B panel is reused by group_m consecutive tiles while L2-resident).  Grouped: the
+  // routed (expert, m-tile) slot is the fast index, rows stop at offsets[e + 1], B = W[e].
+  int m_end = M;
+  const uint16_t* Bg = B;
+  auto tile_origin = [&](int lid, int& m0, int& n0) {
+    if constexpr (GROUPED) {
+      const int slot = lid % S;
+      int e = 0, before = 0;
+      for (; e < n_groups; ++e) {
+        const int c = (offsets[e + 1] - offsets[e] + BM - 1) / BM;
+        if (slot < before + c) break;
+        before += c;
+      }
+      m0 = offsets[e] + (slot - before) * BM;
+      n0 = (lid / S) * BN;
       m_end = offsets[e + 1];
       Bg = B + (size_t)e * N * ldb;
     } else {
-      tile_origin(lid, m0g, n0g);
+      const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
+      const int gm_here = min(group_m, m_tiles - band * group_m);
+      m0 = (band * group_m + in_band % gm_here) * BM;
+      n0 = (in_band / gm_here) * BN;
     }
+  };
+  // iteration range of this workgroup in K-tiles of the logical tile space
+  int it, it_end, m0g = 0, n0g = 0;
+  const int s_idx = dp ? 0 : sk_index(Lb, sk.n_base, n_sk);
+  if (dp) {
+    // XCD-aware remap of the data-parallel part: each XCD a contiguous range of tiles
+    const int G = n_dp;
+    const int q = G >> 3, rr = G & 7, xcd = Lb & 7, slot = Lb >> 3;
+    const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+    tile_origin(lid, m0g, n0g);
     it = lid * nk;
     it_end = it + nk;
   } else {
-    const int s = sk_index(Lb, sk.n_dp, gridDim.x - sk.n_dp);
-    it = sk.t0 * nk + s * sk.ipw;
-    it_end = sk.t0 * nk + min((s + 1) * sk.ipw, sk.n_iters);
+    it = t0 * nk + s_idx * ipw;
+    it_end = t0 * nk + min((s_idx + 1) * ipw, n_iters);
   }
 
   f32x4 acc[8][4];
@@ -542,19 +598,25 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform): the
+    // partner group's MFMAs then run alone on the SIMD.  Ragged M, and above all the last
+    // m-tile of every expert in the grouped (MoE) GEMM, half empty on average.
+    const int rows_here = sk.skip_dead ? m_end - m0 : BM;
     auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
       raw_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
+      if (grp * 128 + mi * 64 < rows_here) {
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-            acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
-      __builtin_amdgcn_s_setprio(0);
+            for (int kk = 0; kk < 2; ++kk)
+              acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       raw_barrier();
     };
@@ -607,9 +669,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
 
     if (SK && k1 - k0 != nk) {
       // stream-K partial tile: slot, ticket, and (last contributor only) the fixup
-      const int s = sk_index(Lb, sk.n_dp, gridDim.x - sk.n_dp), base = sk.t0 * nk;
-      auto slot_of = [&](int w) { return 2 * w + (tile == (base + w * sk.ipw) / nk ? 0 : 1); };
-      const int first_w = (tile * nk - base) / sk.ipw, last_w = (tile * nk + nk - 1 - base) / sk.ipw;
+      const int s = s_idx, base = t0 * nk;
+      auto slot_of = [&](int w) { return 2 * w + (tile == (base + w * ipw) / nk ? 0 : 1); };
+      const int first_w = (tile * nk - base) / ipw, last_w = (tile * nk + nk - 1 - base) / ipw;
       // hand-off (MI355X_MICROARCH.md "Valid forms", first table row): 16-B sc1 (write-through)
       // stores, every storing wave's vmcnt(0), a barrier, ONE lane's agent-scope ticket add;
       // the workgroup whose add came last loads the other slots with 16-B sc1 loads after a
@@ -632,9 +694,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       __syncthreads();
       int* flag = reinterpret_cast<int*>(smem);
       if (tid == 0) {
-        const int t = __hip_atomic_fetch_add(sk.cnt + (tile - sk.t0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int t = __hip_atomic_fetch_add(sk.cnt + (tile - t0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = t == last_w - first_w;
-        if (last) __hip_atomic_store(sk.cnt + (tile - sk.t0), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) __hip_atomic_store(sk.cnt + (tile - t0), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = last;
       }
       __syncthreads();
@@ -732,6 +794,7 @@ struct SkBuf {
 static SkBuf g_sk[16];
 static int g_sk_mode = env_int("MLOP_GEMM_SK", 1);
 static const int g_sk_min_iters = env_int("MLOP_GEMM_SK_MIN_ITERS", 16);
+static const int g_skip_dead = env_int("MLOP_GEMM_SKIP_DEAD", 1);
 
 int gemm_sk_mode(int set) {
   if (set >= 0) g_sk_mode = set;
@@ -774,22 +837,7 @@ bool gemm_sk_reserve() {
 //   1                        a second pipeline fill + ticket
 // Ranges that straddle tiles (general stream-K) were measured slower than the data-parallel
 // grid whenever the tail exceeds half the chip: twice the partial traffic, two fills.
-// d for the r tail tiles of a T-tile launch on `cus` CUs (0: keep the data-parallel grid)
-static int sk_choose_d(int T, int nk, int cus) {
-  const int r = T % cus;
-  if (r == 0) return 0;
-  double best = 0.9 * nk;  // require a 10 % gain on the tail round
-  int best_d = 0;
-  for (int d = 2; d <= std::min(32, cus / r); ++d) {
-    if (nk % d || nk / d < std::max(1, g_sk_min_iters / 2)) continue;
-    const double cost = nk / d + std::max(2.0, 0.04 * r * d) + 2.0 * (d >= 3 ? d : d - 1) + 1.0;
-    if (cost < best) {
-      best = cost;
-      best_d = d;
-    }
-  }
-  return best_d;
-}
+static int sk_min_half() { return std::max(1, g_sk_min_iters / 2); }
 
 static SkBuf* sk_buf() {
   int dev = 0;
@@ -799,11 +847,11 @@ static SkBuf* sk_buf() {
 }
 
 static SkArgs sk_plan(int T, int nk, int& n_sk) {
-  SkArgs a{T, T, 1, 0, nullptr, nullptr};
+  SkArgs a{T, T, 1, 0, nullptr, nullptr, T, 256, sk_min_half(), g_skip_dead};
   n_sk = 0;
   SkBuf* b = sk_buf();
   if (!b) return a;
-  const int d = sk_choose_d(T, nk, b->cus);
+  const int d = sk_choose_d(T, nk, b->cus, sk_min_half());
   if (!d) return a;
   const int r = T % b->cus;
   a.n_dp = T - r;
@@ -812,6 +860,8 @@ static SkArgs sk_plan(int T, int nk, int& n_sk) {
   a.n_iters = r * nk;
   a.ws = b->ws;
   a.cnt = b->cnt + (size_t)(b->next++ % kCntRegions) * kSkMaxWg;
+  a.n_base = a.n_dp;
+  a.cus = b->cus;
   n_sk = r * d;
   return a;
 }
@@ -835,18 +885,30 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
   const int gm = std::max(1, std::min(group_m, gy));
   int n_sk = 0;
-  const SkArgs sk = GROUPED ? SkArgs{gx * gy, gx * gy, 1, 0, nullptr, nullptr} : sk_plan(gx * gy, K / kBK, n_sk);
-  if constexpr (!GROUPED) {
-    if (n_sk > 0) {
-      auto ksk = gemm_pp_kernel<EPI, false, true>;
-      static bool attr_sk = false;
-      if (!attr_sk) {
-        hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_sk = true;
-      }
-      ksk<<<sk.n_dp + n_sk, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
-      return;
+  SkArgs sk = sk_plan(gx * gy, K / kBK, n_sk);
+  if constexpr (GROUPED) {
+    // the routed tile count is only known on device: the grid is the worst case (every
+    // expert's last m-tile partial) plus one stream-K block per CU; the kernel plans the
+    // split from offsets[] with the same sk_choose_d and idles the blocks it does not need
+    SkBuf* b = sk_buf();
+    const int T_max = gx * gy;
+    sk = SkArgs{T_max, T_max, 1, 0, nullptr, nullptr, T_max, 256, sk_min_half(), g_skip_dead};
+    if (b) {
+      sk.ws = b->ws;
+      sk.cnt = b->cnt + (size_t)(b->next++ % kCntRegions) * kSkMaxWg;
+      sk.cus = b->cus;
+      n_sk = b->cus;
     }
+  }
+  if (n_sk > 0) {
+    auto ksk = gemm_pp_kernel<EPI, GROUPED, true>;
+    static bool attr_sk = false;
+    if (!attr_sk) {
+      hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_sk = true;
+    }
+    ksk<<<sk.n_base + n_sk, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
+    return;
   }
   kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
 }
@@ -866,7 +928,7 @@ struct Plan {
 // true when the stream-K tail is available here and splits ALL T (<= C / 2) tiles
 static bool sk_halves_ok(long T, int nk) {
   const SkBuf* b = sk_buf();
-  return b && T * 2 <= b->cus && sk_choose_d((int)T, nk, b->cus) >= 2;
+  return b && T * 2 <= b->cus && sk_choose_d((int)T, nk, b->cus, sk_min_half()) >= 2;
 }
 
 static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_group) {

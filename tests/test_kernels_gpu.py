@@ -461,6 +461,41 @@ def test_grouped_gemm_large_groups(gpu, rows, epi):
         close(y[a:b], r)
 
 
+@pytest.mark.parametrize("counts,epi,N,K", [
+    ([530, 498, 512, 470, 555, 505, 490, 528], 0, 4096, 14336),  # 19 slots x 16 = 304 tiles: 48 tail tiles in 4
+    ([530, 498, 512, 470, 555, 505, 490, 528], 1, 28672, 4096),  # 2128 tiles: 80 tail tiles in 2 halves
+    ([2000, 0, 0, 7, 0, 1500, 300, 281], 0, 4096, 14336),        # empty / tiny experts
+])
+def test_grouped_gemm_stream_k(gpu, counts, epi, N, K):
+    """Mixtral-size grouped GEMM with the stream-K tail planned ON DEVICE from the routed
+    offsets (the host only knows the worst-case grid), three launches in a row, vs fp32
+    per expert and vs the data-parallel grid."""
+    torch.manual_seed(sum(counts) + N)
+    ops._sk_reserve(torch.device(gpu))
+    E = len(counts)
+    off = torch.tensor([0] + list(np.cumsum(counts)), device=gpu, dtype=torch.int32)
+    Mt = int(off[-1])
+    x = torch.randn(Mt, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(E, N, K, device=gpu)).to(bf)
+    ys = [ops.grouped_gemm(x, w, off, epi=epi, avg_rows=Mt // E) for _ in range(3)]
+    prev = torch.ops.mlop.gemm_sk_mode(-1)
+    torch.ops.mlop.gemm_sk_mode(0)
+    try:
+        dp = ops.grouped_gemm(x, w, off, epi=epi, avg_rows=Mt // E)
+    finally:
+        torch.ops.mlop.gemm_sk_mode(prev)
+    for e in range(E):
+        a, b = int(off[e]), int(off[e + 1])
+        if a == b:
+            continue
+        r = (x[a:b].float() @ w[e].float().t())
+        if epi:
+            r = ref.silu_mul(ops.deinterleave_cols(r.to(bf)))
+        for y in ys + [dp]:
+            close(y[a:b], r, atol=3e-2, rtol=3e-2)
+    close(ys[0], ys[2], atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("counts", [[1, 0, 0, 0, 0, 0, 1, 0], [0, 3, 0, 2, 0, 0, 0, 3], [0, 0, 0, 0, 0, 0, 0, 1],
                                     [1, 1, 1, 1, 1, 1, 1, 1]])
 @pytest.mark.parametrize("epi,N,K", [(1, 28672, 4096), (0, 4096, 14336), (1, 1024, 512), (0, 1024, 2048)])
