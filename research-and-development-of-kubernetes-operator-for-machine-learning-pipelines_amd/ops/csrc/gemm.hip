@@ -519,6 +519,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       const int gm_here = min(group_m, m_tiles - band * group_m);
       m0 = (band * group_m + in_band % gm_here) * BM;
       n0 = (in_band / gm_here) * BN;
+      // RoPE epilogue: the V heads (last columns) write their dim-major pages with 2-B
+      // scattered stores and are the slow tiles; walk each band's n-tiles backwards so they
+      // are dispatched in the first round and their CUs take no second tile
+      if constexpr (EPI == EPI_ROPE) n0 = (n_tiles_x - 1) * BN - n0;
     }
   };
   // iteration range of this workgroup in K-tiles of the logical tile space
