@@ -349,8 +349,11 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
 //   K page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ k        (ds_read_b128, 16 keys/group)
 //   V page [128 dims][4 x 8 B]:  chunk c of dim d at c ^ ((d>>3&1)<<1) (ds_read_b64, dims d, d+8)
 // both conflict-free for the fragment reads below.
+#ifndef FLASH_WG_PER_CU
+#define FLASH_WG_PER_CU 3
+#endif
 template <int G>
-__global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
+__global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
@@ -421,44 +424,36 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
     if (pp + 2 < n_pairs) issue((pp + 2) % STAGES, pp + 2);
     const uint16_t* sK = smem + (pp % STAGES) * STAGE;
     const uint16_t* sV = sK + 2 * PAGE;
-    bf16x8 ka[4], kb[4];
+    // S^T = K . Q^T for both column tiles, each K fragment read once and used twice
+    f32x4 sa[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int slot = ((kk * 4 + g4) ^ r) << 3;
-      ka[kk] = *reinterpret_cast<const bf16x8*>(sK + r * kD + slot);
-      kb[kk] = *reinterpret_cast<const bf16x8*>(sK + PAGE + r * kD + slot);
-    }
-    bf16x4 va[8], vb[8];
+      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(sK + r * kD + slot);
+      const bf16x8 kb = *reinterpret_cast<const bf16x8*>(sK + PAGE + r * kD + slot);
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      const int dim = d * 16 + r;
-      const int c8 = (g4 ^ (((dim >> 3) & 1) << 1)) << 2;
-      va[d] = *reinterpret_cast<const bf16x4*>(sV + dim * kBS + c8);
-      vb[d] = *reinterpret_cast<const bf16x4*>(sV + PAGE + dim * kBS + c8);
+      for (int c = 0; c < 2; ++c) {
+        sa[c] = mfma16(ka, qf[c][kk], sa[c]);
+        sb[c] = mfma16(kb, qf[c][kk], sb[c]);
+      }
     }
     const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
     const bool full_pair = pp * 32 + 31 <= wg_min_pos;  // every key of the pair is visible to every row
+    bf16x8 pf[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        sa = mfma16(ka[kk], qf[c][kk], sa);
-        sb = mfma16(kb[kk], qf[c][kk], sb);
-      }
       // running max kept in RAW score units (scale > 0 preserves order); the scale
-      // folds into the exponent's FMA: p = exp2(s*c - m*c).  VALU, not MFMA, bounds
-      // this loop, so the causal mask is applied only on pairs that cross the
-      // workgroup's diagonal (wave-uniform test).
+      // folds into the exponent's FMA: p = exp2(s*c - m*c).  The causal mask is applied
+      // only on pairs that cross the workgroup's diagonal (wave-uniform test).
       float pa[4], pb[4];
       if (full_pair) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { pa[i] = sa[i]; pb[i] = sb[i]; }
+        for (int i = 0; i < 4; ++i) { pa[i] = sa[c][i]; pb[i] = sb[c][i]; }
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          pa[i] = (tokA + i <= pos_r[c]) ? sa[i] : -INFINITY;
-          pb[i] = (tokB + i <= pos_r[c]) ? sb[i] : -INFINITY;
+          pa[i] = (tokA + i <= pos_r[c]) ? sa[c][i] : -INFINITY;
+          pb[i] = (tokB + i <= pos_r[c]) ? sb[c][i] : -INFINITY;
         }
       }
       float mx = fmaxf(fmaxf(fmaxf(pa[0], pa[1]), fmaxf(pa[2], pa[3])),
@@ -470,14 +465,13 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
       m[c] = m_new;
       const float mc = -m_new * scale_log2;
       float rs = 0.f;
-      bf16x8 pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         pa[i] = exp2f(fmaf(pa[i], scale_log2, mc));
         pb[i] = exp2f(fmaf(pb[i], scale_log2, mc));
         rs += pa[i] + pb[i];
-        pf[i] = (short)f2bf(pa[i]);
-        pf[4 + i] = (short)f2bf(pb[i]);
+        pf[c][i] = (short)f2bf(pa[i]);
+        pf[c][4 + i] = (short)f2bf(pb[i]);
       }
       l[c] = l[c] * alpha + rs;
       // rescale O only when some row's running max moved (after the first pairs of a
@@ -486,11 +480,18 @@ __global__ void __launch_bounds__(256, 2) flash_prefill_kernel(
 #pragma unroll
         for (int d = 0; d < 8; ++d) o[c][d] *= alpha;
       }
+    }
+    // O^T += V^T . P^T: one V fragment per 16-dim block, read just in time and used by
+    // both column tiles (8 VGPRs of V live instead of 32: 3 waves per SIMD fit)
 #pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        bf16x8 vf = {va[d][0], va[d][1], va[d][2], va[d][3], vb[d][0], vb[d][1], vb[d][2], vb[d][3]};
-        o[c][d] = mfma16(vf, pf, o[c][d]);
-      }
+    for (int d = 0; d < 8; ++d) {
+      const int dim = d * 16 + r;
+      const int c8 = (g4 ^ (((dim >> 3) & 1) << 1)) << 2;
+      const bf16x4 va = *reinterpret_cast<const bf16x4*>(sV + dim * kBS + c8);
+      const bf16x4 vb = *reinterpret_cast<const bf16x4*>(sV + PAGE + dim * kBS + c8);
+      const bf16x8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
     }
   }
 
