@@ -32,6 +32,11 @@
 
 namespace mlop {
 
+// exp2 as the bare v_exp_f32: exp2f() wraps it in a denormal-range rescale (v_cmp +
+// v_cndmask + v_ldexp per call, a fifth of the flash loop's VALU).  Softmax arguments are
+// <= 0, so results below 2^-126 flushing to 0 changes nothing that survives bf16 P / f32 l.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 constexpr int kD = 128;
 constexpr int kBS = 16;
 constexpr float kNegBig = -1.0e30f;
@@ -143,13 +148,13 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m, mx);
-    const float alpha = exp2f(m - m_new);
+    const float alpha = fast_exp2(m - m_new);
     m = m_new;
     float rs = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      pa[i] = exp2f(pa[i] - m_new);
-      pb[i] = exp2f(pb[i] - m_new);
+      pa[i] = fast_exp2(pa[i] - m_new);
+      pb[i] = fast_exp2(pb[i] - m_new);
       rs += pa[i] + pb[i];
     }
     l = l * alpha + rs;
@@ -365,7 +370,10 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   constexpr int PAGE = kBS * kD;
   __shared__ __attribute__((aligned(16))) uint16_t smem[STAGES * STAGE];
 
-  const int tile = blockIdx.x, kvh = blockIdx.y;
+  // 1-D grid, kv head fastest: blocks are dealt to the 8 XCDs round-robin, so with 8 kv
+  // heads every workgroup of one head runs on ONE XCD and the 64+ q-tiles of a sequence
+  // re-read that head's K/V pages from its L2 instead of from the fabric
+  const int tile = blockIdx.x / Hkv, kvh = blockIdx.x % Hkv;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = ptile_seq[tile], q0 = ptile_q0[tile];
   const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
@@ -406,9 +414,11 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
   const int vdim = wid * 32 + (lane >> 1);
   const int v_off = kvh * PAGE + vdim * kBS + ((((lane & 1) ^ ((vdim >> 3) & 1))) << 3);
-  auto issue = [&](int buf, int pp) {
-    const int pgA = min(max(bt[2 * pp], 0), num_blocks - 1);
-    const int pgB = (2 * pp + 1 < n_pages) ? min(max(bt[2 * pp + 1], 0), num_blocks - 1) : pgA;
+  // page ids of pair pp; the loop reads them one iteration ahead of their DMA, so the
+  // block-table load's latency is not paid in front of every issue
+  auto page_of = [&](int idx) { return idx < n_pages ? min(max(bt[idx], 0), num_blocks - 1) : -1; };
+  auto issue_pages = [&](int buf, int pgA, int pgB) {
+    if (pgB < 0) pgB = pgA;
     uint16_t* base = smem + buf * STAGE + wid * 512;
     __builtin_amdgcn_global_load_lds((const void*)(kc + pgA * page_stride + k_off), (lds_void_t*)(base), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_off), (lds_void_t*)(base + PAGE), 16, 0, 0);
@@ -416,12 +426,17 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     __builtin_amdgcn_global_load_lds((const void*)(vc + pgB * page_stride + v_off), (lds_void_t*)(base + 3 * PAGE), 16, 0, 0);
   };
 
-  issue(0, 0);
-  if (n_pairs > 1) issue(1, 1);
+  issue_pages(0, page_of(0), page_of(1));
+  if (n_pairs > 1) issue_pages(1, page_of(2), page_of(3));
+  int nxtA = page_of(4), nxtB = page_of(5);  // pair 2
   for (int pp = 0; pp < n_pairs; ++pp) {
     if (pp + 1 < n_pairs) wait_vmcnt<4>(); else wait_vmcnt<0>();
     raw_barrier();  // pair pp visible to every wave; buffer (pp-1)%3 free
-    if (pp + 2 < n_pairs) issue((pp + 2) % STAGES, pp + 2);
+    if (pp + 2 < n_pairs) {
+      issue_pages((pp + 2) % STAGES, nxtA, nxtB);
+      nxtA = page_of(2 * pp + 6);
+      nxtB = page_of(2 * pp + 7);
+    }
     const uint16_t* sK = smem + (pp % STAGES) * STAGE;
     const uint16_t* sV = sK + 2 * PAGE;
     // S^T = K . Q^T for both column tiles, each K fragment read once and used twice
@@ -461,14 +476,14 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m[c], mx);
-      const float alpha = exp2f((m[c] - m_new) * scale_log2);
+      const float alpha = fast_exp2((m[c] - m_new) * scale_log2);
       m[c] = m_new;
       const float mc = -m_new * scale_log2;
       float rs = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        pa[i] = exp2f(fmaf(pa[i], scale_log2, mc));
-        pb[i] = exp2f(fmaf(pb[i], scale_log2, mc));
+        pa[i] = fast_exp2(fmaf(pa[i], scale_log2, mc));
+        pb[i] = fast_exp2(fmaf(pb[i], scale_log2, mc));
         rs += pa[i] + pb[i];
         pf[c][i] = (short)f2bf(pa[i]);
         pf[c][4 + i] = (short)f2bf(pb[i]);
@@ -487,11 +502,15 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     for (int d = 0; d < 8; ++d) {
       const int dim = d * 16 + r;
       const int c8 = (g4 ^ (((dim >> 3) & 1) << 1)) << 2;
-      const bf16x4 va = *reinterpret_cast<const bf16x4*>(sV + dim * kBS + c8);
-      const bf16x4 vb = *reinterpret_cast<const bf16x4*>(sV + PAGE + dim * kBS + c8);
-      const bf16x8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+      // the two 8-B halves (page A keys, page B keys) land in the fragment's halves directly
+      union {
+        bf16x8 v8;
+        u32x2 h[2];
+      } vf;
+      vf.h[0] = *reinterpret_cast<const u32x2*>(sV + dim * kBS + c8);
+      vf.h[1] = *reinterpret_cast<const u32x2*>(sV + PAGE + dim * kBS + c8);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
+      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf.v8, pf[c], o[c][d]);
     }
   }
 
@@ -520,7 +539,7 @@ void launch_flash_prefill(void* out, const void* q, const void* kc, const void* 
                           const int* q_start, const int* q_len, const int* ctx_len, int num_ptiles,
                           int Hq, int Hkv, float scale_log2, int num_blocks, hipStream_t st) {
   if (num_ptiles == 0) return;
-  dim3 grid(num_ptiles, Hkv);
+  dim3 grid(num_ptiles * Hkv);
 #define MLOP_FLASH_CASE(GG)                                                                       \
   case GG:                                                                                        \
     flash_prefill_kernel<GG><<<grid, 256, 0, st>>>(                                              \
