@@ -411,7 +411,10 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   const size_t page_stride = (size_t)Hkv * PAGE;
   // this lane's DMA source offsets inside a page (wave w moves piece w of each page)
   const int kkey = wid * 4 + (lane >> 4);
+  // page B's K image is swizzled with an extra ^4: the permuted row order below reads keys
+  // {0-3, 8-11} (or {4-7, 12-15}) of BOTH pages in one 16-lane group, all 16 slots distinct
   const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
+  const int k_offB = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15) ^ 4) << 3);
   const int vdim = wid * 32 + (lane >> 1);
   const int v_off = kvh * PAGE + vdim * kBS + ((((lane & 1) ^ ((vdim >> 3) & 1))) << 3);
   // page ids of pair pp; the loop reads them one iteration ahead of their DMA, so the
@@ -421,7 +424,7 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     if (pgB < 0) pgB = pgA;
     uint16_t* base = smem + buf * STAGE + wid * 512;
     __builtin_amdgcn_global_load_lds((const void*)(kc + pgA * page_stride + k_off), (lds_void_t*)(base), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_off), (lds_void_t*)(base + PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_offB), (lds_void_t*)(base + PAGE), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(vc + pgA * page_stride + v_off), (lds_void_t*)(base + 2 * PAGE), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(vc + pgB * page_stride + v_off), (lds_void_t*)(base + 3 * PAGE), 16, 0, 0);
   };
@@ -443,16 +446,21 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     f32x4 sa[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const int slot = ((kk * 4 + g4) ^ r) << 3;
-      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(sK + r * kD + slot);
-      const bf16x8 kb = *reinterpret_cast<const bf16x8*>(sK + PAGE + r * kD + slot);
+      // decode kernel's token order: MFMA row r of the first product is pair token
+      // 8(r>>2) + (r&3), of the second that + 4, so lane group g4 ends up owning the 8
+      // consecutive tokens 8g4..8g4+7 and its V^T fragment is one 16-B LDS read
+      const int ch = kk * 4 + g4;
+      const uint16_t* kp = sK + (r >> 3) * PAGE;
+      const int key_a = 8 * ((r >> 2) & 1) + (r & 3), key_b = key_a + 4, pb4 = (r >> 3) << 2;
+      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kp + key_a * kD + ((ch ^ key_a ^ pb4) << 3));
+      const bf16x8 kb = *reinterpret_cast<const bf16x8*>(kp + key_b * kD + ((ch ^ key_b ^ pb4) << 3));
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         sa[c] = mfma16(ka, qf[c][kk], sa[c]);
         sb[c] = mfma16(kb, qf[c][kk], sb[c]);
       }
     }
-    const int tokA = pp * 32 + g4 * 4, tokB = tokA + 16;
+    const int tokA = pp * 32 + g4 * 8, tokB = tokA + 4;
     const bool full_pair = pp * 32 + 31 <= wg_min_pos;  // every key of the pair is visible to every row
     bf16x8 pf[2];
 #pragma unroll
@@ -501,16 +509,11 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
       const int dim = d * 16 + r;
-      const int c8 = (g4 ^ (((dim >> 3) & 1) << 1)) << 2;
-      // the two 8-B halves (page A keys, page B keys) land in the fragment's halves directly
-      union {
-        bf16x8 v8;
-        u32x2 h[2];
-      } vf;
-      vf.h[0] = *reinterpret_cast<const u32x2*>(sV + dim * kBS + c8);
-      vf.h[1] = *reinterpret_cast<const u32x2*>(sV + PAGE + dim * kBS + c8);
+      const int c8 = ((2 * (g4 & 1)) ^ (((dim >> 3) & 1) << 1)) << 2;
+      // tokens 8g4..8g4+7 = page g4>>1, 8-B chunks 2(g4&1), +1 (swizzled pair stays adjacent)
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sV + (g4 >> 1) * PAGE + dim * kBS + c8);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf.v8, pf[c], o[c][d]);
+      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
     }
   }
 
