@@ -112,6 +112,21 @@ class KVCache:
                                              self.n_chunks - self._first, True):
             raise RuntimeError("KV arena: could not start the background backing thread")
         self._filling = True
+        self._fill_t0 = time.perf_counter()
+
+    def wait_ready(self, timeout_s: float = 300.0) -> dict:
+        """Block until every page is backed (a lazy arena's background fill is done).
+        Returns {"kv_fill_wait_ms": time spent here, "kv_fill_ms": fill start -> full}."""
+        t0 = time.perf_counter()
+        while self.ready_blocks() < self.num_blocks:
+            if time.perf_counter() - t0 > timeout_s:
+                raise TimeoutError(f"KV arena: {self.ready_blocks()} of {self.num_blocks} pages backed "
+                                   f"after {timeout_s:.0f} s")
+            time.sleep(0.005)
+        t1 = time.perf_counter()
+        start = getattr(self, "_fill_t0", None)
+        return {"kv_fill_wait_ms": int(1e3 * (t1 - t0)),
+                "kv_fill_ms": int(1e3 * (t1 - start)) if start is not None else 0}
 
     def ready_blocks(self) -> int:
         """Page ids [0, ready_blocks()) are backed and zeroed (all of them when eager)."""
