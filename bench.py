@@ -63,6 +63,8 @@ def parse(argv=None):
                     help="the first N prompt tokens are the same for every request (a system prompt): "
                          "exercises the prefix cache; 0 = fully random prompts (the headline)")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--tune-in-timed", action="store_true",
+                    help="keep timing first-seen GEMM shapes during the timed steps (default: frozen after warmup)")
     ap.add_argument("--save-gemm-table", default=None,
                     help="after the run, write the per-shape GEMM backend choices measured here to this JSON")
     ap.add_argument("--tp", type=int, default=1,
@@ -159,6 +161,12 @@ def main(argv=None):
         ramp += 1
     deploy_info["ramp_steps"] = ramp
     run_steps(a.warmup)
+    if not a.tune_in_timed:
+        # shapes first seen from here on take the nearest tuned row count's GEMM backend
+        # instead of being timed inside the measured steps
+        from mlopamd import ops as _ops
+
+        _ops.freeze_autotune()
     engine.sync_point()  # device sync + world barrier (TP workers join it)
     s0 = dict(engine.stats)
     t_start = time.perf_counter()
