@@ -1107,13 +1107,40 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
     launch_gemv_grouped(A, B, C, offsets, n_groups, M, N, K, epi, st);
     return;
   }
-  const Plan p = plan(M, N, K, true, n_groups, max_rows);
+  Plan p = plan(M, N, K, true, n_groups, max_rows);
+  // Mid-size MoE batches (a few dozen rows per expert): one m-tile per expert x N/64 tiles
+  // is too few workgroups to stream every expert's weights at full rate (down at batch 64:
+  // 512 workgroups of K = 14336, 4.7 TB/s).  Split K like the dense path, partials in the
+  // stream-K slab buffer (same stream, so never in use by another launch), then the reduce
+  // kernel applies the epilogue.  Routed tiles are estimated as one m-tile per expert.
+  float* ws = nullptr;
+  if (p.variant != 3 && K >= 2048) {
+    const SkBuf* b = sk_buf();
+    const long t_est = (long)((N + p.BN - 1) / p.BN) * std::max(1, std::min(n_groups, (M + p.BM - 1) / p.BM + n_groups));
+    static const int target = env_int("MLOP_GROUPED_SPLIT_TARGET", 1024);
+    int s = (int)std::min<long>(8, std::max<long>(1, target / std::max<long>(1, t_est)));
+    while (s > 1 && (K / s) % kBK) --s;
+    if (b && s > 1 && (size_t)s * M * N * 4 <= (size_t)2 * kSkMaxWg * 256 * 256 * 4) {
+      p.splits = s;
+      p.k_chunk = K / s;
+      ws = b->ws;
+    }
+  }
   if (epi == EPI_NONE)
     launch_plan<EPI_NONE, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N,
-                                nullptr, M, N, K, offsets, n_groups, st);
+                                ws, M, N, K, offsets, n_groups, st);
   else
     launch_plan<EPI_SILU_MUL, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C,
-                                    N / 2, nullptr, M, N, K, offsets, n_groups, st);
+                                    N / 2, ws, M, N, K, offsets, n_groups, st);
+  if (p.splits > 1) {
+    const int outw = epi == EPI_NONE ? N : N / 2;
+    const long total = (long)M * (outw / 8);
+    const int g = (int)std::min<long>((total + 255) / 256, 4096);
+    if (epi == EPI_NONE)
+      splitk_reduce_kernel<EPI_NONE><<<g, 256, 0, st>>>((uint16_t*)C, N, ws, M, N, p.splits);
+    else
+      splitk_reduce_kernel<EPI_SILU_MUL><<<g, 256, 0, st>>>((uint16_t*)C, N / 2, ws, M, N, p.splits);
+  }
 }
 
 }  // namespace mlop

@@ -465,6 +465,8 @@ def test_grouped_gemm_large_groups(gpu, rows, epi):
     ([530, 498, 512, 470, 555, 505, 490, 528], 0, 4096, 14336),  # 19 slots x 16 = 304 tiles: 48 tail tiles in 4
     ([530, 498, 512, 470, 555, 505, 490, 528], 1, 28672, 4096),  # 2128 tiles: 80 tail tiles in 2 halves
     ([2000, 0, 0, 7, 0, 1500, 300, 281], 0, 4096, 14336),        # empty / tiny experts
+    ([16, 17, 15, 16, 16, 18, 14, 16], 0, 4096, 14336),           # mid-size batch: split-K grouped (reduce)
+    ([16, 16, 0, 30, 16, 10, 16, 24], 1, 28672, 4096),            # ... with the SiLU-mul epilogue in the reduce
 ])
 def test_grouped_gemm_stream_k(gpu, counts, epi, N, K):
     """Mixtral-size grouped GEMM with the stream-K tail planned ON DEVICE from the routed
