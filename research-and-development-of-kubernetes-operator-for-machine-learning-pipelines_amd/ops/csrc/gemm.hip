@@ -140,7 +140,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed; the STAGES-2 younger stages may stay in flight
-    if (STAGES == 3 && kt + 1 < nk) wait_vmcnt<PPW>(); else wait_vmcnt<0>();
+    // the STAGES-2 younger stages may stay in flight (fewer near the end: drain)
+    if (STAGES >= 3 && kt + STAGES - 2 < nk) wait_vmcnt<(STAGES >= 3 ? (STAGES - 2) * PPW : 0)>();
+    else wait_vmcnt<0>();
     raw_barrier();  // stage kt visible to all waves; stage kt-1's buffer free
     if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
     const uint16_t* sA = smem + (kt % STAGES) * STAGE;
@@ -361,6 +363,12 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
+}
+
+static int g_small_stages = env_int("MLOP_GEMM_SMALL_STAGES", 3);
+int gemm_small_stages(int set) {
+  if (set >= 0) g_small_stages = set;
+  return g_small_stages;
 }
 
 // large-M kernel choice (plan() variants below); MLOP_GEMM_BIG_VARIANT at load, and
@@ -970,7 +978,8 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
   static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 256);  // run49: down -5..-15% at M 8-64
-  if (!grouped && tiles < 160 && K >= 1024 && p.variant != 3) {
+  static const int split_max_tiles = env_int("MLOP_GEMM_SPLIT_MAX_TILES", 160);
+  if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
@@ -993,7 +1002,11 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
   } else {
-    if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
+    // weight-streaming tiles (M <= 128): a deeper LDS-DMA ring keeps more weight bytes in
+    // flight per CU (3 stages x 16 KB per workgroup streamed gate_up at 4.7 TB/s at M = 64)
+    if (p.BM == 64 && g_small_stages >= 6) MLOP_GEMM(64, 64, 1, 4, 6, false);
+    else if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
+    else if (p.BM == 128 && g_small_stages >= 5) MLOP_GEMM(128, 64, 2, 2, 5, false);
     else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
     else if (p.BN == 64) MLOP_GEMM(256, 64, 4, 2, 3, false);
     else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
