@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import collections
 import itertools
+import operator
 import time
 from dataclasses import dataclass, field
 from enum import Enum
@@ -236,7 +237,12 @@ class Engine:
         self.r_nblk = np.zeros(R, np.int64)     # KV pages held
         self.r_sid = np.zeros(R, np.int64)
         self.r_random = np.zeros(R, bool)       # non-greedy sampling
+        # rows of ``self.running`` in order, and their output lists (kept in step with the
+        # list: appended rows go to ``_rows_add``, finished rows are masked out in
+        # ``_decode_finish``, a preempted one popped off the end; anything else sets dirty)
         self._rows = np.zeros(0, np.int32)
+        self._outs: list[list] = []
+        self._rows_add: list[int] = []
         self._rows_dirty = True
         self.sampler = Sampler(self.device, cfg.seed)
         self.waiting: collections.deque[Sequence] = collections.deque()
@@ -297,6 +303,7 @@ class Engine:
         for lst in (self.prefilling, self.running):
             if seq in lst:
                 lst.remove(seq)
+        self._rows_dirty = True
         if seq in self.waiting:
             self.waiting.remove(seq)
         self._finish(seq, "abort")
@@ -335,12 +342,11 @@ class Engine:
             self.free_rows.append(seq.row)
             seq.row = -1
         seq.num_cached = 0
-        self._rows_dirty = True
 
     def _params_of_running(self):
         """Sampling params of the decode batch; a falsy ``any_random`` lets the sampler
         take the all-greedy fast path without a per-sequence Python scan."""
-        lst = _ParamsList(s.params for s in self.running) if self.r_random[self._rows].any() else _ALL_GREEDY
+        lst = _ParamsList(s.params for s in self.running) if self.r_random[self._sync_rows()].any() else _ALL_GREEDY
         return lst
 
     def _register_running(self, s: Sequence):
@@ -349,7 +355,7 @@ class Engine:
         self.r_len[r], self.r_gen[r], self.r_maxgen[r] = s.length, len(s.output), p.max_tokens
         self.r_last[r] = s.output[-1] if s.output else s.prompt[-1]
         self.r_ignore[r], self.r_hasstop[r], self.r_sid[r] = p.ignore_eos, bool(p.stop_token_ids), s.seq_id
-        self._rows_dirty = True
+        self._rows_add.append(r)  # s was just appended to self.running
 
     def _finish(self, seq: Sequence, reason: str):
         seq.status = Status.FINISHED
@@ -564,21 +570,47 @@ class Engine:
         crossing a page boundary allocate (vectorised test, Python only for those
         few); on exhaustion the newest sequence is preempted."""
         while True:
-            if self._rows_dirty:
-                self._rows = np.fromiter((s.row for s in self.running), dtype=np.int32, count=len(self.running))
-                self._rows_dirty = False
-            rows = self._rows
+            rows = self._sync_rows()
             ctx = self.r_len[rows]
-            need = np.nonzero((ctx + BLOCK_SIZE - 1) // BLOCK_SIZE > self.r_nblk[rows])[0]
+            nblk = self.r_nblk[rows]
+            want = (ctx + BLOCK_SIZE - 1) // BLOCK_SIZE
+            need = np.nonzero(want > nblk)[0]
+            if len(need) and self.alloc.can_allocate(len(need)) and (want[need] - nblk[need] == 1).all():
+                # the steady-state case, vectorised: each crossing row takes exactly one page
+                new = self.alloc.allocate(len(need))
+                r = rows[need]
+                self.meta.bt_h[r, nblk[need]] = new
+                self.r_nblk[r] += 1
+                run = self.running
+                collections.deque(map(list.append, [run[i].blocks for i in need.tolist()], new), maxlen=0)
+                return rows, ctx
             ok = True
             for i in need.tolist():
                 s = self.running[i]
                 if not self._ensure_blocks(s, s.length):
                     self._preempt(self.running.pop())  # newest goes back to the queue
+                    self._rows = self._rows[:-1]
+                    self._outs.pop()
                     ok = False
                     break
             if ok:
                 return rows, ctx
+
+    def _sync_rows(self) -> np.ndarray:
+        """``self._rows`` brought in step with ``self.running`` (O(appended) per step; a
+        full rebuild only after an out-of-band change such as an abort)."""
+        if self._rows_dirty:
+            run = self.running
+            self._rows = np.fromiter((s.row for s in run), dtype=np.int32, count=len(run))
+            self._outs = [s.output for s in run]
+            self._rows_add.clear()
+            self._rows_dirty = False
+        elif self._rows_add:
+            n = len(self._rows_add)
+            self._rows = np.concatenate([self._rows, np.asarray(self._rows_add, dtype=np.int32)])
+            self._outs.extend(s.output for s in self.running[-n:])
+            self._rows_add.clear()
+        return self._rows
 
     def _decode_step(self):
         t0 = time.perf_counter()
@@ -626,8 +658,8 @@ class Engine:
             if int(toks[i]) in run[i].params.stop_token_ids:
                 fin_stop[i] = True
         fin = fin_stop | fin_len
-        for s, t in zip(run, toks.tolist()):
-            s.output.append(t)
+        # one token onto every running sequence's output list, at C speed
+        collections.deque(map(list.append, self._outs, toks.tolist()), maxlen=0)
         sids = self.r_sid[rows].copy()
         reasons = {}
         fi = np.nonzero(fin)[0]
@@ -635,9 +667,15 @@ class Engine:
             done = [run[i] for i in fi.tolist()]
             for i, s in zip(fi.tolist(), done):
                 reasons[s.seq_id] = "stop" if fin_stop[i] else "length"
-            dset = set(id(s) for s in done)
-            self.running = [s for s in run if id(s) not in dset]
-            self._rows_dirty = True
+            keep = np.nonzero(~fin)[0]
+            if len(keep) == 0:
+                self.running, self._outs = [], []
+            elif len(keep) == 1:
+                self.running, self._outs = [run[keep[0]]], [self._outs[keep[0]]]
+            else:
+                get = operator.itemgetter(*keep.tolist())
+                self.running, self._outs = list(get(run)), list(get(self._outs))
+            self._rows = rows[keep]
             for s in done:
                 self._finish(s, reasons[s.seq_id])
         return StepBatch(sids, toks, fin, reasons)
