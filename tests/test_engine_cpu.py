@@ -260,3 +260,42 @@ def test_prefix_cache_survives_preemption():
     for p, o in zip(prompts, outs):
         assert o == greedy_ref(m, p, 40)
     assert eng.alloc.num_free == eng.alloc.available - 1  # every reference returned
+
+
+@pytest.mark.parametrize("mixed", [True, False])
+def test_running_rows_bookkeeping_randomized(tiny, mixed):
+    """The decode hot path keeps ``running``'s rows / output lists in step incrementally
+    (appends, masked finishes, preemption pops; aborts force a rebuild).  Under random
+    arrivals, aborts, stop tokens and a KV pool small enough to preempt, after every step
+    the incremental state must equal a rebuild, and every sequence that ran to completion
+    must still match the dense greedy oracle."""
+    rng = np.random.default_rng(7)
+    eng = Engine(tiny, EngineConfig(max_num_seqs=6, max_num_batched_tokens=48, max_model_len=256,
+                                    num_kv_blocks=12, use_graphs=False, mixed_prefill=mixed,
+                                    mixed_min_chunk=8, enable_prefix_caching=False))
+    seqs = []
+    for it in range(160):
+        if rng.random() < 0.35 and len(seqs) < 24:
+            p = rng.integers(2, 500, size=int(rng.integers(3, 40))).tolist()
+            stop = [int(rng.integers(2, 500))] if rng.random() < 0.3 else []
+            seqs.append(eng.add_request(p, SamplingParams(max_tokens=int(rng.integers(2, 40)), ignore_eos=True,
+                                                          stop_token_ids=stop)))
+        if rng.random() < 0.04:
+            live = [s for s in seqs if s.status != Status.FINISHED]
+            if live:
+                eng.abort(live[int(rng.integers(len(live)))].seq_id)
+        if eng.has_work():
+            eng.step()
+        rows = eng._sync_rows()
+        assert rows.tolist() == [s.row for s in eng.running]
+        assert len(eng._outs) == len(eng.running)
+        assert all(o is s.output for o, s in zip(eng._outs, eng.running))
+    while eng.has_work():
+        eng.step()
+    assert eng.stats["preemptions"] > 0
+    done = [s for s in seqs if s.finish_reason in ("length", "stop")]
+    assert len(done) >= 8
+    for s in done[:8]:
+        ref = greedy_ref(tiny, s.prompt, len(s.output))
+        assert s.output == ref
+    assert eng.alloc.num_free == eng.alloc.num_blocks - 1
