@@ -109,14 +109,22 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
         return single()
     world, rank = dist.get_world_size(), dist.get_rank()
     assert world % tp_size == 0, f"world {world} not divisible by tp {tp_size}"
-    tp_handle = None
-    for start in range(0, world, tp_size):
-        ranks = list(range(start, start + tp_size))
-        h = dist.new_group(ranks) if tp_size < world else None
-        if rank in ranks:
-            tp_handle = h
+    assert world % ep_size == 0, f"world {world} not divisible by ep {ep_size}"
+
+    def groups(size):  # consecutive blocks of `size` ranks; every rank creates every group
+        mine = None
+        for start in range(0, world, size):
+            ranks = list(range(start, start + size))
+            h = dist.new_group(ranks) if size < world else None
+            if rank in ranks:
+                mine = h
+        return mine
+
+    tp_handle = groups(tp_size)
     tp = Group(rank=rank % tp_size, size=tp_size, handle=tp_handle)
-    ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=tp_handle)
+    # EP over the TP ranks (tokens replicated by TP attention, partial MoE outputs summed by
+    # the TP all-reduce) or over its own block of ranks (all-to-all dispatch / combine)
+    ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=groups(ep_size))
     car_env = os.environ.get("MLOP_CUSTOM_AR", "1")
     backend_ok = dist.get_backend(tp_handle) == "nccl" or car_env == "force"  # force: gloo + GPU tests
     if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() and backend_ok and car_env != "0":

@@ -115,11 +115,9 @@ def ep_alltoall(rank, world):
     w13 = 0.1 * torch.randn(E, 2 * I, H)
     w2 = 0.1 * torch.randn(E, H, I)
     xs = [torch.randn(7, H), torch.randn(5, H)]  # different token counts per rank
-    ps = make_parallel_state(tp_size=1, ep_size=1)
-    from mlopamd.parallel.comm import Group
-    import torch.distributed as dist
-
-    ep = Group(rank=rank, size=world, handle=None)
+    ps = make_parallel_state(tp_size=1, ep_size=world)  # DP attention + EP MoE layout
+    ep = ps.ep
+    assert ps.tp.size == 1 and ep.size == world and ep.rank == rank
     nl = E // world
     out = moe_forward(xs[rank], router, w13[rank * nl:(rank + 1) * nl], w2[rank * nl:(rank + 1) * nl], k, ep,
                       rank * nl, nl, mode="alltoall")
