@@ -79,6 +79,13 @@ LLAMA3_70B = ModelConfig(
     name="llama3-70b", vocab_size=128256, hidden_size=8192, intermediate_size=28672,
     num_layers=80, num_heads=64, num_kv_heads=8, rope_theta=500000.0, max_position=8192)
 
+# Llama-3.1: same shapes, 128k context through the "llama3" RoPE frequency scaling
+# (public HF config.json of meta-llama/Llama-3.1-8B / -70B)
+_LLAMA31_ROPE = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                 "original_max_position_embeddings": 8192}
+LLAMA31_8B = replace(LLAMA3_8B, name="llama3.1-8b", max_position=131072, rope_scaling=_LLAMA31_ROPE)
+LLAMA31_70B = replace(LLAMA3_70B, name="llama3.1-70b", max_position=131072, rope_scaling=_LLAMA31_ROPE)
+
 MIXTRAL_8X7B = ModelConfig(
     name="mixtral-8x7b", vocab_size=32000, hidden_size=4096, intermediate_size=14336,
     num_layers=32, num_heads=32, num_kv_heads=8, rope_theta=1e6, max_position=32768,
@@ -93,11 +100,14 @@ TINY_MIXTRAL = ModelConfig(
     name="tiny-mixtral", vocab_size=512, hidden_size=256, intermediate_size=256, num_layers=2,
     num_heads=4, num_kv_heads=1, max_position=2048, num_experts=4, top_k=2, eos_token_id=1)
 
-PRESETS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL)}
+PRESETS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, LLAMA31_8B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA,
+                                TINY_MIXTRAL)}
 # accepted aliases (MLflow tags / CR annotations use HF-ish names)
 ALIASES = {
     "meta-llama/Meta-Llama-3-8B": "llama3-8b", "llama-3-8b": "llama3-8b", "Llama-3-8B": "llama3-8b",
     "meta-llama/Meta-Llama-3-70B": "llama3-70b", "llama-3-70b": "llama3-70b", "Llama-3-70B": "llama3-70b",
+    "meta-llama/Llama-3.1-8B": "llama3.1-8b", "meta-llama/Meta-Llama-3.1-8B": "llama3.1-8b",
+    "meta-llama/Llama-3.1-70B": "llama3.1-70b", "meta-llama/Meta-Llama-3.1-70B": "llama3.1-70b",
     "mistralai/Mixtral-8x7B-v0.1": "mixtral-8x7b", "Mixtral-8x7B": "mixtral-8x7b",
 }
 
