@@ -17,7 +17,8 @@ import torch
 
 from . import reference as ref
 
-_LIB = Path(__file__).resolve().parent / "_C.so"
+# MLOP_LIB: load another build of the extension (in-process A/B of two kernel builds on one box)
+_LIB = Path(os.environ.get("MLOP_LIB") or Path(__file__).resolve().parent / "_C.so")
 _loaded = False
 
 
