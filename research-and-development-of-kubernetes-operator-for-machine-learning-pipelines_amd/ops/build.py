@@ -52,6 +52,14 @@ def _newer(target: Path, deps) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+# Per-file code-generation flags.  attention: no NaN operands assumed (the masks use -inf,
+# which stays honoured), so fmaxf on MFMA results needs no canonicalising v_max first: -16 of
+# the flash-prefill loop's ~215 VALU instructions per 32-key step (the loop is VALU-issue
+# bound, profiles/r02_flash_prefill.md).  NaN scores give unspecified (not NaN-propagating)
+# attention outputs.
+FILE_FLAGS = {"attention": ["-fno-honor-nans"]}
+
+
 def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -69,9 +77,9 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     jobs_list = []
     for src in kernels:
         obj = BUILD / (src.stem + ".o")
-        if force or _newer(obj, [src, *headers]):
+        if force or _newer(obj, [src, *headers, Path(__file__)]):
             cmd = [hipcc, *common, f"--offload-arch={ARCH}", "-ffp-contract=fast",
-                   "-c", str(src), "-o", str(obj)]
+                   *FILE_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)]
             jobs_list.append(cmd)
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "bindings.o"

@@ -145,8 +145,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       pb[i] = (tb < p_end && tb <= pos_r) ? sb[i] * scale_log2 : -INFINITY;
       mx = fmaxf(mx, fmaxf(pa[i], pb[i]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_x16_x32(mx);
     const float m_new = fmaxf(m, mx);
     const float alpha = fast_exp2(m - m_new);
     m = m_new;
@@ -171,8 +170,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     }
   }
 
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = sum_x16_x32(l);
   // O^T[d][row]: lane holds row r, dims 16*dblk + 4*g4 + i
 #pragma unroll
   for (int d = 0; d < 8; ++d)
@@ -481,8 +479,7 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
       }
       float mx = fmaxf(fmaxf(fmaxf(pa[0], pa[1]), fmaxf(pa[2], pa[3])),
                        fmaxf(fmaxf(pb[0], pb[1]), fmaxf(pb[2], pb[3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = max_x16_x32(mx);
       const float m_new = fmaxf(m[c], mx);
       const float alpha = fast_exp2((m[c] - m_new) * scale_log2);
       m[c] = m_new;
@@ -520,8 +517,7 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     float L = l[c];
-    L += __shfl_xor(L, 16, 64);
-    L += __shfl_xor(L, 32, 64);
+    L = sum_x16_x32(L);
     const int R = 32 * wid + 16 * c + r;
     const int qi = q0 + R / G;
     if (qi >= ql) continue;

@@ -50,16 +50,50 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// Cross-lane all-reduces without the LDS: __shfl_xor lowers to ds_bpermute_b32 (an LDS
+// round trip, ~50+ cycles on the reduction's critical path per step).  Here the steps
+// inside a 16-lane row are DPP operand modifiers (quad_perm [1,0,3,2] / [2,3,0,1],
+// row_half_mirror, row_mirror: each pairs every lane with one from the other half of its
+// group), and the 16- / 32-lane steps are gfx950's v_permlane16/32_swap.  Each step
+// combines x with its partner's y while the partner combines y with x: commutative ops give
+// every lane bit-identical results.
+namespace detail {
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+}  // namespace detail
+
+// sum / max over lane groups {l, l^16, l^32, l^48} (the 4 lane groups of an MFMA fragment
+// column).  The swap leaves (self, partner) in (r[0], r[1]) on one side and (partner, self) on
+// the other, so combining r[0] with r[1] needs no lane select.
+__device__ __forceinline__ float sum_x16_x32(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_x16_x32(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += detail::dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += detail::dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += detail::dpp<0x141>(v);  // row_half_mirror: lane i <-> 7-i (the other quad)
+  v += detail::dpp<0x140>(v);  // row_mirror: lane i <-> 15-i (the other 8 lanes)
+  return sum_x16_x32(v);
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, detail::dpp<0xB1>(v));
+  v = fmaxf(v, detail::dpp<0x4E>(v));
+  v = fmaxf(v, detail::dpp<0x141>(v));
+  v = fmaxf(v, detail::dpp<0x140>(v));
+  return max_x16_x32(v);
 }
 
 // Block-wide sum; `scratch` needs blockDim.x/64 floats. Result valid in all threads.
