@@ -27,6 +27,8 @@
 //
 // REQUIREMENT: the cache is zero-initialised at allocation (masked lanes multiply
 // p = 0 with whatever the unused slots hold; NaN garbage would poison O).
+#include <type_traits>
+
 #include "common.h"
 #include "launch.h"
 
@@ -430,15 +432,18 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   issue_pages(0, page_of(0), page_of(1));
   if (n_pairs > 1) issue_pages(1, page_of(2), page_of(3));
   int nxtA = page_of(4), nxtB = page_of(5);  // pair 2
-  for (int pp = 0; pp < n_pairs; ++pp) {
+  // one pair through ring slot ST (= pp % STAGES, a template constant: the slot's LDS offset
+  // becomes the ds_read immediate instead of a per-read VALU add)
+  auto pair_step = [&](auto st_tag, int pp) {
+    constexpr int ST = decltype(st_tag)::value;
     if (pp + 1 < n_pairs) wait_vmcnt<4>(); else wait_vmcnt<0>();
     raw_barrier();  // pair pp visible to every wave; buffer (pp-1)%3 free
     if (pp + 2 < n_pairs) {
-      issue_pages((pp + 2) % STAGES, nxtA, nxtB);
+      issue_pages((ST + 2) % STAGES, nxtA, nxtB);
       nxtA = page_of(2 * pp + 6);
       nxtB = page_of(2 * pp + 7);
     }
-    const uint16_t* sK = smem + (pp % STAGES) * STAGE;
+    const uint16_t* sK = smem + ST * STAGE;
     const uint16_t* sV = sK + 2 * PAGE;
     // S^T = K . Q^T for both column tiles, each K fragment read once and used twice
     f32x4 sa[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -512,6 +517,11 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
 #pragma unroll
       for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
     }
+  };
+  for (int pp = 0; pp < n_pairs; pp += STAGES) {
+    pair_step(std::integral_constant<int, 0>{}, pp);
+    if (pp + 1 < n_pairs) pair_step(std::integral_constant<int, 1>{}, pp + 1);
+    if (pp + 2 < n_pairs) pair_step(std::integral_constant<int, 2>{}, pp + 2);
   }
 
 #pragma unroll
