@@ -1055,6 +1055,10 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {
   if (gemv_takes(M, N, K, epi)) return 0;
+  if (wsg_takes(M, N, K, epi)) {  // slabs for split-K, or one fp32 tile for the fused add + RMSNorm
+    const int s = wsg_splits(M, N, K, epi);
+    return (epi == EPI_NONE || s > 1) ? (long)s * M * N : 0;
+  }
   const Plan p = plan(M, N, K, false, 0, 0);
   return p.splits > 1 ? (long)p.splits * M * N : 0;
 }
@@ -1064,6 +1068,18 @@ void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ld
   if (M == 0) return;
   if (gemv_takes(M, N, K, epi) && lda % 8 == 0 && ldb % 8 == 0) {
     launch_gemv(A, lda, B, ldb, C, ldc, M, N, K, epi, st);
+    return;
+  }
+  if (wsg_takes(M, N, K, epi) && lda % 8 == 0 && ldb % 8 == 0) {
+    int s = wsg_splits(M, N, K, epi);
+    if (s > 1 && (long)s * M * N > ws_floats) s = 1;
+    s = launch_wsg(A, lda, B, ldb, C, ldc, s > 1 ? ws : nullptr, M, N, K, epi, s, st);
+    if (s > 1) {
+      const int outw = epi == EPI_NONE ? N : N / 2;
+      const int g = (int)std::min<long>(((long)M * (outw / 8) + 255) / 256, 4096);
+      if (epi == EPI_NONE) splitk_reduce_kernel<EPI_NONE><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, s);
+      else splitk_reduce_kernel<EPI_SILU_MUL><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, s);
+    }
     return;
   }
   Plan p = plan(M, N, K, false, 0, 0);
@@ -1093,10 +1109,18 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              int K, hipStream_t st) {
   if (M == 0) return true;
   if (gemv_takes(M, N, K, EPI_NONE)) return false;  // GEMV + add_rmsnorm
-  const Plan p = plan(M, N, K, false, 0, 0);
-  if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
-  launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
-                               M, N, K, nullptr, 0, st);
+  int splits;
+  if (wsg_takes(M, N, K, EPI_NONE) && lda % 8 == 0) {  // fp32 slab(s) even without a K split
+    splits = wsg_splits(M, N, K, EPI_NONE);
+    if ((long)splits * M * N > ws_floats || N % 8) return false;
+    splits = launch_wsg(A, lda, B, K, nullptr, N, ws, M, N, K, EPI_NONE, splits, st);
+  } else {
+    const Plan p = plan(M, N, K, false, 0, 0);
+    if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
+    launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
+                                 M, N, K, nullptr, 0, st);
+    splits = p.splits;
+  }
   const int nvec = N / 8;
   int vpt = 1;
   while (vpt < 8 && nvec / vpt > 512) vpt <<= 1;
@@ -1105,10 +1129,10 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
   auto* r = (uint16_t*)residual;
   auto* wv = (const uint16_t*)w;
   switch (vpt) {
-    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
-    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
-    case 4: splitk_add_rmsnorm_kernel<4><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
-    default: splitk_add_rmsnorm_kernel<8><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, p.splits); break;
+    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, splits); break;
+    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, splits); break;
+    case 4: splitk_add_rmsnorm_kernel<4><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, splits); break;
+    default: splitk_add_rmsnorm_kernel<8><<<M, threads, 0, st>>>(o, r, ws, wv, eps, M, N, splits); break;
   }
   return true;
 }

@@ -66,6 +66,12 @@ struct NormPro {
   const uint16_t* w;
   float eps;
 };
+// K2' weight-streaming MFMA GEMM (wsgemm.hip): decode projections above the GEMV's rows, M <= 64
+bool wsg_takes(int M, int N, int K, int epi);
+int wsg_splits(int M, int N, int K, int epi);
+int launch_wsg(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws, int M, int N,
+               int K, int epi, int splits, hipStream_t st);
+int wsg_config(int max_m, int min_wg);  // set >= 0 overrides; returns max_m (0 = off)
 bool gemv_norm_takes(int M, int N, int K, int epi);
 bool gemv_grouped_takes(int M, int N, int K, int epi);
 void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,

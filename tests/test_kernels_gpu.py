@@ -343,7 +343,7 @@ def test_gemm_stream_k(gpu, M, N, K, epi):
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1280, 8192), (8192, 1024),
                                  (8192, 3584), (16, 1024)])
 def test_gemv(gpu, M, N, K):
-    """K2 skinny GEMV (gemv.hip, M <= 4; M = 5 / 8 take the MFMA tiles): wave-per-row-pair
+    """K2 skinny GEMV (gemv.hip, M <= 4; M = 5 / 8 take wsgemm.hip or the MFMA tiles): wave-per-row-pair
     (N >= 4096) and the 4-waves-split-K form (N = 1280 / 16: 70B TP=8 shards, tiny N), K
     not a multiple of the unrolled stride (1024, 3584); vs fp32 matmul."""
     torch.manual_seed(M * 7 + N + K)
@@ -356,6 +356,60 @@ def test_gemv(gpu, M, N, K):
     torch.ops.mlop.gemm(y, x, w, torch.empty(max(nws, 0), device=gpu), 0)
     exp = x.float() @ w.float().t()
     close(y, exp, atol=2e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [5, 8, 16, 17, 32, 40, 64])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (28672, 4096, 1),
+                                     (1280, 8192, 0)])
+@pytest.mark.parametrize("min_wg", [1, 256, 4096])  # no K split / the default / forced slabs
+def test_wsg_gemm(gpu, M, N, K, epi, min_wg):
+    """K2' weight-streaming MFMA GEMM (wsgemm.hip, 4 < M <= 64): register-streamed B fragments,
+    4 waves interleaving K steps with an LDS sum, optional K split into fp32 slabs reduced by
+    gemm.hip (plain / SiLU-mul epilogue); ragged M (17, 40: clamped A rows); vs fp32 matmul."""
+    torch.manual_seed(M * 13 + N + K + epi)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    if epi:
+        g = (0.05 * torch.randn(N // 2, K, device=gpu)).to(bf)
+        u = (0.05 * torch.randn(N // 2, K, device=gpu)).to(bf)
+        w = ops.interleave_gate_up(g, u)
+        exp = ref.silu_mul((x.float() @ torch.cat([g, u]).float().t()).to(bf))
+    else:
+        w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
+        exp = x.float() @ w.float().t()
+    prev = torch.ops.mlop.gemm_wsg_config()  # off by default (rejected on speed); forced on here
+    torch.ops.mlop.gemm_wsg_config(64, min_wg)
+    try:
+        y = torch.empty(M, N // 2 if epi else N, device=gpu, dtype=bf)
+        nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
+        torch.ops.mlop.gemm(y, x, w, torch.full((max(nws, 1),), float("nan"), device=gpu), epi)
+    finally:
+        torch.ops.mlop.gemm_wsg_config(prev, 256)
+    close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [8, 24, 64])
+@pytest.mark.parametrize("min_wg", [1, 256])
+def test_wsg_gemm_add_rmsnorm(gpu, M, min_wg):
+    """wsgemm's fp32 slab(s) (one split included) feeding the fused residual add + RMSNorm reduce."""
+    N, K = 4096, 4096
+    torch.manual_seed(M)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    res = torch.randn(M, N, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
+    exp_out, exp_res = ref.add_rmsnorm((x.float() @ w.float().t()).to(bf), res, nw, 1e-5)
+    prev = torch.ops.mlop.gemm_wsg_config()
+    torch.ops.mlop.gemm_wsg_config(64, min_wg)
+    try:
+        nws = torch.ops.mlop.gemm_workspace(M, N, K, 0)
+        assert nws >= M * N
+        out = torch.empty(M, N, device=gpu, dtype=bf)
+        r2 = res.clone()
+        assert torch.ops.mlop.gemm_add_rmsnorm(out, r2, x, w, nw, torch.empty(nws, device=gpu), 1e-5)
+    finally:
+        torch.ops.mlop.gemm_wsg_config(prev, 256)
+    close(r2, exp_res, atol=3e-2, rtol=2e-2)
+    close(out, exp_out, atol=5e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("M", [1, 2, 4])
