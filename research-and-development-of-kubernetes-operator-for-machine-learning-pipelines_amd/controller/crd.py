@@ -36,6 +36,7 @@ EV_ROLLBACK_COMPLETE = "RollbackComplete"
 EV_PREDICTOR_READY = "PredictorReady"
 EV_PREDICTOR_UNAVAILABLE = "PredictorUnavailable"
 EV_REGISTRY_UNAVAILABLE = "RegistryUnavailable"
+EV_METRICS_UNAVAILABLE = "MetricsUnavailable"
 
 
 @dataclass(frozen=True)

@@ -1,6 +1,8 @@
 """Prometheus side of the canary gate (reference C9/C11, mlflow_operator.py:363-460).
 
-* ``PromClient`` — async ``/api/v1/query`` client (replaces prometheus_api_client).
+* ``PromClient`` — async ``/api/v1/query`` client (replaces prometheus_api_client); a
+  backend that cannot answer raises ``MetricsUnavailable`` (the reference's client raised
+  too and its handler crashed; here the canary pauses, see reconciler.canary_tick).
 * ``get_model_metrics`` — the reference's SIX PromQL queries, verbatim shapes,
   per predictor: p95 latency, error count, error rate, mean latency, request
   count, feedback count.
@@ -138,6 +140,12 @@ def should_promote(new: dict, old: dict, thresholds: dict, error_rate_floor: flo
 
 # ------------------------------------------------------------ client --
 
+class MetricsUnavailable(Exception):
+    """The metrics backend could not answer (unreachable, timeout, HTTP / query error).
+    Distinct from an answer with no samples: the canary pauses on this instead of counting
+    a failed gate attempt (a monitoring outage must not roll back a healthy version)."""
+
+
 class PromClient:
     def __init__(self, url: str, timeout_s: float = 10.0):
         self.url = url.rstrip("/")
@@ -155,10 +163,11 @@ class PromClient:
         try:
             async with self._session.get(f"{self.url}/api/v1/query", params=params) as r:
                 d = await r.json(content_type=None)
-        except Exception:  # noqa: BLE001 - unreachable Prometheus = no data (gate fails safe)
-            return []
-        if d.get("status") != "success":
-            return []
+        except Exception as e:  # noqa: BLE001 - transport / timeout / non-JSON body
+            raise MetricsUnavailable(f"{type(e).__name__}: {e}"[:300]) from e
+        if not isinstance(d, dict) or d.get("status") != "success":
+            err = d.get("error") if isinstance(d, dict) else None
+            raise MetricsUnavailable(f"query failed: {err or d!r}"[:300])
         res = d["data"]["result"]
         if d["data"].get("resultType") == "scalar":
             return [{"metric": {}, "value": res}]

@@ -27,13 +27,13 @@ import logging
 
 from . import seldon
 from .crd import (EV_ALIAS_NOT_FOUND, EV_NEW_VERSION, EV_PREDICTOR_READY, EV_PREDICTOR_UNAVAILABLE,
-                  EV_PROMOTION_COMPLETE, EV_PROMOTION_FAILED, EV_REGISTRY_UNAVAILABLE, EV_ROLLBACK_COMPLETE,
+                  EV_METRICS_UNAVAILABLE, EV_PROMOTION_COMPLETE, EV_PROMOTION_FAILED, EV_REGISTRY_UNAVAILABLE, EV_ROLLBACK_COMPLETE,
                   EV_TRAFFIC_INCREASE, GROUP, PLURAL, SELDON_GROUP, SELDON_PLURAL, SELDON_VERSION,
                   VERSION, ModelSpec, OperatorSettings, artifact_uri)
 from .kube import ApiError
 from .mlflow import NotFound, RegistryError, RegistryUnavailable
 from .placement import plan
-from .prometheus import get_model_metrics, gpu_guard_queries, should_promote
+from .prometheus import MetricsUnavailable, get_model_metrics, gpu_guard_queries, should_promote
 
 PH_DEPLOYING, PH_READY, PH_CANARY = "Deploying", "Ready", "Canary"
 PH_PROMOTED, PH_ROLLED_BACK, PH_FAILED, PH_NO_ALIAS = "Promoted", "RolledBack", "PromotionFailed", "AliasNotFound"
@@ -163,6 +163,12 @@ class MlflowModelReconciler:
                     if e.status == 404:  # CR deleted (reference crashed here)
                         return
                     logger.warning("[%s/%s] reconcile error: %s", ns, name, e)
+                    wait = min(spec.monitoring_interval, 10.0)
+                except asyncio.CancelledError:
+                    raise
+                except Exception:  # noqa: BLE001 - any other failure retries (kopf's handler
+                    # retry); it must not end this CR's daemon for good
+                    logger.exception("[%s/%s] unexpected reconcile error; retrying", ns, name)
                     wait = min(spec.monitoring_interval, 10.0)
                 await self._sleep_or_kick(wait, kick)
         finally:
@@ -307,10 +313,24 @@ class MlflowModelReconciler:
         if now < next_at:
             return next_at - now
         guards = pol.gpu_guards or {}
-        new_m = await get_model_metrics(self.prom, name, pc, ns, pol.window_s,
-                                        extra_queries=guards and gpu_guard_queries(name, pc, ns, pol.window_s))
-        old_m = await get_model_metrics(self.prom, name, pp, ns, pol.window_s,
-                                        extra_queries=guards and gpu_guard_queries(name, pp, ns, pol.window_s))
+        try:
+            new_m = await get_model_metrics(self.prom, name, pc, ns, pol.window_s,
+                                            extra_queries=guards and gpu_guard_queries(name, pc, ns, pol.window_s))
+            old_m = await get_model_metrics(self.prom, name, pp, ns, pol.window_s,
+                                            extra_queries=guards and gpu_guard_queries(name, pp, ns, pol.window_s))
+        except MetricsUnavailable as e:
+            # the metrics backend is down: hold the split, do not count an attempt (the
+            # reference's sync client raised here and its handler died mid-canary)
+            if status.get("metricsUnavailable") != "True":
+                status["metricsUnavailable"] = "True"
+                body = await self._patch_status(ns, name, {"metricsUnavailable": "True"})
+                logger.warning("[%s/%s] metrics backend unavailable, canary paused: %s", ns, name, e)
+                await self.op.event(body, "Warning", EV_METRICS_UNAVAILABLE,
+                                    f"Prometheus unavailable, canary paused at {status.get('canaryTraffic')}%: {e}"[:1000])
+            return pol.attempt_delay_s
+        if status.get("metricsUnavailable") == "True":
+            status["metricsUnavailable"] = None
+            await self._patch_status(ns, name, {"metricsUnavailable": None})
         logger.info("[%s/%s] Metrics for new model (version %s): %s", ns, name, cur, new_m)
         logger.info("[%s/%s] Metrics for old model (version %s): %s", ns, name, prev, old_m)
         gate = should_promote(new_m, old_m, pol.thresholds, pol.error_rate_floor, logger=logger,

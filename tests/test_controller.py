@@ -18,7 +18,7 @@ from mlopamd.controller.crd import (GROUP, PLURAL, SELDON_GROUP, SELDON_PLURAL, 
 from mlopamd.controller.kube import FakeKube
 from mlopamd.controller.local import FakeSeldonController, SimLauncher, mlflow_model_cr
 from mlopamd.controller.mlflow import LocalMlflowClient, SqliteRegistry
-from mlopamd.controller.prometheus import LocalProm, MetricStore
+from mlopamd.controller.prometheus import LocalProm, MetricStore, MetricsUnavailable
 
 NS = "models"
 
@@ -260,6 +260,57 @@ def test_registry_outage_keeps_serving():
         env.reg.fail_mode = None
         await env.clock.sleep(120)
         assert "registryUnavailable" not in await env.status()
+        await env.stop()
+    run(go())
+
+
+class _FlakyProm:
+    """LocalProm that raises MetricsUnavailable while ``down`` (Prometheus outage)."""
+
+    def __init__(self, inner):
+        self.inner, self.down, self.calls = inner, False, 0
+
+    async def query(self, q, at=None):
+        self.calls += 1
+        if self.down:
+            raise MetricsUnavailable("connection refused")
+        return await self.inner.query(q, at)
+
+    async def close(self):
+        pass
+
+
+def test_metrics_outage_pauses_canary_without_rollback():
+    """A Prometheus outage longer than the gate's 10 attempts x 10 s must not roll back a
+    healthy canary (missing data from a live backend still counts as a failed attempt):
+    the split holds, one MetricsUnavailable Warning, then promotion resumes."""
+    async def go():
+        env = Env(profiles={"1": {"latency": 0.05}, "2": {"latency": 0.05}})
+        env.reg.set_alias("m", "champion", env.version())
+        flaky = _FlakyProm(LocalProm(env.store, env.clock))
+        env.op, env.rec = make_operator(env.kube, LocalMlflowClient(env.reg), flaky, env.clock,
+                                        OperatorSettings(), metrics=env.metrics)
+        env.ctl = FakeSeldonController(env.kube, env.launcher, env.clock).start()
+        await env.op.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+
+        async def at_30():
+            st = await env.status()
+            return st.get("phase") == "Canary" and st.get("canaryTraffic", 0) >= 30
+        assert await env.run_until(at_30, 2000)
+        flaky.down = True
+        split = seldon.traffic_of(await env.sd())
+        await env.clock.sleep(600)  # 60 gate attempts' worth of outage
+        st = await env.status()
+        assert st["phase"] == "Canary" and st["metricsUnavailable"] == "True"
+        assert seldon.traffic_of(await env.sd()) == split
+        assert env.reasons().count("MetricsUnavailable") == 1
+        assert "RollbackComplete" not in env.reasons() and "PromotionFailed" not in env.reasons()
+        flaky.down = False
+        assert await env.run_until(lambda: _phase(env, "Promoted"), 3000)
+        assert "metricsUnavailable" not in await env.status()
         await env.stop()
     run(go())
 

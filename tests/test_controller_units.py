@@ -11,7 +11,8 @@ from mlopamd.controller import crd, placement, prometheus, seldon
 from mlopamd.controller.kube import ApiError, FakeKube, merge_patch
 from mlopamd.controller.mlflow import (MlflowRestClient, NotFound, RegistryUnavailable, SqliteRegistry,
                                        serve_registry)
-from mlopamd.controller.prometheus import (LocalProm, MetricStore, PromClient, evaluate, get_model_metrics,
+from mlopamd.controller.prometheus import (LocalProm, MetricStore, MetricsUnavailable, PromClient, evaluate,
+                                           get_model_metrics,
                                            model_queries, serve_prometheus, should_promote)
 
 
@@ -140,9 +141,14 @@ def test_fake_prometheus_http_roundtrip():
         c = PromClient(url)
         res = await c.query(model_queries("m", "v1", "ns")["latency_95th"], at=t)
         assert abs(float(res[0]["value"][1]) - 0.3) < 1e-9
-        assert await c.query("bogus((", at=t) == []
+        with pytest.raises(MetricsUnavailable):  # a query error is not "no samples"
+            await c.query("bogus((", at=t)
         await c.close()
         await runner.cleanup()
+        c2 = PromClient(url, timeout_s=2.0)
+        with pytest.raises(MetricsUnavailable):  # nothing listening any more
+            await c2.query("up")
+        await c2.close()
     asyncio.run(go())
 
 
