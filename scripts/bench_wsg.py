@@ -4,7 +4,8 @@ LDS-DMA MFMA tiles (gemm.hip, wsgemm off) vs hipBLASLt, Llama-3-8B shapes.
 Decode reads every weight once per step, so the weights rotate over enough copies (> 1 GB)
 that no call finds its matrix in L2 / the 256 MB MALL; us per call over one pass of the copies,
 best of 3 interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  TB/s = weight bytes / time.
-Env: BENCH_MS (row counts), WSG_MIN_WG (comma list swept for the wsgemm arm)."""
+Env: BENCH_MS (row counts), WSG_MIN_WG (comma list swept for the wsgemm arm, empty = none),
+SMALL_TILES (gemm_small_tile values: row-fitted BM x 32 / 64 LDS-DMA tiles)."""
 import json
 import os
 import sys
@@ -17,7 +18,8 @@ from mlopamd import ops  # noqa: E402
 ops.load()
 dev = torch.device("cuda")
 Ms = [int(m) for m in os.environ.get("BENCH_MS", "8,16,32,64").split(",")]
-MIN_WG = [int(v) for v in os.environ.get("WSG_MIN_WG", "256").split(",")]
+MIN_WG = [int(v) for v in os.environ.get("WSG_MIN_WG", "256").split(",") if v]
+SMALL_TILES = [int(v) for v in os.environ.get("SMALL_TILES", "").split(",") if v]  # gemm_small_tile arms
 SHAPES = (("qkv", 6144, 4096, 0), ("o", 4096, 4096, 2), ("gate_up", 28672, 4096, 1), ("down", 4096, 14336, 2))
 
 
@@ -69,6 +71,11 @@ for name, N, K, epi in SHAPES:
                 torch.ops.mlop.gemm_wsg_config(64, mw)
                 k = f"wsg{mw}"
                 arms[k] = min(arms.get(k, 1e9), run_pass(mlop, ws, xs))
+            for st in SMALL_TILES:
+                torch.ops.mlop.gemm_small_tile(st)
+                k = f"st{st}"
+                arms[k] = min(arms.get(k, 1e9), run_pass(mlop, ws, xs))
+            torch.ops.mlop.gemm_small_tile(0)
             arms["hipblaslt"] = min(arms.get("hipblaslt", 1e9), run_pass(blas, ws, xs))
         torch.ops.mlop.gemm_wsg_config(0, 256)
         wb = N * K * 2

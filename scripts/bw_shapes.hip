@@ -16,10 +16,10 @@
 
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 
-template <int SHAPE, int U>
+template <int SHAPE, int U, int RPW = 32>
 __global__ void __launch_bounds__(256) stream(const uint16_t* __restrict__ W, int N, int K, float* sink) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * 32;  // 32 rows per workgroup, the 4 waves split K in quarters
+  const int row0 = blockIdx.x * RPW;  // RPW rows per workgroup, the 4 waves split K in quarters
   const int kq = K / 4, k0 = w * kq;
   // lane -> (row offset, element offset) inside one 1-KiB instruction
   int rr, ce;
@@ -31,8 +31,9 @@ __global__ void __launch_bounds__(256) stream(const uint16_t* __restrict__ W, in
   constexpr int EPI = 512 / RPI;                                      // elements per row per instr.
   // a step = 8 instructions; with more than 8 row groups (2 x 512 B, 1 KiB) consecutive steps
   // take the next 8 row groups before K advances (NB blocks)
-  constexpr int RG = 32 / RPI;
+  constexpr int RG = RPW / RPI > 0 ? RPW / RPI : 1;
   constexpr int IPRG = RG >= 8 ? 1 : 8 / RG;  // instructions per row group per step
+  static_assert(RPW % RPI == 0, "rows per workgroup");
   constexpr int NB = RG >= 8 ? RG / 8 : 1;
   constexpr int step_k = IPRG * EPI;
   const int nsteps = NB * (kq / step_k);
@@ -73,7 +74,7 @@ __global__ void __launch_bounds__(256) stream(const uint16_t* __restrict__ W, in
   if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[threadIdx.x] = 1.f;
 }
 
-template <int SHAPE, int U>
+template <int SHAPE, int U, int RPW = 32>
 float run(const std::vector<uint16_t*>& ws, int N, int K, float* sink) {
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -81,7 +82,7 @@ float run(const std::vector<uint16_t*>& ws, int N, int K, float* sink) {
   float best = 1e30f;
   for (int rep = 0; rep < 3; ++rep) {
     hipEventRecord(a);
-    for (auto* w : ws) stream<SHAPE, U><<<N / 32, 256>>>(w, N, K, sink);
+    for (auto* w : ws) stream<SHAPE, U, RPW><<<N / RPW, 256>>>(w, N, K, sink);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -93,25 +94,29 @@ float run(const std::vector<uint16_t*>& ws, int N, int K, float* sink) {
 }
 
 int main() {
-  const int K = 4096;
-  for (int N : {28672, 6144, 4096}) {
-    const size_t one = (size_t)N * K * 2;
-    const int copies = (int)((size_t)(1536u << 20) / one) + 1;
-    std::vector<uint16_t*> ws(copies);
-    for (auto& w : ws) {
-      hipMalloc(&w, one);
-      hipMemset(w, 0x3c, one);
+  for (int K : {4096, 14336}) {
+    for (int N : {28672, 6144, 4096}) {
+      if (K == 14336 && N != 4096) continue;
+      const size_t one = (size_t)N * K * 2;
+      const int copies = (int)((size_t)(1536u << 20) / one) + 1;
+      std::vector<uint16_t*> ws(copies);
+      for (auto& w : ws) {
+        hipMalloc(&w, one);
+        hipMemset(w, 0x3c, one);
+      }
+      float* sink;
+      hipMalloc(&sink, 4096);
+      run<0, 3>(ws, N, K, sink);  // warm
+      printf("N=%d K=%d copies=%d  TB/s: frag16x64B U3 %.2f U4 %.2f | piece8x128B U3 %.2f U4 %.2f | "
+             "2x512B U3 %.2f U4 %.2f | 1x1KiB U3 %.2f U4 %.2f | 8 rows/WG: piece U3 %.2f U2 %.2f, 1KiB U3 %.2f | "
+             "16 rows/WG piece U3 %.2f\n",
+             N, K, copies, run<0, 3>(ws, N, K, sink), run<0, 4>(ws, N, K, sink), run<1, 3>(ws, N, K, sink),
+             run<1, 4>(ws, N, K, sink), run<2, 3>(ws, N, K, sink), run<2, 4>(ws, N, K, sink),
+             run<3, 3>(ws, N, K, sink), run<3, 4>(ws, N, K, sink), run<1, 3, 8>(ws, N, K, sink),
+             run<1, 2, 8>(ws, N, K, sink), run<3, 3, 8>(ws, N, K, sink), run<1, 3, 16>(ws, N, K, sink));
+      for (auto* w : ws) hipFree(w);
+      hipFree(sink);
     }
-    float* sink;
-    hipMalloc(&sink, 4096);
-    run<0, 3>(ws, N, K, sink);  // warm
-    printf("N=%d K=%d copies=%d  TB/s: frag16x64B U3 %.2f U4 %.2f | piece8x128B U3 %.2f U4 %.2f | "
-           "2x512B U3 %.2f U4 %.2f | 1x1KiB U3 %.2f U4 %.2f\n",
-           N, K, copies, run<0, 3>(ws, N, K, sink), run<0, 4>(ws, N, K, sink), run<1, 3>(ws, N, K, sink),
-           run<1, 4>(ws, N, K, sink), run<2, 3>(ws, N, K, sink), run<2, 4>(ws, N, K, sink),
-           run<3, 3>(ws, N, K, sink), run<3, 4>(ws, N, K, sink));
-    for (auto* w : ws) hipFree(w);
-    hipFree(sink);
   }
   return 0;
 }

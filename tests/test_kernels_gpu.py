@@ -358,6 +358,42 @@ def test_gemv(gpu, M, N, K):
     close(y, exp, atol=2e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [5, 13, 16, 24, 32, 48, 64])
+@pytest.mark.parametrize("tile", [32, 64])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (1280, 8192, 0)])
+def test_gemm_small_tiles(gpu, M, tile, N, K, epi):
+    """Row-fitted LDS-DMA tiles for M <= 64 (gemm.hip plan, ``gemm_small_tile``): BM 16 / 32 / 64
+    by the batch, BN 32 / 64, split-K slabs on narrow N; plain, SiLU-mul and the fused
+    add + RMSNorm reduce; vs fp32 matmul."""
+    torch.manual_seed(M * 7 + tile + N)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    if epi:
+        g = (0.05 * torch.randn(N // 2, K, device=gpu)).to(bf)
+        u = (0.05 * torch.randn(N // 2, K, device=gpu)).to(bf)
+        w = ops.interleave_gate_up(g, u)
+        exp = ref.silu_mul((x.float() @ torch.cat([g, u]).float().t()).to(bf))
+    else:
+        w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
+        exp = x.float() @ w.float().t()
+    prev = torch.ops.mlop.gemm_small_tile()
+    torch.ops.mlop.gemm_small_tile(tile)
+    try:
+        y = torch.empty(M, N // 2 if epi else N, device=gpu, dtype=bf)
+        nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
+        torch.ops.mlop.gemm(y, x, w, torch.full((max(nws, 1),), float("nan"), device=gpu), epi)
+        close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+        if not epi and nws:  # split-K: the residual add + RMSNorm reduce on the same slabs
+            res = torch.randn(M, N, device=gpu, dtype=bf)
+            nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
+            e_out, e_res = ref.add_rmsnorm(exp.to(bf), res, nw, 1e-5)
+            out = torch.empty(M, N, device=gpu, dtype=bf)
+            assert torch.ops.mlop.gemm_add_rmsnorm(out, res, x, w, nw, torch.empty(nws, device=gpu), 1e-5)
+            close(res, e_res, atol=3e-2, rtol=2e-2)
+            close(out, e_out, atol=5e-2, rtol=3e-2)
+    finally:
+        torch.ops.mlop.gemm_small_tile(prev)
+
+
 @pytest.mark.parametrize("M", [5, 8, 16, 17, 32, 40, 64])
 @pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (28672, 4096, 1),
                                      (1280, 8192, 0)])
