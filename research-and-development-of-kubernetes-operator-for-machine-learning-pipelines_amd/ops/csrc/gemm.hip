@@ -1020,8 +1020,11 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     // weight-streaming tiles (M <= 128): a deeper LDS-DMA ring keeps more weight bytes in
     // flight per CU (3 stages x 16 KB per workgroup streamed gate_up at 4.7 TB/s at M = 64)
     if (p.BM == 16 && p.BN == 32) MLOP_GEMM(16, 32, 1, 2, 4, false);
+    else if (p.BM == 16 && p.BN == 64 && g_small_stages >= 8) MLOP_GEMM(16, 64, 1, 2, 8, false);
+    else if (p.BM == 16 && p.BN == 64 && g_small_stages >= 6) MLOP_GEMM(16, 64, 1, 2, 6, false);
     else if (p.BM == 16 && p.BN == 64) MLOP_GEMM(16, 64, 1, 2, 4, false);
     else if (p.BM == 32 && p.BN == 32) MLOP_GEMM(32, 32, 1, 2, 4, false);
+    else if (p.BM == 32 && p.BN == 64 && g_small_stages >= 6) MLOP_GEMM(32, 64, 1, 4, 6, false);
     else if (p.BM == 32 && p.BN == 64) MLOP_GEMM(32, 64, 1, 4, 4, false);
     else if (p.BM == 64 && p.BN == 32) MLOP_GEMM(64, 32, 1, 2, 4, false);
     else if (p.BM == 64 && g_small_stages >= 6) MLOP_GEMM(64, 64, 1, 4, 6, false);

@@ -20,6 +20,7 @@ dev = torch.device("cuda")
 Ms = [int(m) for m in os.environ.get("BENCH_MS", "8,16,32,64").split(",")]
 MIN_WG = [int(v) for v in os.environ.get("WSG_MIN_WG", "256").split(",") if v]
 SMALL_TILES = [int(v) for v in os.environ.get("SMALL_TILES", "").split(",") if v]  # gemm_small_tile arms
+STAGES = [int(v) for v in os.environ.get("SMALL_STAGES", "3").split(",") if v]  # gemm_small_stages sweep
 SHAPES = (("qkv", 6144, 4096, 0), ("o", 4096, 4096, 2), ("gate_up", 28672, 4096, 1), ("down", 4096, 14336, 2))
 
 
@@ -73,8 +74,11 @@ for name, N, K, epi in SHAPES:
                 arms[k] = min(arms.get(k, 1e9), run_pass(mlop, ws, xs))
             for st in SMALL_TILES:
                 torch.ops.mlop.gemm_small_tile(st)
-                k = f"st{st}"
-                arms[k] = min(arms.get(k, 1e9), run_pass(mlop, ws, xs))
+                for sg in STAGES:
+                    torch.ops.mlop.gemm_small_stages(sg)
+                    k = f"st{st}" + (f"s{sg}" if len(STAGES) > 1 else "")
+                    arms[k] = min(arms.get(k, 1e9), run_pass(mlop, ws, xs))
+                torch.ops.mlop.gemm_small_stages(3)
             torch.ops.mlop.gemm_small_tile(0)
             arms["hipblaslt"] = min(arms.get("hipblaslt", 1e9), run_pass(blas, ws, xs))
         torch.ops.mlop.gemm_wsg_config(0, 256)
