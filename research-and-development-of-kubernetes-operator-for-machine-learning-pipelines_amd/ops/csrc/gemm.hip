@@ -1052,12 +1052,20 @@ int gemm_sk_workgroups(int M, int N, int K) {
   return n_sk;
 }
 
-// EPI_ROPE: the plain (no split-K) plan must stage whole heads: BN >= 128, i.e. M > 256
+// EPI_ROPE: the plain (no split-K) plan must stage whole heads: BN >= 128, i.e. M > 256.
+// Small M whose plan splits K: the slabs go to the stream-K scratch and the split-K reduce is
+// fused into the RoPE + cache kernel (one launch instead of reduce + rope_cache).
+static bool rope_slabs_ok(const Plan& p, int M, int N) {
+  const SkBuf* b = sk_buf();
+  return p.splits > 1 && p.variant != 3 && b != nullptr &&
+         (size_t)p.splits * M * N <= (size_t)2 * kSkMaxWg * 256 * 256;
+}
+
 bool gemm_rope_supported(int M, int N, int K) {
   if (M <= 0 || N % 128 || K % kBK) return false;
   if (gemv_takes(M, N, K, EPI_ROPE)) return true;  // decode M <= 8: gemv.hip
   const Plan p = plan(M, N, K, false, 0, 0);
-  return p.BM == 256 && p.BN >= 128;
+  return (p.BM == 256 && p.BN >= 128) || rope_slabs_ok(p, M, N);
 }
 
 bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
@@ -1069,6 +1077,13 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     return true;
   }
   Plan p = plan(M, N, K, false, 0, 0);
+  if (!(p.BM == 256 && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
+    float* ws = sk_buf()->ws;
+    launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
+                                 M, N, K, nullptr, 0, st);
+    launch_rope_cache_slabs(re, ws, p.splits, M, N, st);
+    return true;
+  }
   p.splits = 1;
   p.k_chunk = K;
   launch_plan<EPI_ROPE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, nullptr,

@@ -42,6 +42,9 @@ struct RopeEpi {
   const int* slots;
   int Hq, Hkv, BS;
 };
+// RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
+// split-K reduce fused in: small-M launch_gemm_rope)
+void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
 long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value

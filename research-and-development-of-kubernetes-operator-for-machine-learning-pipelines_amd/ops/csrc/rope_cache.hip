@@ -13,17 +13,42 @@
 
 namespace mlop {
 
+// SLABS: the input is the QKV projection's split-K partials instead of its bf16 output,
+// ws[s][T][qkv_stride] fp32: the 8 values of a vector are summed over the splits and rounded
+// to bf16 (splitk_reduce_kernel's order and rounding), so one launch replaces reduce + RoPE.
+template <bool SLABS>
+__device__ __forceinline__ u32x4 load8(const uint16_t* row, const float* ws, int t, int T, int stride,
+                                       int splits, int col) {
+  if constexpr (!SLABS) {
+    return *reinterpret_cast<const u32x4*>(row + col);
+  } else {
+    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < splits; ++s) {
+      const float4* p = reinterpret_cast<const float4*>(ws + ((size_t)s * T + t) * stride + col);
+      const float4 x = p[0], y = p[1];
+      a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
+      a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
+    }
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack2(a[2 * j], a[2 * j + 1]);
+    return o;
+  }
+}
+
+template <bool SLABS>
 __global__ void __launch_bounds__(256) rope_cache_kernel(
     uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const uint16_t* __restrict__ qkv, const int* __restrict__ pos, const float* __restrict__ cos_sin,
-    const int* __restrict__ slots, int Hq, int Hkv, int D, int qkv_stride, int BS) {
-  const int t = blockIdx.x;
+    const int* __restrict__ slots, int Hq, int Hkv, int D, int qkv_stride, int BS,
+    const float* __restrict__ ws = nullptr, int splits = 0) {
+  const int t = blockIdx.x, T = gridDim.x;
   const int half = D >> 1;
   const int vph = half >> 3;  // 8-element vectors per half-head
   const int p = pos[t];
   const int slot = slots ? slots[t] : -1;
   const float* cs = cos_sin + (size_t)p * D;
-  const uint16_t* row = qkv + (size_t)t * qkv_stride;
+  const uint16_t* row = SLABS ? nullptr : qkv + (size_t)t * qkv_stride;
   const int n_rope = (Hq + Hkv) * vph;
   const int n_v = Hkv * (D >> 3);
   const int blk = slot >= 0 ? slot / BS : 0;
@@ -31,9 +56,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   for (int it = threadIdx.x; it < n_rope + n_v; it += blockDim.x) {
     if (it < n_rope) {
       const int h = it / vph, c = (it % vph) * 8;
-      const uint16_t* src = row + h * D;  // q heads then k heads are contiguous
-      u32x4 a = *reinterpret_cast<const u32x4*>(src + c);
-      u32x4 b = *reinterpret_cast<const u32x4*>(src + half + c);
+      // q heads then k heads are contiguous
+      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + c);
+      u32x4 b = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + half + c);
       const float4* cp = reinterpret_cast<const float4*>(cs + c);
       const float4* sp = reinterpret_cast<const float4*>(cs + half + c);
       float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
@@ -60,7 +85,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     } else if (slot >= 0) {
       const int iv = it - n_rope;
       const int kh = iv / (D >> 3), c = (iv % (D >> 3)) * 8;
-      u32x4 a = *reinterpret_cast<const u32x4*>(row + (Hq + Hkv + kh) * D + c);
+      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, (Hq + Hkv + kh) * D + c);
       uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c) * BS + off;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -75,9 +100,15 @@ void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qk
                        const float* cos_sin, const int* slots, int T, int Hq, int Hkv, int D,
                        int qkv_stride, int BS, hipStream_t st) {
   if (T == 0) return;
-  rope_cache_kernel<<<T, 256, 0, st>>>((uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)v_cache,
-                                       (const uint16_t*)qkv, pos, cos_sin, slots, Hq, Hkv, D,
-                                       qkv_stride, BS);
+  rope_cache_kernel<false><<<T, 256, 0, st>>>((uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)v_cache,
+                                              (const uint16_t*)qkv, pos, cos_sin, slots, Hq, Hkv, D,
+                                              qkv_stride, BS);
+}
+
+void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st) {
+  if (T == 0) return;
+  rope_cache_kernel<true><<<T, 256, 0, st>>>(re.q_out, re.k_cache, re.v_cache, nullptr, re.pos, re.cos_sin,
+                                             re.slots, re.Hq, re.Hkv, 128, N, re.BS, ws, splits);
 }
 
 }  // namespace mlop

@@ -73,10 +73,12 @@ def test_rope_cache(gpu, Hq, Hkv):
 
 
 @pytest.mark.parametrize("M,Hq,Hkv", [(300, 32, 8), (1024, 32, 8), (2048, 32, 8), (3000, 32, 8),
-                                      (600, 8, 1)])
+                                      (600, 8, 1), (12, 32, 8), (16, 32, 8), (24, 32, 8), (48, 32, 8),
+                                      (16, 8, 1)])
 def test_qkv_rope_cache_fused(gpu, M, Hq, Hkv):
     """QKV GEMM with RoPE + paged K/V stores in its epilogue (EPI_ROPE; the ping-pong
-    256x256 kernel at M=2048/3000, the 256x128 kernel otherwise) vs fp32 GEMM + rope_cache."""
+    256x256 kernel at M=2048/3000, the 256x128 kernel otherwise; decode-size M: split-K slabs
+    whose reduce is fused into the RoPE + cache kernel) vs fp32 GEMM + rope_cache."""
     from mlopamd.models.layers import rope_table
 
     D, K, BS = 128, 4096, 16
