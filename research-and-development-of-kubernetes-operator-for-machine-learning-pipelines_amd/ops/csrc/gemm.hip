@@ -372,12 +372,12 @@ int gemm_small_stages(int set) {
 }
 
 // Row-fitted narrow tiles for M <= 64 (plan()): 0 = the 64 x 64 tile; 32 / 64 = BN with BM the
-// batch rounded up to 16 / 32 / 64 (no padding rows streamed through the A ring: the 16-row
+// batch rounded up to 16 / 32 / 64; 1 (default) = BM fitted, BN and ring depth per shape (no padding rows streamed through the A ring: the 16-row
 // tile's 4-stage ring is 10 KB instead of 16, so more workgroups stay resident per CU).
 // Default 64: M <= 32 cold projections 6-17 % faster than the 64 x 64 tile (qkv 18.3 -> 15.3 us,
 // o+norm 14.9 -> 12.9, gate_up 47.1 -> 45.6, down+norm 32.9 -> 27.3 at M = 16; BN 32 loses:
 // profiles/r02_midbatch_decode.md, scripts/run131.sh).  Run-time settable for A/B.
-static int g_small_tile = env_int("MLOP_GEMM_SMALL_TILE", 64);  // 64 x 64 for M 33-64 either way
+static int g_small_tile = env_int("MLOP_GEMM_SMALL_TILE", 1);  // 1 = per-shape (plan); 64 x 64 for M 33-64
 int gemm_small_tile(int set) {
   if (set >= 0) g_small_tile = set;
   return g_small_tile;
@@ -939,6 +939,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
 
 struct Plan {
   int BM, BN, splits, k_chunk, m_tiles, variant;
+  int stages;  // LDS-DMA ring depth of the small-M tiles (0: g_small_stages)
 };
 
 
@@ -962,6 +963,17 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   static const int pp_group_min_rows = env_int("MLOP_GEMM_PP_GROUP_MIN_ROWS", 256);
   if (grouped && mrows >= pp_group_min_rows && K % kBK == 0 && N % 256 == 0) {
     p.BM = 256; p.BN = 256; p.variant = 3;  // grouped ping-pong
+  } else if (mrows <= 64 && !grouped && g_small_tile == 1) {
+    // per shape (scripts/run137.sh, cold us at M = 16): wide N (gate_up) 64 columns with a
+    // 6-deep ring (47.0 -> 44.8); narrow N 32 columns with an 8-deep ring at BM 16 (qkv
+    // 15.3 -> 13.5, o / down unchanged): more weight bytes in flight per CU
+    p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
+    p.BN = 64;
+    if (p.BM == 16) {
+      const bool wide = N >= 16384;
+      p.BN = wide ? 64 : 32;
+      p.stages = wide ? 6 : 8;
+    }
   } else if (mrows <= 64 && !grouped && (g_small_tile == 32 || g_small_tile == 64)) {
     p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
     p.BN = g_small_tile;
@@ -1019,12 +1031,15 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
   } else {
     // weight-streaming tiles (M <= 128): a deeper LDS-DMA ring keeps more weight bytes in
     // flight per CU (3 stages x 16 KB per workgroup streamed gate_up at 4.7 TB/s at M = 64)
-    if (p.BM == 16 && p.BN == 32) MLOP_GEMM(16, 32, 1, 2, 4, false);
-    else if (p.BM == 16 && p.BN == 64 && g_small_stages >= 8) MLOP_GEMM(16, 64, 1, 2, 8, false);
-    else if (p.BM == 16 && p.BN == 64 && g_small_stages >= 6) MLOP_GEMM(16, 64, 1, 2, 6, false);
+    const int sst = p.stages ? p.stages : g_small_stages;
+    if (p.BM == 16 && p.BN == 32 && sst >= 8) MLOP_GEMM(16, 32, 1, 2, 8, false);
+    else if (p.BM == 16 && p.BN == 32 && sst >= 6) MLOP_GEMM(16, 32, 1, 2, 6, false);
+    else if (p.BM == 16 && p.BN == 32) MLOP_GEMM(16, 32, 1, 2, 4, false);
+    else if (p.BM == 16 && p.BN == 64 && sst >= 8) MLOP_GEMM(16, 64, 1, 2, 8, false);
+    else if (p.BM == 16 && p.BN == 64 && sst >= 6) MLOP_GEMM(16, 64, 1, 2, 6, false);
     else if (p.BM == 16 && p.BN == 64) MLOP_GEMM(16, 64, 1, 2, 4, false);
     else if (p.BM == 32 && p.BN == 32) MLOP_GEMM(32, 32, 1, 2, 4, false);
-    else if (p.BM == 32 && p.BN == 64 && g_small_stages >= 6) MLOP_GEMM(32, 64, 1, 4, 6, false);
+    else if (p.BM == 32 && p.BN == 64 && sst >= 6) MLOP_GEMM(32, 64, 1, 4, 6, false);
     else if (p.BM == 32 && p.BN == 64) MLOP_GEMM(32, 64, 1, 4, 4, false);
     else if (p.BM == 64 && p.BN == 32) MLOP_GEMM(64, 32, 1, 2, 4, false);
     else if (p.BM == 64 && g_small_stages >= 6) MLOP_GEMM(64, 64, 1, 4, 6, false);

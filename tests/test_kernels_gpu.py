@@ -92,18 +92,24 @@ def test_qkv_rope_cache_fused(gpu, M, Hq, Hkv):
     slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
     slots[5] = -1
     slots[M - 1] = -1
-    assert torch.ops.mlop.gemm_rope_supported(M, N, K)
-    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
-    q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
-    assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
-    qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
-    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
-    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
-    close(q, q_ref)
-    close(kc, kr)
-    close(vc, vr)
-    # the wrapper (autotuned fused vs hipBLASLt + rope_cache) agrees too
+    prev = torch.ops.mlop.gemm_small_tile()
+    if M <= 64:  # the 64-column small-M tiles split K at these N: the slab-fed RoPE kernel
+        torch.ops.mlop.gemm_small_tile(64)
+    try:
+        assert torch.ops.mlop.gemm_rope_supported(M, N, K)
+        kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+        vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+        q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
+        assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
+        qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
+        kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+        q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+        close(q, q_ref)
+        close(kc, kr)
+        close(vc, vr)
+    finally:
+        torch.ops.mlop.gemm_small_tile(prev)
+    # the wrapper (autotuned fused vs hipBLASLt + rope_cache; default small-M tiles) agrees too
     q2 = ops.qkv_rope_cache(x, w, pos, cs, slots, kc, vc, Hq)
     close(q2, q_ref)
 
@@ -361,12 +367,13 @@ def test_gemv(gpu, M, N, K):
 
 
 @pytest.mark.parametrize("M", [5, 13, 16, 24, 32, 48, 64])
-@pytest.mark.parametrize("tile", [32, 64])
-@pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (1280, 8192, 0)])
+@pytest.mark.parametrize("tile", [1, 32, 64])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (1280, 8192, 0),
+                                     (28672, 4096, 1)])
 def test_gemm_small_tiles(gpu, M, tile, N, K, epi):
     """Row-fitted LDS-DMA tiles for M <= 64 (gemm.hip plan, ``gemm_small_tile``): BM 16 / 32 / 64
-    by the batch, BN 32 / 64, split-K slabs on narrow N; plain, SiLU-mul and the fused
-    add + RMSNorm reduce; vs fp32 matmul."""
+    by the batch, BN 32 / 64 (1 = per shape: 8- / 6-deep rings at BM 16), split-K slabs on
+    narrow N; plain, SiLU-mul and the fused add + RMSNorm reduce; vs fp32 matmul."""
     torch.manual_seed(M * 7 + tile + N)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     if epi:
