@@ -378,6 +378,12 @@ int gemm_small_stages(int set) {
 // o+norm 14.9 -> 12.9, gate_up 47.1 -> 45.6, down+norm 32.9 -> 27.3 at M = 16; BN 32 loses:
 // profiles/r02_midbatch_decode.md, scripts/run131.sh).  Run-time settable for A/B.
 static int g_small_tile = env_int("MLOP_GEMM_SMALL_TILE", 1);  // 1 = per-shape (plan); 64 x 64 for M 33-64
+// M 17-32 narrow projections on 32-column 8-deep tiles as at M <= 16: measured 1-2 % slower end
+// to end at batch 24 / 32 (scripts/run140.sh), off
+static const int g_small_bm32_narrow = env_int("MLOP_GEMM_BM32_NARROW", 0);
+// ring depth of the grouped (MoE) 64-row tiles on narrow N (the down projection): 6 measured
+// neutral on Mixtral batch 32 / 64 (1,651 vs 1,655, 3,142 vs 3,134 tok/s, scripts/run141.sh)
+static const int g_grouped_small_stages = env_int("MLOP_GEMM_GROUPED_SMALL_STAGES", 3);
 int gemm_small_tile(int set) {
   if (set >= 0) g_small_tile = set;
   return g_small_tile;
@@ -969,17 +975,22 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // 15.3 -> 13.5, o / down unchanged): more weight bytes in flight per CU
     p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
     p.BN = 64;
-    if (p.BM == 16) {
+    if (p.BM == 16 || (p.BM == 32 && g_small_bm32_narrow)) {
       const bool wide = N >= 16384;
       p.BN = wide ? 64 : 32;
-      p.stages = wide ? 6 : 8;
+      p.stages = wide ? (p.BM == 16 ? 6 : 0) : 8;
     } else if (p.BM == 64 && N < 16384) {
       p.stages = 6;  // M 33-64 narrow N (run133: qkv 19.8 -> 18.4, down+norm 35.9 -> 32.0 us)
     }
   } else if (mrows <= 64 && !grouped && (g_small_tile == 32 || g_small_tile == 64)) {
     p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
     p.BN = g_small_tile;
-  } else if (mrows <= 64) { p.BM = 64; p.BN = 64; }
+  } else if (mrows <= 64) {
+    p.BM = 64;
+    p.BN = 64;
+    // grouped (MoE at a few dozen rows per expert), narrow down projection: ring depth knob
+    if (grouped && N < 16384) p.stages = g_grouped_small_stages;
+  }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
   else if (mrows <= 256) {
     static const int bn_min_tiles = env_int("MLOP_GEMM_BN128_MIN_TILES", 192);
@@ -1040,6 +1051,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (p.BM == 16 && p.BN == 64 && sst >= 8) MLOP_GEMM(16, 64, 1, 2, 8, false);
     else if (p.BM == 16 && p.BN == 64 && sst >= 6) MLOP_GEMM(16, 64, 1, 2, 6, false);
     else if (p.BM == 16 && p.BN == 64) MLOP_GEMM(16, 64, 1, 2, 4, false);
+    else if (p.BM == 32 && p.BN == 32 && sst >= 8) MLOP_GEMM(32, 32, 1, 2, 8, false);
     else if (p.BM == 32 && p.BN == 32) MLOP_GEMM(32, 32, 1, 2, 4, false);
     else if (p.BM == 32 && p.BN == 64 && sst >= 6) MLOP_GEMM(32, 64, 1, 4, 6, false);
     else if (p.BM == 32 && p.BN == 64) MLOP_GEMM(32, 64, 1, 4, 4, false);

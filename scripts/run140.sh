@@ -1,0 +1,13 @@
+#!/bin/bash
+# M 17-32: narrow projections on 32-column tiles with an 8-deep ring (as at M <= 16) vs the
+# previous build (64 columns, 4-deep).
+source scripts/gpu_check.sh
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+BASE=$GRAFT_REPO_ROOT/build/ab/_C_base.so
+step m32_tests 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 150 --timeout-method thread -k "small_tiles or rope_cache_fused"
+for r in 1 2; do
+  for b in 24 32; do
+    step e2e_base_${b}_$r 200 env MLOP_LIB=$BASE python bench.py --batch $b --steps 150 --warmup 20 --no-operator
+    step e2e_n32_${b}_$r 200 python bench.py --batch $b --steps 150 --warmup 20 --no-operator
+  done
+done
