@@ -979,8 +979,10 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
       const bool wide = N >= 16384;
       p.BN = wide ? 64 : 32;
       p.stages = wide ? (p.BM == 16 ? 6 : 0) : 8;
-    } else if (p.BM == 64 && N < 16384) {
-      p.stages = 6;  // M 33-64 narrow N (run133: qkv 19.8 -> 18.4, down+norm 35.9 -> 32.0 us)
+    } else if (p.BM == 64) {
+      // M 33-64: narrow N on the 6-deep ring (run133: qkv 19.8 -> 18.4, down+norm 35.9 -> 32.0 us),
+      // gate_up on a 4-deep one (run145: 48.2 -> 47.1 at M = 64, 6 stages lose: 50.4)
+      p.stages = N < 16384 ? 6 : 4;
     }
   } else if (mrows <= 64 && !grouped && (g_small_tile == 32 || g_small_tile == 64)) {
     p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
@@ -1057,6 +1059,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (p.BM == 32 && p.BN == 64) MLOP_GEMM(32, 64, 1, 4, 4, false);
     else if (p.BM == 64 && p.BN == 32) MLOP_GEMM(64, 32, 1, 2, 4, false);
     else if (p.BM == 64 && p.BN == 64 && sst >= 6) MLOP_GEMM(64, 64, 1, 4, 6, false);
+    else if (p.BM == 64 && p.BN == 64 && sst == 4) MLOP_GEMM(64, 64, 1, 4, 4, false);
     else if (p.BM == 64) MLOP_GEMM(64, 64, 1, 4, 3, false);
     else if (p.BM == 128 && g_small_stages >= 5) MLOP_GEMM(128, 64, 2, 2, 5, false);
     else if (p.BM == 128) MLOP_GEMM(128, 64, 2, 2, 3, false);
