@@ -34,14 +34,14 @@ FAULTS = {
 async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, device: str = "cuda",
                          namespace: str = "llm", concurrency: int = 8, prompt_len: int = 32,
                          max_tokens: int = 16, warm_requests: int = 16, timeout_s: float = 600.0,
-                         engine_env: dict | None = None) -> dict:
+                         engine_env: dict | None = None, gpu_slots: int | None = None) -> dict:
     import aiohttp
 
     from .app import OperatorMetrics, make_operator
     from .clock import RealClock
     from .crd import GROUP, PLURAL, SELDON_GROUP, SELDON_PLURAL, SELDON_VERSION, VERSION, OperatorSettings
     from .kube import FakeKube
-    from .local import FakeSeldonController, ProcessLauncher, Router, mlflow_model_cr, wait_for
+    from .local import FakeSeldonController, GpuPool, ProcessLauncher, Router, mlflow_model_cr, wait_for
     from .mlflow import MlflowRestClient, SqliteRegistry, serve_registry
     from .prometheus import MetricStore, PromClient, Scraper, serve_prometheus
     from ..models.config import get_config
@@ -67,7 +67,14 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
     env = {"MLOP_DEVICE": device, "MLOP_ENGINE_MAX_NUM_SEQS": str(max(16, 2 * concurrency)),
            "MLOP_ENGINE_MAX_MODEL_LEN": "1024", "MLOP_ENGINE_MAX_NUM_BATCHED_TOKENS": "2048"}
     env.update(engine_env or {})
-    launcher = ProcessLauncher(scraper, extra_env=env, per_predictor_env={"v2": FAULTS[regress]})
+    pool = GpuPool.detect()
+    if device == "cpu":
+        pool = GpuPool(8)
+    # one predictor per GPU when the node has a GPU per canary pod (config 3); a 1-GPU box
+    # time-shares its card between the two versions (both fit 288 GB)
+    slots = gpu_slots or (1 if len(pool.devices) >= 2 else 2)
+    pool.slots = slots
+    launcher = ProcessLauncher(scraper, extra_env=env, per_predictor_env={"v2": FAULTS[regress]}, gpus=pool)
     ctl = FakeSeldonController(kube, launcher, clock).start()
     router = Router(ctl)
     scraper.start()
@@ -109,7 +116,10 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
                 served["errors"] += 1
             i += 1
 
-    out = {"config": f"{arch} / mlop-llm / {device}", "cr_ready_s": round(cr_ready_s, 3)}
+    out = {"config": f"{arch} / mlop-llm / {device}", "cr_ready_s": round(cr_ready_s, 3),
+           "predictor_gpus": {p.predictor: p.extra.get("gpus") for p in ctl.pods.values()},
+           "predictor_process_ready_s": {p.predictor: round(p.extra.get("ready_s", 0.0), 3)
+                                         for p in ctl.pods.values()}}
     async with aiohttp.ClientSession() as session:
         t0 = time.perf_counter()
         await asyncio.gather(*(worker(session, max(1, warm_requests // concurrency)) for _ in range(concurrency)))
@@ -127,6 +137,7 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
         final = await wait_for(settled, timeout_s=timeout_s, poll_s=0.2)
         stop.set()
         await asyncio.gather(*bg)
+        out["canary_predictor_gpus"] = {p.predictor: p.extra.get("gpus") for p in ctl.pods.values()}
         out.update(canary_phase=final.get("phase"), canary_seconds=round(time.perf_counter() - t1, 2),
                    current_version=final.get("currentModelVersion"),
                    rolled_back_version=final.get("rolledBackVersion"), error=final.get("error"),
@@ -155,6 +166,8 @@ if __name__ == "__main__":
     ap.add_argument("--regress", choices=["latency", "errors"], default=None)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--concurrency", type=int, default=8)
+    ap.add_argument("--gpu-slots", type=int, default=None, help="predictors per GPU (default: 2 on a 1-GPU node)")
+    ap.add_argument("--timeout", type=float, default=600.0)
     a = ap.parse_args()
-    print(json.dumps(asyncio.run(run_llm_canary(a.arch, a.regress, a.device, concurrency=a.concurrency)),
-                     indent=2))
+    print(json.dumps(asyncio.run(run_llm_canary(a.arch, a.regress, a.device, concurrency=a.concurrency,
+                                                gpu_slots=a.gpu_slots, timeout_s=a.timeout)), indent=2))

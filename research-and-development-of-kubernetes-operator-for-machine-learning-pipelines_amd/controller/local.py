@@ -98,14 +98,98 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def _container_of(pred: dict) -> dict | None:
+    for cs in pred.get("componentSpecs") or []:
+        for c in cs.get("spec", {}).get("containers", []):
+            return c
+    return None
+
+
+class GpuPool:
+    """The node's ``amd.com/gpu`` devices as the device plugin hands them out: a pod that asks
+    for k GPUs gets k free device indices, exported to its containers as
+    ``HIP_VISIBLE_DEVICES`` (so ``cuda:0..k-1`` inside the pod are ITS GPUs and a TP=k
+    predictor's ranks land on k distinct GPUs).  ``slots_per_gpu`` > 1 time-shares devices
+    (a dev node serving two 8B canary predictors from one MI355X); 1 is the kubelet's
+    exclusive assignment.  A request the free slots cannot cover fails like an
+    unschedulable pod (``Insufficient amd.com/gpu``)."""
+
+    def __init__(self, devices, slots_per_gpu: int = 1):
+        self.devices = list(range(devices)) if isinstance(devices, int) else list(devices)
+        self.slots = max(1, int(slots_per_gpu))
+        self.used: dict[int, int] = {d: 0 for d in self.devices}
+
+    @classmethod
+    def detect(cls, slots_per_gpu: int = 1) -> "GpuPool":
+        """Devices visible to this process: HIP_VISIBLE_DEVICES, else the driver's count
+        (``torch.cuda.device_count`` does not initialise HIP on this image)."""
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+        if vis:
+            return cls([int(x) for x in vis.split(",") if x.strip()], slots_per_gpu)
+        n = int(os.environ.get("MLOP_NODE_GPUS", "-1"))
+        if n < 0:
+            try:
+                import torch
+
+                n = torch.cuda.device_count()
+            except Exception:  # noqa: BLE001
+                n = 0
+        return cls(n, slots_per_gpu)
+
+    @property
+    def free(self) -> int:
+        return sum(self.slots - u for u in self.used.values())
+
+    def acquire(self, k: int) -> list[int]:
+        if k <= 0:
+            return []
+        # least-used devices first, distinct devices for one pod (its ranks must not share)
+        order = sorted((u, d) for d, u in self.used.items() if u < self.slots)
+        if len(order) < k:
+            raise RuntimeError(f"0/1 nodes are available: Insufficient amd.com/gpu (requested {k}, "
+                               f"{len(order)} of {len(self.devices)} devices have a free slot)")
+        got = [d for _, d in order[:k]]
+        for d in got:
+            self.used[d] += 1
+        return sorted(got)
+
+    def release(self, devs: list[int]) -> None:
+        for d in devs or []:
+            if self.used.get(d, 0) > 0:
+                self.used[d] -= 1
+
+
 class ProcessLauncher:
-    """One OS process per predictor replica running the V2 runtime server."""
+    """One OS process (group) per predictor replica, started from the predictor container's own
+    ``command`` / ``args`` as the Seldon controller's pod would (``python`` resolved to this
+    interpreter, ``--port`` rewritten to a free local port), with the container env and the
+    GPUs the container requests (``amd.com/gpu`` -> ``HIP_VISIBLE_DEVICES`` from ``gpus``, a
+    ``GpuPool``).  A TP predictor's container (``--tp N``) launches its own N rank processes
+    (runtime/server.py ``launch_ranks``)."""
 
     def __init__(self, scraper=None, extra_env: dict | None = None, python: str = sys.executable,
-                 ready_timeout_s: float = 600.0, per_predictor_env: dict | None = None):
+                 ready_timeout_s: float = 600.0, per_predictor_env: dict | None = None,
+                 gpus: GpuPool | int | None = None, gpu_resource: str = "amd.com/gpu"):
         self.scraper, self.extra_env, self.python = scraper, extra_env or {}, python
         self.per_predictor_env = per_predictor_env or {}  # predictor name -> env (fault injection)
         self.ready_timeout_s = ready_timeout_s
+        if gpus is None and self.extra_env.get("MLOP_DEVICE") == "cpu":
+            gpus = 8  # CPU emulation of an 8-GPU node: device indices are labels only
+        self.gpus = GpuPool(gpus) if isinstance(gpus, int) else (gpus or GpuPool.detect())
+        self.gpu_resource = gpu_resource
+
+    def command(self, pod: Pod, port: int) -> list[str]:
+        c = _container_of(pod.spec)
+        if c is None or not c.get("command"):  # stock MLFLOW_SERVER predictor: our sklearn server
+            return [self.python, "-m", "mlopamd.runtime.server", "--port", str(port), "--host", "127.0.0.1"]
+        cmd = [self.python if x in ("python", "python3") else x for x in c["command"]]
+        args = list(c.get("args") or [])
+        for flag, val in (("--port", str(port)), ("--host", "127.0.0.1")):
+            if flag in args:
+                args[args.index(flag) + 1] = val
+            else:
+                args += [flag, val]
+        return cmd + args
 
     async def start(self, pod: Pod):
         import aiohttp
@@ -117,6 +201,15 @@ class ProcessLauncher:
         env.update(self.per_predictor_env.get(pod.predictor, {}))
         env["SELDON_DEPLOYMENT_ID"] = pod.sd
         env["SELDON_NAMESPACE"] = pod.namespace
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):  # the pod is its own rank group
+            env.pop(k, None)
+        need = seldon.gpus_of(pod.spec, self.gpu_resource)
+        devs = self.gpus.acquire(need)  # raises (unschedulable) when the node has no free GPUs
+        pod.extra["gpus"] = devs
+        if need:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, devs))
+            env.pop("ROCR_VISIBLE_DEVICES", None)
+            env.pop("CUDA_VISIBLE_DEVICES", None)
         repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
         import tempfile
@@ -125,20 +218,23 @@ class ProcessLauncher:
         # status and the CR report (`kubectl logs --previous` in a real cluster)
         pod.extra["log"] = log_f = tempfile.NamedTemporaryFile(prefix=f"mlop-{pod.predictor}-", suffix=".log",
                                                              delete=False)
-        pod.proc = subprocess.Popen([self.python, "-m", "mlopamd.runtime.server", "--port", str(port),
-                                     "--host", "127.0.0.1"], env=env, stdout=subprocess.DEVNULL,
+        pod.extra["cmd"] = cmd = self.command(pod, port)
+        pod.extra["t_start"] = time.perf_counter()
+        pod.proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL,
                                     stderr=log_f, start_new_session=True)
         pod.endpoint = f"http://127.0.0.1:{port}"
         t0 = time.monotonic()
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as s:
             while time.monotonic() - t0 < self.ready_timeout_s:
                 if pod.proc.poll() is not None:
+                    self.gpus.release(pod.extra.pop("gpus", []))
                     raise RuntimeError(f"predictor {pod.predictor} exited with {pod.proc.returncode}: "
                                        f"{self._log_tail(pod)}")
                 try:
                     async with s.get(pod.endpoint + "/v2/health/ready") as r:
                         if r.status == 200:
                             pod.ready = True
+                            pod.extra["ready_s"] = time.perf_counter() - pod.extra["t_start"]
                             break
                 except (aiohttp.ClientError, asyncio.TimeoutError, OSError):
                     pass
@@ -171,9 +267,15 @@ class ProcessLauncher:
         if pod.proc is not None and pod.proc.poll() is None:
             pod.proc.terminate()
             try:
-                pod.proc.wait(timeout=10)
+                pod.proc.wait(timeout=20)
             except subprocess.TimeoutExpired:
-                pod.proc.kill()
+                # the whole process group: a TP predictor's rank processes included
+                try:
+                    os.killpg(pod.proc.pid, 9)
+                except OSError:
+                    pod.proc.kill()
+                pod.proc.wait()
+        self.gpus.release(pod.extra.pop("gpus", []))
         f = pod.extra.pop("log", None)
         if f is not None:
             f.close()

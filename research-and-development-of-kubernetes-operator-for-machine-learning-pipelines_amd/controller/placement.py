@@ -46,7 +46,21 @@ def _valid_tp(cfg: ModelConfig, tp: int) -> bool:
 def plan(arch: str | ModelConfig, max_model_len: int = 4096, max_num_seqs: int = 256,
          hbm_gb: float = 288.0, gpus_per_node: int = 8, utilization: float = 0.90,
          reserve_gb: float = 8.0, requested_tp: int | None = None, requested_ep: int | None = None,
-         kv_target_fraction: float = 0.5) -> Placement:
+         kv_target_fraction: float = 0.5, free_gpus: int | None = None) -> Placement:
+    """``free_gpus``: GPUs the target node still has unallocated (reconciler.node_capacity);
+    a placement needing more is returned with ``fits=False`` and the reason (the pod would
+    stay Pending), whatever its HBM arithmetic says."""
+    p = _plan(arch, max_model_len, max_num_seqs, hbm_gb, gpus_per_node, utilization, reserve_gb,
+              requested_tp, requested_ep, kv_target_fraction)
+    if free_gpus is not None and p.gpus > free_gpus:
+        p.fits = False
+        p.reason = (f"needs {p.gpus} GPUs (TP={p.tensorParallel}), the node has {free_gpus} of "
+                    f"{gpus_per_node} amd.com/gpu free") + (f"; {p.reason}" if p.reason else "")
+    return p
+
+
+def _plan(arch, max_model_len, max_num_seqs, hbm_gb, gpus_per_node, utilization, reserve_gb, requested_tp,
+          requested_ep, kv_target_fraction) -> Placement:
     cfg = arch if isinstance(arch, ModelConfig) else get_config(arch)
     usable = hbm_gb * utilization
     wbytes = cfg.weight_bytes()

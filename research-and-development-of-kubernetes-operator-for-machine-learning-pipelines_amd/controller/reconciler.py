@@ -95,6 +95,55 @@ class MlflowModelReconciler:
                 logger.error("[%s/%s] Error deleting SeldonDeployment '%s': %s", ns, name, name, e)
                 raise
 
+    # ------------------------------------------------------------ nodes --
+    async def node_capacity(self, exclude: tuple | None = None) -> dict:
+        """The GPU node a new predictor would land on, as the scheduler sees it: Node objects'
+        ``status.allocatable[amd.com/gpu]`` (the device plugin's count) and HBM per GPU from
+        the AMD node labeller's ``amd.com/gpu.vram`` label (e.g. ``288G``), minus the GPUs
+        other SeldonDeployments' predictors already request (replicas x limits).  Picks the
+        node with the most free GPUs.  {} when no node exposes the resource (or nodes cannot
+        be listed): the planner then uses the operator settings (RBAC
+        ``nodes`` get/list/watch, manifests/rbac.yaml)."""
+        res = self.settings.gpu_resource
+        try:
+            nodes = await self.kube.list("", "v1", None, "nodes")
+        except Exception:  # noqa: BLE001 - no RBAC / no node API: static settings
+            return {}
+        cands = []
+        for n in nodes:
+            alloc = ((n.get("status") or {}).get("allocatable") or {}).get(res)
+            if not alloc:
+                continue
+            labels = (n.get("metadata") or {}).get("labels") or {}
+            vram = labels.get(f"{res}.vram") or labels.get("amd.com/gpu.vram")
+            hbm = None
+            if vram:
+                try:
+                    hbm = float(str(vram).rstrip("GgBi"))
+                except ValueError:
+                    hbm = None
+            cands.append({"node": n["metadata"]["name"], "gpus": int(alloc), "hbm_gb": hbm})
+        if not cands:
+            return {}
+        used = 0
+        try:
+            sds = await self.kube.list(SELDON_GROUP, SELDON_VERSION, None, SELDON_PLURAL)
+        except Exception:  # noqa: BLE001
+            sds = []
+        for sd in sds:
+            md = sd.get("metadata") or {}
+            if exclude and (md.get("namespace"), md.get("name")) == exclude:
+                continue
+            for p in (sd.get("spec") or {}).get("predictors", []):
+                used += int(p.get("replicas", 1)) * seldon.gpus_of(p, res)
+        # one node's view: the free GPUs are taken from the roomiest node (used GPUs are
+        # charged to it, a conservative single-node model of the scheduler)
+        best = max(cands, key=lambda c: c["gpus"])
+        out = {"node": best["node"], "gpus": best["gpus"], "free_gpus": max(0, best["gpus"] - used)}
+        if best["hbm_gb"]:
+            out["hbm_gb"] = best["hbm_gb"]
+        return out
+
     # --------------------------------------------------------- desired --
     async def _uri(self, spec: ModelSpec, version) -> tuple[str, object]:
         mv = await self.mlflow.get_model_version(spec.model_name, version)
@@ -118,18 +167,33 @@ class MlflowModelReconciler:
         split = phase in (PH_CANARY, PH_FAILED) and prev is not None
         ct = int(status.get("canaryTraffic") or 0)
         versions = [(prev, 100 - ct), (cur, ct)] if split else [(cur, 100)]
+        node = None
         for v, traffic in versions:
             uri, mv = await self._uri(spec, v)
             runtime, arch = self._runtime_of(spec, mv)
             placement = None
             if runtime == seldon.RUNTIME_LLM and arch:
+                if node is None:
+                    node = await self.node_capacity(exclude=(md["namespace"], md["name"]))
                 p = plan(arch, max_model_len=spec.max_model_len or 4096, max_num_seqs=spec.max_num_seqs or 256,
-                         hbm_gb=self.settings.hbm_per_gpu_gb, gpus_per_node=self.settings.gpus_per_node,
+                         hbm_gb=node.get("hbm_gb", self.settings.hbm_per_gpu_gb),
+                         gpus_per_node=node.get("gpus", self.settings.gpus_per_node),
                          requested_tp=spec.tensor_parallel, requested_ep=spec.expert_parallel,
-                         kv_target_fraction=spec.kv_target_fraction or 0.5)
+                         kv_target_fraction=spec.kv_target_fraction or 0.5,
+                         free_gpus=node.get("free_gpus"))
                 placement = {"tensorParallel": p.tensorParallel, "expertParallel": p.expertParallel,
                              "gpus": p.gpus, "weightGBPerGPU": p.weightGBPerGPU,
                              "kvTokenCapacity": p.kvTokenCapacity, "fits": p.fits}
+                if not p.fits:
+                    placement["reason"] = p.reason
+                if node.get("node"):
+                    placement["node"] = node["node"]
+                if node.get("free_gpus") is not None:  # the canary's second predictor needs its own
+                    node = dict(node, free_gpus=max(0, node["free_gpus"] - p.gpus * spec.replicas))
+            elif runtime == seldon.RUNTIME_LLM and spec.tensor_parallel:
+                # a checkpoint of unknown architecture (no preset): honour the requested degree
+                tp = int(spec.tensor_parallel)
+                placement = {"tensorParallel": tp, "expertParallel": int(spec.expert_parallel or 1), "gpus": tp}
             engine_args = {}
             if spec.max_model_len:
                 engine_args["max_model_len"] = spec.max_model_len

@@ -136,6 +136,18 @@ def predictor_health(sd: dict | None, predictor: str) -> tuple[int, bool, str]:
     return restarts, failed, reason
 
 
+def gpus_of(pred: dict, resource: str = "amd.com/gpu") -> int:
+    """GPUs one replica of a predictor requests (container limits win over requests, as the
+    scheduler reads them); 0 for the stock MLFLOW_SERVER predictor."""
+    n = 0
+    for cs in pred.get("componentSpecs") or []:
+        for c in cs.get("spec", {}).get("containers", []):
+            res = c.get("resources") or {}
+            v = (res.get("limits") or {}).get(resource, (res.get("requests") or {}).get(resource, 0))
+            n += int(v or 0)
+    return n
+
+
 def traffic_of(sd: dict | None) -> dict:
     return {p["name"]: p.get("traffic", 0) for p in ((sd or {}).get("spec") or {}).get("predictors", [])}
 

@@ -233,7 +233,62 @@ def engine_kwargs_from_env() -> dict:
     return out
 
 
+def launch_ranks(tp: int, argv: list[str]) -> int:
+    """``--tp N`` in a container started WITHOUT a rank launcher (what the SeldonDeployment's
+    predictor command is): this process becomes the launcher of N fresh rank processes, one
+    per visible GPU (``LOCAL_RANK`` indexes ``HIP_VISIBLE_DEVICES``), and never touches the GPU
+    itself (no HIP call before the children exist).  Rank 0 serves HTTP on ``--port``, the
+    others park in the engine's worker loop (runtime/tp_worker.py).  The first rank to exit
+    ends the group: the rest are terminated and the launcher exits with that rank's status,
+    so the kubelet (or the local Seldon stand-in) sees one pod that failed, as it would for
+    ``torchrun``.  Reference contract: one predictor per model version
+    (mlflow_operator.py:194-222) — with TP it is one pod of N ranks."""
+    import signal
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(tp):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(tp),
+                   LOCAL_WORLD_SIZE=str(tp), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, "-m", "mlopamd.runtime.server", *argv], env=env))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    try:
+        while True:
+            done = [p for p in procs if p.poll() is not None]
+            if done:
+                rc = next((p.returncode for p in done if p.returncode), 0)
+                break
+            time.sleep(0.2)
+    finally:
+        # rank 0 first: its shutdown sends STOP to the parked workers (engine.shutdown)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=10 if p is procs[0] else 3)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+    return rc
+
+
 def main(argv=None):
+    import sys
+
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description="mlopamd V2 inference server")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=int(os.environ.get("MLOP_PORT", 9000)))
@@ -245,6 +300,8 @@ def main(argv=None):
     ap.add_argument("--device", default=os.environ.get("MLOP_DEVICE", "cuda"))
     ap.add_argument("--tp", type=int, default=1)
     a = ap.parse_args(argv)
+    if a.tp > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(a.tp, argv))
 
     from aiohttp import web
 

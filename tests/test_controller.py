@@ -426,6 +426,59 @@ def test_llm_runtime_predictor_gets_gpus_and_placement():
     run(go())
 
 
+def _gpu_node(name, gpus, vram="288G"):
+    return {"apiVersion": "v1", "kind": "Node",
+            "metadata": {"name": name, "labels": {"amd.com/gpu.vram": vram}},
+            "status": {"allocatable": {"amd.com/gpu": str(gpus), "cpu": "128"}}}
+
+
+def test_placement_reads_node_capacity():
+    """G2 node-aware: the planner reads Node allocatable amd.com/gpu and the labeller's VRAM,
+    subtracts GPUs other SeldonDeployments hold, and marks a TP=8 70B predictor unplaceable on
+    a node with 4 free GPUs (fits=false + reason), while an auto-planned one lands in them."""
+    async def go():
+        env = Env()
+        await env.kube.create("", "v1", None, "nodes", _gpu_node("mi355x-0", 8))
+        # another team's predictor already holds 4 of the 8 GPUs
+        other = seldon.build_seldon_deployment("other", "team", {"metadata": {"name": "o", "uid": "u"}}, [
+            seldon.build_predictor(1, "s3://x", None, 100, runtime=seldon.RUNTIME_LLM,
+                                   placement={"tensorParallel": 4, "gpus": 4})])
+        await env.kube.create(SELDON_GROUP, SELDON_VERSION, "team", SELDON_PLURAL, other)
+        v = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v)
+        await env.start()
+        await env.create_cr(tensorParallel=8, maxModelLen=8192, maxNumSeqs=128)
+        assert await env.run_until(lambda: _ready(env))
+        (p,) = (await env.sd())["spec"]["predictors"]
+        ann = p["annotations"]
+        assert ann["mlop.amd.com/fits"] == "False" and ann["mlop.amd.com/node"] == "mi355x-0"
+        assert "needs 8 GPUs" in ann["mlop.amd.com/reason"] and "4 of 8" in ann["mlop.amd.com/reason"]
+        await env.stop()
+
+        env2 = Env()
+        await env2.kube.create("", "v1", None, "nodes", _gpu_node("mi355x-0", 8))
+        await env2.kube.create(SELDON_GROUP, SELDON_VERSION, "team", SELDON_PLURAL, other)
+        v = env2.version(tags={"mlop.architecture": "llama3-70b"})
+        env2.reg.set_alias("m", "champion", v)
+        await env2.start()
+        await env2.create_cr(maxModelLen=8192, maxNumSeqs=128)  # auto: smallest TP that fits HBM
+        assert await env2.run_until(lambda: _ready(env2))
+        (p,) = (await env2.sd())["spec"]["predictors"]
+        ann = p["annotations"]
+        assert ann["mlop.amd.com/fits"] == "True" and int(ann["mlop.amd.com/gpus"]) <= 4
+        await env2.stop()
+    run(go())
+
+
+def test_placement_uses_node_vram_label():
+    from mlopamd.controller import placement
+
+    small = placement.plan("llama3-70b", 8192, 16, hbm_gb=96.0)  # a 96 GB part: 70B needs TP >= 2
+    assert small.tensorParallel >= 2 and small.fits
+    p = placement.plan("llama3-70b", 8192, 16, free_gpus=0)
+    assert not p.fits and "0 of 8" in p.reason
+
+
 def test_invalid_spec_reports_error():
     async def go():
         env = Env()
