@@ -191,8 +191,11 @@ class LlamaModel:
             x = ops.add_rmsnorm(m, residual, nxt, eps)
         return x
 
+    def logits_local(self, hidden: torch.Tensor) -> torch.Tensor:
+        """[n, H] -> this rank's vocab shard of the logits [n, V/TP] (model dtype)."""
+        return linear(hidden, self.lm_head)
+
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[n, H] -> full-vocab logits [n, V] in the model dtype (bf16 on GPU: the
         greedy argmax reads them directly, the sampler upcasts), gathered over TP."""
-        lg = linear(hidden, self.lm_head)
-        return self.ps.tp.all_gather(lg, dim=-1)
+        return self.ps.tp.all_gather(self.logits_local(hidden), dim=-1)

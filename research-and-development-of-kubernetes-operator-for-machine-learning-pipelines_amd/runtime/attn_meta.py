@@ -86,21 +86,36 @@ class MetaBuffers:
                  ("tile_q0", self.max_tiles), ("ptile_seq", self.max_tiles), ("ptile_q0", self.max_tiles),
                  ("q_start", max_seqs), ("q_len", max_seqs),
                  ("ctx_len", max_seqs), ("block_tables", max_seqs * max_blocks_per_seq)]
+        # ONE int32 buffer per side: [header | int32 metadata | ids (int64) | logits index (int64)],
+        # every region 64-int aligned.  One H2D ships a step; a tensor-parallel step is ONE
+        # broadcast of the device buffer (engine.StepSync: header + metadata + ids together)
+        self.HDR = 16
         self.off = {}
-        o = 0
+        o = self.HDR
         for name, n in sizes:
             self.off[name] = (o, n)
             o += (n + 63) // 64 * 64
+        meta_lo, meta_hi = self.HDR, o
+        ids_lo = o
+        o += (2 * max_tokens + 63) // 64 * 64
+        lidx_lo = o
+        o += (2 * max_seqs + 63) // 64 * 64
+        self.total = o
         pin = self.device.type == "cuda"
-        self.h = torch.zeros(o, dtype=torch.int32, pin_memory=pin)
-        self.hn = self.h.numpy()
-        self.d = torch.zeros(o, dtype=torch.int32, device=self.device)
-        self.ids_h = torch.zeros(max_tokens, dtype=torch.int64, pin_memory=pin)
+        self.hbuf = torch.zeros(o, dtype=torch.int32, pin_memory=pin)
+        self.dbuf = torch.zeros(o, dtype=torch.int32, device=self.device)
+        self.hdr_h = self.hbuf[:self.HDR]
+        self.hdr_hn = self.hdr_h.numpy()
+        # metadata views keep their old names; offsets in self.off are into the whole buffer
+        self.h, self.d = self.hbuf, self.dbuf
+        self.hn = self.hbuf.numpy()
+        self._meta_hi = meta_hi
+        self.ids_h = self.hbuf[ids_lo:ids_lo + 2 * max_tokens].view(torch.int64)
         self.ids_hn = self.ids_h.numpy()
-        self.ids_d = torch.zeros(max_tokens, dtype=torch.int64, device=self.device)
-        self.lidx_h = torch.zeros(max_seqs, dtype=torch.int64, pin_memory=pin)
+        self.ids_d = self.dbuf[ids_lo:ids_lo + 2 * max_tokens].view(torch.int64)
+        self.lidx_h = self.hbuf[lidx_lo:lidx_lo + 2 * max_seqs].view(torch.int64)
         self.lidx_hn = self.lidx_h.numpy()
-        self.lidx_d = torch.zeros(max_seqs, dtype=torch.int64, device=self.device)
+        self.lidx_d = self.dbuf[lidx_lo:lidx_lo + 2 * max_seqs].view(torch.int64)
         # partial-softmax workspace for the split-KV path (sized for the worst launch)
         # plan_partitions only splits launches with < target/2 base workgroups, so
         # tiles * n_kv * nparts stays <= ~2 * target: size for 4096 partial tiles
@@ -120,13 +135,12 @@ class MetaBuffers:
         o, cap = self.off[name]
         return self.d[o:o + (cap if n is None else n)]
 
-    def upload(self, n_ids: int, n_logits: int):
-        """One async H2D of the metadata (+ ids, logits index) on the current stream."""
-        self.d.copy_(self.h, non_blocking=True)
-        if n_ids:
-            self.ids_d[:n_ids].copy_(self.ids_h[:n_ids], non_blocking=True)
-        if n_logits:
-            self.lidx_d[:n_logits].copy_(self.lidx_h[:n_logits], non_blocking=True)
+    def upload(self, n_ids: int = 0, n_logits: int = 0):
+        """ONE async H2D of header + metadata + ids + logits index on the current stream."""
+        self.dbuf.copy_(self.hbuf, non_blocking=True)
+
+    def set_header(self, vals) -> None:
+        self.hdr_hn[:len(vals)] = vals
 
     def meta(self, num_tokens: int, num_tiles: int, n_logits: int, part_tokens: int, nparts: int,
              num_ptiles: int = 0) -> AttnMeta:

@@ -33,6 +33,7 @@ from enum import Enum
 import numpy as np
 import torch
 
+from .. import ops
 from .attn_meta import MetaBuffers, plan_partitions
 from .kv_cache import BLOCK_SIZE, BlockAllocator, KVCache, blocks_for_budget, blocks_needed, prefix_hashes
 from .sampler import Sampler, SamplingParams
@@ -43,39 +44,42 @@ KIND_STOP, KIND_EAGER, KIND_GRAPH, KIND_BARRIER = 0, 1, 2, 3
 
 
 class StepSync:
-    """Lock-step execution across a tensor-parallel group: rank 0 broadcasts
-    [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket, num_flash_tiles] and the
-    already-uploaded metadata / ids / logits-index device buffers (over RCCL
-    on GPU, gloo on CPU); every rank then runs the identical forward."""
+    """Lock-step execution across a tensor-parallel group.  Rank 0 writes
+    the step header [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket, num_flash_tiles,
+    greedy] into the head of the step's packed metadata buffer (attn_meta.MetaBuffers: header,
+    int32 metadata, ids and logits index in ONE device buffer, already uploaded by one H2D) and
+    broadcasts that buffer: ONE collective per step (RCCL on GPU, gloo on CPU); every rank then
+    runs the identical forward."""
+
+    NHDR = 9
 
     def __init__(self, group):
         self.g = group
         self.is_leader = group.rank == 0
 
-    def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0):
-        hdr = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt], dtype=torch.int64, device=eng.device)
-        self.g.broadcast(hdr, 0)
-        if kind in (KIND_STOP, KIND_BARRIER):
-            return
+    def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
         m = eng.meta
-        self.g.broadcast(m.d, 0)
-        if T:
-            self.g.broadcast(m.ids_d[:T], 0)
-        if nl:
-            self.g.broadcast(m.lidx_d[:nl], 0)
+        m.set_header([kind, T, nt, nl, part, nparts, bucket, npt, greedy])
+        if kind in (KIND_STOP, KIND_BARRIER):  # no step metadata: ship the header alone
+            m.dbuf[:m.HDR].copy_(m.hdr_h, non_blocking=True)
+        self.g.broadcast(m.dbuf, 0)
 
     def recv(self, eng):
-        hdr = torch.zeros(8, dtype=torch.int64, device=eng.device)
-        self.g.broadcast(hdr, 0)
-        kind, T, nt, nl, part, nparts, bucket, npt = hdr.tolist()
-        if kind not in (KIND_STOP, KIND_BARRIER):
-            m = eng.meta
-            self.g.broadcast(m.d, 0)
-            if T:
-                self.g.broadcast(m.ids_d[:T], 0)
-            if nl:
-                self.g.broadcast(m.lidx_d[:nl], 0)
-        return kind, T, nt, nl, part, nparts, bucket, npt
+        m = eng.meta
+        self.g.broadcast(m.dbuf, 0)
+        return tuple(m.dbuf[:self.NHDR].tolist())
+
+
+class _Tokens:
+    """Token ids chosen inside ``_execute`` (TP greedy: no logits were gathered)."""
+
+    __slots__ = ("ids",)
+
+    def __init__(self, ids):
+        self.ids = ids
+
+    def __getitem__(self, k):
+        return _Tokens(self.ids[k])
 
 
 class Status(Enum):
@@ -260,7 +264,10 @@ class Engine:
         self.profile_window = TorchProfileWindow()
         import os
 
-        tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS") == "1"
+        # TP decode graphs capture the row-parallel all-reduces (K15 one-shot kernel, or RCCL
+        # inside capture); the vocab gather runs after the replay (``_gather``).
+        # MLOP_TP_GRAPHS=0: eager TP decode (A/B)
+        tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS", "1") != "0"
         if cfg.use_graphs and self.device.type == "cuda" and tp_graphs:
             self.capture_graphs()
         self.kv.start_background_fill()  # after capture: the rest of a lazy KV arena
@@ -505,11 +512,12 @@ class Engine:
         done = [c == s.length for s, c in zip(batch, ctx)]
         T, nt, nl = self.meta.fill(rows, chunks, ctx, toks, want_logits=done)
         part, nparts = plan_partitions(nt, self.model.n_kv, max(ctx))
-        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0)
+        done_params = [s.params for s, d in zip(batch, done) if d]
+        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0,
+                              greedy=all(p.greedy for p in done_params))
         tokens = None
         if nl:
-            done_seqs = [s for s, d in zip(batch, done) if d]
-            tokens = self.sampler(logits, [s.params for s in done_seqs]).tolist()
+            tokens = self._sample(logits, done_params).tolist()
         else:
             torch.cuda.synchronize() if self.device.type == "cuda" else None
         self.stats["prefill_steps"] += 1
@@ -540,14 +548,15 @@ class Engine:
                                          p_rows, chunks, p_ctx, p_toks, want_logits=done)
         part, nparts = plan_partitions(nt, self.model.n_kv, max(int(ctx_d.max()), max(p_ctx)))
         t1 = time.perf_counter()
-        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0)
         done_seqs = [s for s, d in zip(batch, done) if d]
         dparams = self._params_of_running()
         if getattr(dparams, "all_greedy", False) and all(s.params.greedy for s in done_seqs):
             params = _ALL_GREEDY
         else:
             params = _ParamsList([s.params for s in self.running] + [s.params for s in done_seqs])
-        toks = self.sampler(logits, params).cpu().numpy().astype(np.int64)
+        logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0,
+                              greedy=getattr(params, "all_greedy", False))
+        toks = self._sample(logits, params).cpu().numpy().astype(np.int64)
         t2 = time.perf_counter()
         self.stats["mixed_steps"] += 1
         self.stats["decode_tokens"] += B
@@ -622,18 +631,20 @@ class Engine:
         last = self.r_last[rows]
         bucket = next((b for b in self.buckets if b >= B), None)
         g = self.graphs.get(bucket) if bucket is not None else None
+        params = self._params_of_running()
+        greedy = getattr(params, "all_greedy", False)
         if g is not None:
             self.meta.fill_decode(rows, ctx, last, pad_to=bucket)
             t1 = time.perf_counter()
-            logits = self._launch(KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket)[:B]
+            logits = self._launch(KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket, greedy=greedy)[:B]
             self.stats["graph_steps"] += 1
         else:
             self.meta.fill_decode(rows, ctx, last, pad_to=B)
             part, nparts = plan_partitions(B, self.model.n_kv, int(ctx.max()))
             t1 = time.perf_counter()
-            logits = self._launch(KIND_EAGER, B, B, B, part, nparts, 0)
+            logits = self._launch(KIND_EAGER, B, B, B, part, nparts, 0, greedy=greedy)
             self.stats["eager_decode_steps"] += 1
-        toks = self.sampler(logits, self._params_of_running()).cpu().numpy().astype(np.int64)
+        toks = self._sample(logits, params).cpu().numpy().astype(np.int64)
         t2 = time.perf_counter()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += B
@@ -699,27 +710,55 @@ class Engine:
         return StepOutput(s.seq_id, int(tok), reason is not None, reason)
 
     # --------------------------------------------------------- execution --
-    def _launch(self, kind: int, T: int, nt: int, nl: int, part: int, nparts: int, bucket: int):
+    def _launch(self, kind: int, T: int, nt: int, nl: int, part: int, nparts: int, bucket: int,
+                greedy: bool = False):
         """Ship this step's metadata to the device and run it.  With tensor
-        parallelism, rank 0 (the only rank that schedules) first broadcasts a
-        small header + the metadata buffers to the TP group (SURVEY §2.5 CL5);
-        the other ranks run the same ``_execute`` from ``worker_loop``."""
-        self.meta.upload(T, nl)
+        parallelism, rank 0 (the only rank that schedules) puts the step header in the
+        packed metadata buffer and broadcasts it to the TP group in ONE collective
+        (SURVEY §2.5 CL5); the other ranks run the same ``_execute`` from ``worker_loop``.
+        Returns logits, or (TP, all-greedy rows) the chosen token ids already."""
         npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
         if self.step_sync is not None:
-            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt)
-        return self._execute(kind, T, nt, nl, part, nparts, bucket, npt)
+            t0 = time.perf_counter()
+            self.meta.set_header([kind, T, nt, nl, part, nparts, bucket, npt, int(greedy)])
+            self.meta.upload(T, nl)
+            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt, int(greedy))
+            self.stats["tp_sync_us"] += int(1e6 * (time.perf_counter() - t0))
+            self.stats["tp_sync_calls"] += 1
+        else:
+            self.meta.upload(T, nl)
+        return self._execute(kind, T, nt, nl, part, nparts, bucket, npt, greedy)
 
-    def _execute(self, kind, T, nt, nl, part, nparts, bucket, npt=0):
+    def _execute(self, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
         if kind == KIND_GRAPH:
             graph, logits_buf = self.graphs[bucket]
             graph.replay()
-            return logits_buf
+            return self._gather(logits_buf, greedy)
         meta = self.meta.meta(T, nt, nl, part, nparts, npt)
         hidden = self.model.forward(self.meta.ids_d[:T], meta, self.kv)
         if nl == 0:
             return None
-        return self.model.logits(hidden[meta.logits_idx])
+        return self._gather(self.model.logits_local(hidden[meta.logits_idx]), greedy)
+
+    def _gather(self, local, greedy):
+        """Vocab-parallel LM head -> what the sampler needs (CL3).  Greedy rows need only each
+        rank's (max logit, its global index): an [n, 2] all-gather instead of the [n, V/TP]
+        logits shard per rank (70B TP=8: 16 032 columns).  Ties keep the lowest vocabulary
+        index, as an argmax over the full row does."""
+        tp = self.model.ps.tp
+        if tp.size == 1:
+            return local
+        if not greedy:
+            return tp.all_gather(local, dim=-1)
+        idx = ops.argmax(local) if local.is_cuda else local.argmax(-1)
+        val = local.gather(1, idx.view(-1, 1)).float()
+        pair = torch.cat([val, (idx.view(-1, 1) + self.model.vocab_start).float()], dim=1)  # [n, 2]
+        allp = tp.all_gather(pair.contiguous(), dim=1).view(-1, tp.size, 2)  # [n, tp, 2]
+        best = allp[:, :, 0].argmax(dim=1)  # first max: the lowest rank = the lowest vocab index
+        return _Tokens(allp[torch.arange(allp.shape[0], device=allp.device), best, 1].to(torch.int64))
+
+    def _sample(self, out, params):
+        return out.ids if isinstance(out, _Tokens) else self.sampler(out, params)
 
     def worker_loop(self):
         """Non-zero TP ranks: replay rank 0's steps until it sends STOP."""
@@ -770,11 +809,11 @@ class Engine:
                 meta = self.meta.meta(b, b, b, part, nparts)
                 ids = self.meta.ids_d[:b]
                 for _ in range(2 if bi == 0 else 1):  # warm-up (allocator, autotune, lazy init)
-                    m.logits(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                    m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
                 stream.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
-                    logits = m.logits(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                    logits = m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
                 self.graphs[b] = (g, logits)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)

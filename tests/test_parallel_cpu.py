@@ -39,25 +39,32 @@ def run_ranks(fn_name, world=2):
 PROMPTS = [[5, 9, 11, 40, 2, 7], list(range(20, 61)), [100, 3]]
 
 
-def _tp_engine(cfg_name):
+def _tp_engine(cfg_name, world=2, **overrides):
     from mlopamd.models import build_model
     from mlopamd.models.config import get_config
     from mlopamd.parallel.comm import make_parallel_state
     from mlopamd.runtime.engine import Engine, EngineConfig
     from mlopamd.runtime.sampler import SamplingParams
 
-    cfg = get_config(cfg_name)
+    cfg = get_config(cfg_name, **overrides)
     full = build_model(cfg, device="cpu", dtype=torch.float32, seed=4)
-    ps = make_parallel_state(tp_size=2, ep_size=2)
+    ps = make_parallel_state(tp_size=world, ep_size=world)
     shard = build_model(cfg, device="cpu", dtype=torch.float32, pstate=ps, seed=4).load_shard_from(full)
     ec = EngineConfig(max_num_seqs=4, max_num_batched_tokens=32, max_model_len=128, num_kv_blocks=40, use_graphs=False)
     eng = Engine(shard, ec)
     params = SamplingParams(max_tokens=6, ignore_eos=True)
+    # a sampled request alongside greedy ones: the full-logits gather path
+    sampled = [params] * (len(PROMPTS) - 1) + [SamplingParams(max_tokens=6, ignore_eos=True, temperature=0.8,
+                                                              top_k=20)]
     if ps.tp_rank == 0:
         outs = eng.generate(PROMPTS, params)
+        mixed = eng.generate(PROMPTS, sampled)
+        stats = dict(eng.stats)
         eng.shutdown()
-        ref = Engine(full, ec).generate(PROMPTS, params)
-        return {"tp": outs, "ref": ref}
+        ref_eng = Engine(full, ec)
+        ref = ref_eng.generate(PROMPTS, params)
+        ref_mixed = ref_eng.generate(PROMPTS, sampled)
+        return {"tp": outs, "ref": ref, "mixed": mixed, "ref_mixed": ref_mixed, "stats": stats}
     eng.worker_loop()
     return {"worker_steps": eng.stats["worker_steps"]}
 
@@ -97,11 +104,31 @@ def tp_mixtral(rank, world):
     return _tp_engine("tiny-mixtral")
 
 
-@pytest.mark.parametrize("fn", ["tp_llama", "tp_mixtral"])
-def test_tp2_engine_matches_tp1(fn):
-    r0, r1 = run_ranks(fn)
+def tp4_llama(rank, world):
+    return _tp_engine("tiny-llama", world)
+
+
+def tp8_llama(rank, world):  # 8 q heads so TP=8 shards them; the single kv head is replicated
+    return _tp_engine("tiny-llama", world, num_heads=8)
+
+
+def tp4_mixtral(rank, world):
+    return _tp_engine("tiny-mixtral", world)
+
+
+@pytest.mark.parametrize("fn,world", [("tp_llama", 2), ("tp_mixtral", 2), ("tp4_llama", 4),
+                                      ("tp8_llama", 8), ("tp4_mixtral", 4)])
+def test_tp_engine_matches_tp1(fn, world):
+    """TP=2/4/8 lock-step engine == TP=1 on the same weights: greedy tokens, and a batch with
+    one sampled request (same seed: the full-logits gather path feeds the same sampler)."""
+    res = run_ranks(fn, world)
+    r0 = res[0]
     assert r0["tp"] == r0["ref"]
-    assert r1["worker_steps"] > 0
+    assert r0["mixed"][:-1] == r0["ref_mixed"][:-1] and len(r0["mixed"][-1]) == 6
+    assert r0["mixed"][-1] == r0["ref_mixed"][-1]
+    # ONE metadata collective per step (packed header + metadata + ids)
+    assert r0["stats"]["tp_sync_calls"] > 0
+    assert all(r["worker_steps"] > 0 for r in res[1:])
 
 
 def ep_alltoall(rank, world):
