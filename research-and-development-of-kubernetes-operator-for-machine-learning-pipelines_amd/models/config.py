@@ -28,6 +28,13 @@ class ModelConfig:
     top_k: int = 2
     rope_scaling: dict | None = field(default=None, hash=False, compare=False)
     eos_token_id: int = 128001
+    # further end-of-sequence ids (HF eos_token_id lists, e.g. Llama-3.1-Instruct's
+    # [128001, 128008, 128009]: <|eot_id|> must stop generation too)
+    extra_eos_ids: tuple = field(default=(), hash=False, compare=False)
+
+    @property
+    def eos_ids(self) -> tuple:
+        return (self.eos_token_id, *self.extra_eos_ids)
 
     @property
     def is_moe(self) -> bool:

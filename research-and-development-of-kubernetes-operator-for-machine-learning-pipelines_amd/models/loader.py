@@ -69,17 +69,32 @@ def config_from_hf(d: dict, name: str | None = None) -> ModelConfig:
     scaling = d.get("rope_scaling")
     if scaling is None and rp.get("rope_type", "default") not in ("default", None):
         scaling = dict(rp)
+    # settings this runtime cannot serve are REJECTED, never dropped (dropping any of them
+    # gives wrong logits with no error)
+    if scaling:
+        rt = scaling.get("rope_type", scaling.get("type", "default"))
+        if rt not in ("default", "llama3"):
+            raise ValueError(f"unsupported rope_scaling type {rt!r} (supported: default, llama3)")
+    max_pos = int(d.get("max_position_embeddings", 8192))
+    sw = d.get("sliding_window")
+    if sw is not None and d.get("use_sliding_window", True) and int(sw) < max_pos:
+        raise ValueError(f"sliding_window={sw} < max_position_embeddings={max_pos}: "
+                         "sliding-window attention is not implemented")
+    for flag in ("attention_bias", "mlp_bias"):
+        if d.get(flag):
+            raise ValueError(f"{flag}=true is not supported (bias tensors are not loaded)")
     eos = d.get("eos_token_id", 2)
-    eos = eos[0] if isinstance(eos, list) else (eos if eos is not None else 2)
+    eos_all = tuple(int(e) for e in eos) if isinstance(eos, list) else ((int(eos),) if eos is not None else (2,))
+    eos = eos_all[0]
     return ModelConfig(
         name=name or d.get("_name_or_path") or arch, vocab_size=d["vocab_size"], hidden_size=H,
         intermediate_size=d["intermediate_size"], num_layers=d["num_hidden_layers"], num_heads=nh,
         num_kv_heads=d.get("num_key_value_heads") or nh, head_dim=d.get("head_dim") or H // nh,
         rope_theta=float(theta), rms_eps=float(d.get("rms_norm_eps", 1e-5)),
-        max_position=int(d.get("max_position_embeddings", 8192)),
+        max_position=max_pos,
         tie_embeddings=bool(d.get("tie_word_embeddings", False)),
         num_experts=int(d.get("num_local_experts", 0) or 0), top_k=int(d.get("num_experts_per_tok", 2)),
-        rope_scaling=scaling, eos_token_id=int(eos))
+        rope_scaling=scaling, eos_token_id=int(eos), extra_eos_ids=eos_all[1:])
 
 
 class _Tensors:

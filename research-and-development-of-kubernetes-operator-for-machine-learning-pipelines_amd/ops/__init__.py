@@ -17,21 +17,35 @@ import torch
 
 from . import reference as ref
 
-# MLOP_LIB: load another build of the extension (in-process A/B of two kernel builds on one box)
-_LIB = Path(os.environ.get("MLOP_LIB") or Path(__file__).resolve().parent / "_C.so")
+_LIB = Path(__file__).resolve().parent / "_C.so"
 _loaded = False
 
 
+class StaleExtension(RuntimeError):
+    pass
+
+
 def load(build_if_missing: bool = True) -> bool:
-    """Load the extension; build it first if it is missing and hipcc exists."""
+    """Load the in-tree extension; build it first if it is missing and hipcc exists.
+    The library carries the sha256 of the sources it was compiled from
+    (``torch.ops.mlop.src_hash``): a binary that does not match this tree's sources is
+    refused (``StaleExtension``), never run (a kernel replaces the
+    torch op once it passes; the tested ``.so`` must be the one the sources describe)."""
     global _loaded
     if _loaded:
         return True
+    from .build import source_hash
+
+    want = source_hash()
     if not _LIB.exists() and build_if_missing:
         from .build import build
 
         build()
     torch.ops.load_library(str(_LIB))
+    got = torch.ops.mlop.src_hash()
+    if got != want:
+        raise StaleExtension(f"{_LIB} was built from sources {got}, this tree is {want}: "
+                             "rebuild with `python -m mlopamd.ops.build`")
     _loaded = True
     load_gemm_table()
     return True

@@ -25,6 +25,18 @@
 //     (kBlocks) so every block advances its epoch on every call.
 //   * every poll is bounded: on timeout the block sets an error word (read by
 //     car_error) and finishes — a wedged peer never hangs the GPU.
+//
+// Memory: the IPC-exported buffer (flags AND data) is allocated UNCACHED
+// (hipExtMallocWithFlags(hipDeviceMallocUncached)).  Its lines are written by
+// REMOTE agents (peer flag stores and, under xGMI, peer reads of the data): in
+// coarse-grained hipMalloc memory this device's L2 may keep a stale copy of a
+// flag line a peer rewrote (the L2 is not coherent with other agents' stores),
+// and a poll served from that copy never sees the epoch.  Uncached memory keeps
+// every access at the memory side, as RCCL does for its flags; the messages are
+// decode-sized (<= 4 MiB), so bypassing L2 costs nothing measurable next to the
+// hop.  The release / acquire fences stay: they order this wave's own stores
+// and the flag.  If the driver refuses to IPC-export uncached memory the buffer
+// falls back to hipMalloc (car_mem_mode() reports which one is in use).
 #include "common.h"
 #include "launch.h"
 
@@ -48,6 +60,7 @@ struct Peers {
 
 struct CarState {
   int rank = 0, world = 1, device = 0;
+  int uncached = 0;  // 1: the IPC buffer is hipDeviceMallocUncached memory
   size_t max_bytes = 0;  // per parity
   uint8_t* buf = nullptr;
   uint32_t* epochs = nullptr;
@@ -154,7 +167,18 @@ long car_create(int rank, int world, long max_bytes, int device) {
   auto* s = new CarState;
   s->rank = rank, s->world = world, s->device = device, s->max_bytes = (size_t)max_bytes;
   CAR_CHECK(hipSetDevice(device));
-  CAR_CHECK(hipMalloc(&s->buf, kFlagsBytes + 2 * (size_t)max_bytes));
+  const size_t bytes = kFlagsBytes + 2 * (size_t)max_bytes;
+  if (hipExtMallocWithFlags((void**)&s->buf, bytes, hipDeviceMallocUncached) == hipSuccess) {
+    hipIpcMemHandle_t probe;
+    if (hipIpcGetMemHandle(&probe, s->buf) == hipSuccess) {
+      s->uncached = 1;
+    } else {
+      (void)hipFree(s->buf);
+      s->buf = nullptr;
+    }
+  }
+  (void)hipGetLastError();  // clear a refused uncached allocation / export
+  if (!s->buf) CAR_CHECK(hipMalloc(&s->buf, bytes));
   CAR_CHECK(hipMemset(s->buf, 0, kFlagsBytes));
   CAR_CHECK(hipMalloc(&s->epochs, kBlocks * sizeof(uint32_t)));
   CAR_CHECK(hipMemset(s->epochs, 0, kBlocks * sizeof(uint32_t)));
@@ -185,6 +209,8 @@ void car_open(long h, const void* handles) {
 }
 
 long car_max_bytes(long h) { return (long)get(h)->max_bytes; }
+
+int car_mem_mode(long h) { return get(h)->uncached; }
 
 void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st) {
   CarState* s = get(h);

@@ -523,16 +523,23 @@ void car_all_reduce(int64_t h, Tensor out, Tensor inp) {
   mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream());
 }
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
+int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
 
 }  // namespace
 
+// sha256 of the sources this library was built from (ops/build.py writes srchash.cpp)
+extern "C" const char* mlop_src_hash();
+std::string src_hash() { return std::string(mlop_src_hash()); }
+
 TORCH_LIBRARY(mlop, m) {
+  m.def("src_hash() -> str", &src_hash);
   m.def("car_create(int rank, int world, int max_bytes, int device) -> int", &car_create);
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);
   m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp) -> ()");
   m.def("car_error(int h) -> int", &car_error);
+  m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);

@@ -53,6 +53,11 @@ class CustomAllReduce:
         torch.ops.mlop.car_all_reduce(self.h, out, x)
         return out
 
+    @property
+    def uncached(self) -> bool:
+        """True when the IPC buffer (flags + data) is uncached device memory (allreduce.hip)."""
+        return bool(torch.ops.mlop.car_mem_mode(self.h))
+
     def error(self) -> int:
         """Non-zero if any call timed out waiting for a peer (the result is then invalid)."""
         return int(torch.ops.mlop.car_error(self.h))

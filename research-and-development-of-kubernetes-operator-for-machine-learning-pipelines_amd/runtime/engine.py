@@ -401,8 +401,11 @@ class Engine:
         return out
 
     def _step(self):
-        if self.alloc.available < self.alloc.num_blocks:  # lazily backed KV chunks became ready
-            self.alloc.grow(self.kv.ready_blocks())
+        if self.alloc.available < self.alloc.num_blocks and not self.kv.fill_failed:
+            self.alloc.grow(self.kv.ready_blocks())  # lazily backed KV chunks became ready
+            if self.kv.fill_failed:
+                self.stats["kv_fill_failed"] = 1
+                self.stats["kv_blocks_backed"] = self.alloc.available
         if self._want_prefill():
             if self.running and self.cfg.mixed_prefill:
                 kind, out = "mixed", self._mixed_step()
@@ -440,6 +443,10 @@ class Engine:
                 self._release(seq)  # matched prefix pages back to the cache, row freed
                 break
             self.waiting.popleft()
+            # prefix-cache stats once per admission (a head request that waits for pages
+            # re-matches every step and must not inflate the hit rate)
+            self.stats["prefix_query_tokens"] += seq.length
+            self.stats["prefix_hit_tokens"] += seq.num_cached
             seq.status = Status.PREFILL
             self.prefilling.append(seq)
             batch.append(seq)
@@ -451,11 +458,10 @@ class Engine:
         """Reuse cached pages of this sequence's longest cached prefix (never the page
         holding its last token: that one is computed to get the next-token logits)."""
         nfull = (seq.length - 1) // BLOCK_SIZE
-        self.stats["prefix_query_tokens"] += seq.length
         if nfull <= 0:
             return
         if len(seq.hashes) < nfull:
-            prev = seq.hashes[-1] if seq.hashes else 0
+            prev = seq.hashes[-1] if seq.hashes else b""
             seq.hashes += prefix_hashes(seq.tokens(0, nfull * BLOCK_SIZE), nfull, len(seq.hashes), prev)
         m = 0
         for h in seq.hashes[:nfull]:
@@ -470,7 +476,6 @@ class Engine:
             self.r_nblk[seq.row] = m
             seq.num_cached = m * BLOCK_SIZE
             seq.n_reg = m
-            self.stats["prefix_hit_tokens"] += m * BLOCK_SIZE
 
     def _register_prefix(self, seq: Sequence, ctx: int) -> None:
         """Publish the pages this prefill filled (full pages of computed tokens)."""
@@ -478,7 +483,7 @@ class Engine:
         if full <= seq.n_reg:
             return
         if len(seq.hashes) < full:
-            prev = seq.hashes[-1] if seq.hashes else 0
+            prev = seq.hashes[-1] if seq.hashes else b""
             seq.hashes += prefix_hashes(seq.tokens(0, full * BLOCK_SIZE), full, len(seq.hashes), prev)
         for i in range(seq.n_reg, full):
             self.alloc.register(seq.blocks[i], seq.hashes[i])
@@ -662,7 +667,9 @@ class Engine:
         self.r_gen[rows] += 1
         self.r_last[rows] = toks
         fin_len = (self.r_gen[rows] >= self.r_maxgen[rows]) | (self.r_len[rows] >= self.max_model_len)
-        fin_stop = (~self.r_ignore[rows]) & (toks == self.model.cfg.eos_token_id)
+        eos = self.model.cfg.eos_ids
+        is_eos = (toks == eos[0]) if len(eos) == 1 else np.isin(toks, eos)
+        fin_stop = (~self.r_ignore[rows]) & is_eos
         run = self.running
         hs = np.nonzero(self.r_hasstop[rows])[0]
         for i in hs.tolist():
@@ -697,7 +704,7 @@ class Engine:
             s.first_token_time = time.perf_counter()
         p = s.params
         reason = None
-        if (not p.ignore_eos and tok == self.model.cfg.eos_token_id) or tok in p.stop_token_ids:
+        if (not p.ignore_eos and tok in self.model.cfg.eos_ids) or tok in p.stop_token_ids:
             reason = "stop"
         elif len(s.output) >= p.max_tokens:
             reason = "length"

@@ -84,6 +84,7 @@ def _worker(rank, world, port, out_dir):
             res["graph"].append(torch.equal(outs[0].cpu(), _oracle(xs0)) and
                                 torch.equal(outs[1].cpu(), _oracle(xs1)))
         res["error"] = car.error()
+        res["uncached"] = car.uncached
     finally:
         torch.cuda.synchronize()
         dist.barrier()
@@ -101,6 +102,8 @@ def test_custom_all_reduce_two_processes_one_gpu():
     for r in range(world):
         res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
         assert res["error"] == 0, f"rank {r}: a flag wait timed out"
+        # the flags a peer rewrites live in uncached memory (no stale L2 copy can be polled)
+        assert res["uncached"], f"rank {r}: IPC buffer fell back to cached hipMalloc memory"
         assert all(res["eager"]), (r, res["eager"])
         assert all(res["inplace"]), (r, res["inplace"])
         assert all(res["graph"]), (r, res["graph"])

@@ -299,3 +299,55 @@ def test_running_rows_bookkeeping_randomized(tiny, mixed):
         ref = greedy_ref(tiny, s.prompt, len(s.output))
         assert s.output == ref
     assert eng.alloc.num_free == eng.alloc.num_blocks - 1
+
+
+def test_prefix_keys_are_cryptographic_digests():
+    """Page keys are chained BLAKE2b digests of the token ids (not Python hash()): different
+    pages never share a key in practice, equal prefixes always do, and the chain makes a
+    page's key depend on every earlier token."""
+    from mlopamd.runtime.kv_cache import BLOCK_SIZE, prefix_hashes
+
+    a = list(range(3 * BLOCK_SIZE))
+    b = list(a)
+    b[1] = 10**9  # differs in page 0 only
+    ha, hb = prefix_hashes(a, 3), prefix_hashes(b, 3)
+    assert all(isinstance(h, bytes) and len(h) == 16 for h in ha)
+    assert all(x != y for x, y in zip(ha, hb))  # the chain carries page 0's difference forward
+    assert prefix_hashes(a, 3) == ha and prefix_hashes(a, 3, start=1, prev=ha[0]) == ha[1:]
+    # Python's tuple hash of small ints collides for these (-1 and -2 hash alike); the digest does not
+    c, d = [-1] * BLOCK_SIZE, [-2] * BLOCK_SIZE
+    assert hash(tuple(c)) == hash(tuple(d)) and prefix_hashes(c, 1) != prefix_hashes(d, 1)
+
+
+def test_kv_background_fill_failure_keeps_serving(tiny):
+    """A lazily backed KV arena whose background fill fails (another process took the memory)
+    stops growing; the engine keeps serving from the pages already backed and records it."""
+    eng = Engine(tiny, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, max_model_len=256,
+                                    num_kv_blocks=64, use_graphs=False))
+    eng.alloc = BlockAllocator(64, available=24)  # only 24 pages backed so far
+    calls = {"n": 0}
+
+    def ready_blocks():
+        calls["n"] += 1
+        eng.kv.fill_failed = True  # the native worker reported an out-of-memory chunk
+        return 32  # chunks backed before the failure stay usable
+
+    eng.kv.ready_blocks = ready_blocks
+    outs = eng.generate([[5, 6, 7, 8], list(range(20, 60))], SamplingParams(max_tokens=8, ignore_eos=True))
+    assert [len(o) for o in outs] == [8, 8]
+    assert eng.stats["kv_fill_failed"] == 1 and eng.alloc.available == 32 and calls["n"] == 1
+    assert outs[0] == greedy_ref(tiny, [5, 6, 7, 8], 8)
+
+
+def test_multiple_eos_ids_stop_generation(tiny):
+    """HF eos_token_id lists (Llama-3.1-Instruct: <|end_of_text|>, <|eom_id|>, <|eot_id|>) all stop."""
+    import dataclasses
+
+    prompt = [5, 9, 11]
+    free = greedy_ref(tiny, prompt, 6)
+    m = build_model(dataclasses.replace(TINY_LLAMA, eos_token_id=499, extra_eos_ids=(free[2],)), device="cpu",
+                    dtype=torch.float32, seed=1)
+    eng = Engine(m, EngineConfig(max_num_seqs=2, max_num_batched_tokens=32, max_model_len=128, num_kv_blocks=32,
+                                 use_graphs=False))
+    (out,) = eng.generate([prompt], SamplingParams(max_tokens=6))
+    assert out == free[:3]

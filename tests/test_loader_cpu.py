@@ -162,3 +162,20 @@ def test_operator_deploys_hf_checkpoint_end_to_end(tmp_path):
     body = asyncio.run(asyncio.wait_for(go(), 300))
     assert body["output_ids"] == expect
     assert body["text_output"] == tok.decode(expect, skip_special_tokens=True)
+
+
+@pytest.mark.parametrize("patch,msg", [
+    ({"rope_scaling": {"rope_type": "yarn", "factor": 4.0}}, "rope_scaling"),
+    ({"rope_scaling": {"type": "linear", "factor": 2.0}}, "rope_scaling"),
+    ({"sliding_window": 4096, "max_position_embeddings": 32768}, "sliding_window"),
+    ({"attention_bias": True}, "attention_bias"),
+    ({"mlp_bias": True}, "mlp_bias"),
+])
+def test_unservable_settings_are_rejected(patch, msg):
+    base = {"architectures": ["LlamaForCausalLM"], "hidden_size": 256, "num_attention_heads": 2,
+            "vocab_size": 512, "intermediate_size": 512, "num_hidden_layers": 1}
+    with pytest.raises(ValueError, match=msg):
+        loader.config_from_hf(dict(base, **patch))
+    cfg = loader.config_from_hf(dict(base, sliding_window=None, attention_bias=False,
+                                     eos_token_id=[128001, 128008, 128009]))
+    assert cfg.eos_ids == (128001, 128008, 128009)
