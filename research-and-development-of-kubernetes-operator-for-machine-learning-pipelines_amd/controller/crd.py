@@ -61,7 +61,9 @@ class CanaryPolicy:
     # GPU-side guards {metric: max new/old ratio} over prometheus.gpu_guard_queries;
     # skipped for predictors that do not export the series (reference runtimes)
     gpu_guards: dict = field(default_factory=lambda: {
-        "tpot_avg": 1.10, "gpu_memory_used": 1.30, "gpu_power": 1.25})
+        "tpot_avg": 1.10, "gpu_memory_used": 1.30, "gpu_power": 1.25,
+        # kernel-time shares from the pods' in-process profiler (runtime.gpu_metrics)
+        "attention_share": 1.5})
 
     @classmethod
     def from_spec(cls, spec: dict) -> "CanaryPolicy":

@@ -292,7 +292,8 @@ class SimLauncher:
     Seldon executor would (cumulative histogram buckets, counts per code).
     ``profiles[version] = {"latency": s, "error_rate": f, "startup_s": s}``; an LLM
     predictor profile may add ``tpot`` (s per output token), ``gpu_mem`` (bytes)
-    and ``gpu_power`` (W): the runtime's TPOT histogram and amd-smi gauges.
+    and ``gpu_power`` (W): the runtime's TPOT histogram and amd-smi gauges, and
+    ``kernel_shares`` ({class: fraction}): the in-process kernel-time gauge.
     Fault injection: ``fail_start`` (message: the predictor dies while starting, e.g.
     "HIP out of memory"), ``crash_after_s`` (it dies that long after becoming ready;
     ``crashes`` = how many times, default forever: a crash loop)."""
@@ -362,6 +363,8 @@ class SimLauncher:
                 self.store.add("mlop_gpu_memory_used_bytes", dict(lbl, gpu="0"), float(prof["gpu_mem"]), t)
             if "gpu_power" in prof:
                 self.store.add("mlop_gpu_power_watts", dict(lbl, gpu="0"), float(prof["gpu_power"]), t)
+            for k, v in (prof.get("kernel_shares") or {}).items():  # in-process profiler shares
+                self.store.add("mlop_kernel_time_fraction", dict(lbl, kernel=k), float(v), t)
             await self.clock.sleep(self.period)
 
     async def stop(self, pod: Pod):

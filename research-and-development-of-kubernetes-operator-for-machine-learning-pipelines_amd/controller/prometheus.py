@@ -51,6 +51,9 @@ GPU_MEM = "mlop_gpu_memory_used_bytes"
 GPU_POWER = "mlop_gpu_power_watts"
 
 
+KERNEL_SHARE = "mlop_kernel_time_fraction"
+
+
 def gpu_guard_queries(deployment_name: str, predictor_name: str, namespace: str, window: int = 60) -> dict:
     """Extra per-predictor series for the canary gate ("plus amd-smi /
     rocprof series"): mean time per output token from the LLM runtime's TPOT
@@ -63,6 +66,10 @@ def gpu_guard_queries(deployment_name: str, predictor_name: str, namespace: str,
         "tpot_avg": f"sum(increase({TPOT_HIST}_sum{{{sel}}}{w})) / sum(increase({TPOT_HIST}_count{{{sel}}}{w}))",
         "gpu_memory_used": f"max(max_over_time({GPU_MEM}{{{sel}}}{w}))",
         "gpu_power": f"avg(avg_over_time({GPU_POWER}{{{sel}}}{w}))",
+        # in-process rocprof-style kernel-time shares (runtime.gpu_metrics.KernelTimeSampler):
+        # a version whose attention or GEMM share of device time grew regressed on the GPU
+        "attention_share": f'avg(avg_over_time({KERNEL_SHARE}{{{sel}, kernel="attention"}}{w}))',
+        "gemm_share": f'avg(avg_over_time({KERNEL_SHARE}{{{sel}, kernel="gemm"}}{w}))',
     }
 
 

@@ -68,40 +68,54 @@ def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int
     return ops.moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps)
 
 
-def moe_forward(x, router_w, w13, w2, top_k: int, ep, e0: int, n_local: int, mode: str = "allreduce"):
+def moe_forward(x, router_w, w13, w2, top_k: int, ep, e0: int, n_local: int, mode: str = "allreduce",
+                cap_tokens: int | None = None):
     topw, topi = route(x, router_w, top_k)
     if ep.size == 1 or mode == "allreduce":
         return local_experts(x, topw, topi, w13, w2, e0, n_local)
-    return _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local)
+    return _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local, cap_tokens)
 
 
-def _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local):
-    """Expert-parallel MoE with RCCL all-to-all dispatch and combine."""
+def _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local, cap_tokens: int | None = None):
+    """Expert-parallel MoE (DP attention: every rank holds different tokens) with all-to-all
+    dispatch and combine and NO host synchronisation (graph-capturable, CL4):
+
+      * this rank's routed rows are grouped by DESTINATION rank with the MoE permute kernel
+        (K12, the owning rank standing in for the expert), then scattered into a fixed-capacity
+        send buffer [P, C, H], C = cap_tokens * top_k (the worst case: every routed row of
+        a rank goes to one peer), with each row's local expert id beside it (-1 = padding);
+      * ONE equal-split all_to_all_single of rows (+ one of ids): no counts ever reach the
+        host (RCCL over xGMI on GPU; the old path synced ``send_counts.tolist()``);
+      * the received rows run through this rank's experts in ONE grouped GEMM pair (K13;
+        padding rows carry expert -1 and are skipped by the permute);
+      * the outputs go back with a second all-to-all into the same slots and the top-k
+        weighted combine (K14) reads them in place.
+    ``cap_tokens`` must be the same on every rank of the group (the engine agrees on the
+    step's largest token count); default: this rank's T.  The exchange is exact (no token
+    is dropped); its price is P x C rows per direction instead of the routed rows."""
     import torch.distributed as dist
 
     T, H = x.shape
-    P = ep.size
-    flat_e = topi.reshape(-1).long()                      # [T*k]
-    dest = flat_e // n_local                              # owning rank of each routed row
-    order = torch.argsort(dest, stable=True)
-    send_rows = x.index_select(0, order // top_k)         # [T*k, H] grouped by destination
-    send_e = (flat_e[order] % n_local).to(torch.int32)    # local expert id at the destination
-    send_counts = torch.bincount(dest, minlength=P)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=ep.handle)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    n_recv = sum(rc)
-    recv_rows = torch.empty(n_recv, H, dtype=x.dtype, device=x.device)
-    recv_e = torch.empty(n_recv, dtype=torch.int32, device=x.device)
-    dist.all_to_all_single(recv_rows, send_rows, rc, sc, group=ep.handle)
-    dist.all_to_all_single(recv_e, send_e, rc, sc, group=ep.handle)
-    # compute the received rows with the local experts (weight 1: scaled at the source)
-    ones = torch.ones(n_recv, 1, dtype=torch.float32, device=x.device)
-    y = local_experts(recv_rows, ones, recv_e.view(-1, 1), w13, w2, 0, n_local)
-    back = torch.empty(T * top_k, H, dtype=x.dtype, device=x.device)
-    dist.all_to_all_single(back, y, sc, rc, group=ep.handle)
-    # un-permute to [T, k, H] and apply the routing weights
-    slot_rows = torch.empty_like(back)
-    slot_rows[order] = back
-    out = (slot_rows.view(T, top_k, H).float() * topw[..., None]).sum(1)
-    return out.to(x.dtype)
+    P, k = ep.size, top_k
+    C = (T if cap_tokens is None else int(cap_tokens)) * k
+    dev = x.device
+    dest = torch.div(topi, n_local, rounding_mode="floor").to(torch.int32)  # owning rank per slot
+    xp, offs, src, inv = ops.moe_permute(x, dest, 0, P)                    # rows sorted by dest
+    n = T * k
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    d_sorted = torch.searchsorted(offs[1:].to(torch.int64), i, right=True)  # dest of sorted row i
+    pos = d_sorted * C + (i - offs.to(torch.int64)[d_sorted])               # slot in the send buffer
+    send = torch.zeros(P * C, H, dtype=x.dtype, device=dev)
+    send.index_copy_(0, pos, xp[:n])
+    e_loc = torch.full((P * C,), -1, dtype=torch.int32, device=dev)
+    e_loc.index_copy_(0, pos, torch.remainder(topi.reshape(-1)[src[:n].long()], n_local).to(torch.int32))
+    recv = torch.empty_like(send)
+    recv_e = torch.empty_like(e_loc)
+    dist.all_to_all_single(recv, send, group=ep.handle)
+    dist.all_to_all_single(recv_e, e_loc, group=ep.handle)
+    ones = torch.ones(P * C, 1, dtype=torch.float32, device=dev)
+    y = local_experts(recv, ones, recv_e.view(-1, 1), w13, w2, 0, n_local)  # padding rows -> 0
+    back = torch.empty_like(y)
+    dist.all_to_all_single(back, y, group=ep.handle)
+    y_sorted = back.index_select(0, pos)                                     # dest-sorted order
+    return ops.moe_combine(y_sorted, inv, topw)

@@ -83,6 +83,10 @@ class LLMBackend:
         self._stop = False
         self._thread = threading.Thread(target=self._loop, name="mlop-engine", daemon=True)
         self.steps = 0
+        from .gpu_metrics import KernelTimeSampler
+
+        # one profiled engine step per period -> mlop_kernel_time_fraction{kernel=...}
+        self.ktime = KernelTimeSampler(on_shares=metrics.update_kernel_shares if metrics is not None else None)
 
     @property
     def ready(self) -> bool:
@@ -113,9 +117,11 @@ class LLMBackend:
                 self._wake.wait(0.05)
                 self._wake.clear()
                 continue
+            self.ktime.before_step(time.perf_counter())
             outs = eng.step()
             self.steps += 1
             now = time.perf_counter()
+            self.ktime.after_step(now)
             for o in outs:
                 r = self._active.get(o.seq_id)
                 if r is None:

@@ -1,13 +1,21 @@
 """GPU telemetry for the per-pod exporter (G3): amd-smi, with a sysfs fallback.
 
-``sample()`` returns one dict per visible GPU: busy %, HBM used / total,
-socket power.  Source order: the ``amdsmi`` Python bindings shipped with ROCm
-(/opt/rocm/share/amd_smi), then the amdgpu sysfs files
-(gpu_busy_percent, mem_info_vram_used/total).  Everything is best-effort: a
-box without either reports nothing rather than failing the runtime.
+``sample()`` returns one dict per GPU OF THIS POD: busy %, HBM used / total,
+socket power.  The pod's GPUs are the devices the device plugin exported to it
+(``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES``; every GPU when unset), so on
+an 8-GPU node each predictor exports only its own cards and the canary's HBM /
+power guards compare pods, not node totals.  Source order: the ``amdsmi``
+Python bindings shipped with ROCm (/opt/rocm/share/amd_smi), then the amdgpu
+sysfs files (gpu_busy_percent, mem_info_vram_used/total).  Everything is
+best-effort: a box without either reports nothing rather than failing the
+runtime.
 
-``KernelTimeSampler`` turns a rocprofv3 ``*_kernel_stats.csv`` into per-class
-time shares (gemm / attention / norm / other) for the same exporter.
+``KernelTimeSampler`` profiles one engine step every ``period_s`` seconds in
+process (torch.profiler over roctracer: the same kernel records rocprofv3
+reads) and turns the kernels' device time into per-class shares (gemm /
+attention / norm / rope_cache / moe / sampling / other) for the
+``mlop_kernel_time_fraction`` gauge the canary gate can guard on;
+``kernel_shares`` does the same for a rocprofv3 ``*_kernel_stats.csv``.
 """
 from __future__ import annotations
 
@@ -36,9 +44,23 @@ def _init_amdsmi():
     return _amdsmi or None
 
 
+def visible_devices() -> list[int] | None:
+    """Physical indices of the GPUs this process (pod) was given, or None (all of them)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != "":
+            try:
+                return [int(x) for x in v.split(",") if x.strip()]
+            except ValueError:  # UUID-style lists: cannot map, report nothing rather than the node
+                return []
+    return None
+
+
 def _sysfs() -> list[dict]:
     out = []
-    for i, dev in enumerate(sorted(glob.glob("/sys/class/drm/card*/device"))):
+    cards = [d for d in sorted(glob.glob("/sys/class/drm/card*/device"))
+             if os.path.exists(os.path.join(d, "gpu_busy_percent"))]
+    for i, dev in enumerate(cards):
         def rd(name):
             try:
                 with open(os.path.join(dev, name)) as f:
@@ -53,7 +75,15 @@ def _sysfs() -> list[dict]:
     return out
 
 
-def sample() -> list[dict]:
+def sample(devices: list[int] | None = ...) -> list[dict]:
+    """One dict per GPU of this pod (``devices``: physical indices; default: the visible set)."""
+    if devices is ...:
+        devices = visible_devices()
+    keep = (lambda i: True) if devices is None else (lambda i: i in devices)
+    return [d for d in _sample_all() if keep(d["gpu"])]
+
+
+def _sample_all() -> list[dict]:
     smi = _init_amdsmi()
     if smi is not None:
         out = []
@@ -110,3 +140,57 @@ def kernel_shares(stats_csv: str) -> dict:
             c = classify_kernel(r["Name"])
             by[c] = by.get(c, 0.0) + t
     return {k: v / tot for k, v in by.items()} if tot else {}
+
+
+def shares_from_events(events) -> dict:
+    """{class: fraction of device time} from (kernel name, device microseconds) pairs."""
+    tot, by = 0.0, {}
+    for name, us in events:
+        if us <= 0:
+            continue
+        tot += us
+        c = classify_kernel(name)
+        by[c] = by.get(c, 0.0) + us
+    return {k: v / tot for k, v in by.items()} if tot else {}
+
+
+class KernelTimeSampler:
+    """In-process kernel-time shares: every ``period_s`` the serving loop wraps ONE engine step
+    in ``torch.profiler`` (HIP activity) and publishes the per-class device-time shares.  One
+    profiled step per period keeps the overhead to that step; the shares of a mixed / decode
+    step are what a rocprof window of the pod would show."""
+
+    def __init__(self, period_s: float | None = None, on_shares=None):
+        self.period_s = float(os.environ.get("MLOP_KERNEL_SAMPLE_S", 30.0) if period_s is None else period_s)
+        self.on_shares = on_shares
+        self.last: dict = {}
+        self._next = 0.0
+        self._prof = None
+
+    def before_step(self, now: float) -> None:
+        if self.period_s <= 0 or now < self._next or self._prof is not None:
+            return
+        import torch
+
+        if not torch.cuda.is_available():
+            return
+        self._prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA])
+        self._prof.__enter__()
+
+    def after_step(self, now: float) -> dict | None:
+        if self._prof is None:
+            return None
+        import torch
+
+        torch.cuda.synchronize()
+        self._prof.__exit__(None, None, None)
+        ev = [(e.key, float(getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)))
+              for e in self._prof.key_averages()]
+        self._prof = None
+        self._next = now + self.period_s
+        shares = shares_from_events(ev)
+        if shares:
+            self.last = shares
+            if self.on_shares is not None:
+                self.on_shares(shares)
+        return shares

@@ -78,5 +78,10 @@ class RuntimeMetrics:
             if s.get("power_w") is not None:
                 self.gpu_power.labels(**self.lv(gpu=g)).set(s["power_w"])
 
+    def update_kernel_shares(self, shares: dict):
+        """Per-class kernel-time shares (runtime.gpu_metrics.KernelTimeSampler)."""
+        for k in ("gemm", "attention", "norm", "rope_cache", "moe", "sampling", "other"):
+            self.kernel_time.labels(**self.lv(kernel=k)).set(float(shares.get(k, 0.0)))
+
     def exposition(self) -> bytes:
         return generate_latest(self.registry)

@@ -215,6 +215,11 @@ def build_backend(runtime: str, model_uri: str | None, architecture: str | None,
     dtype = {"float32": torch.float32, "bfloat16": torch.bfloat16}[os.environ.get("MLOP_DTYPE", "bfloat16")]
     eng = build_engine(architecture or "llama3-8b", device=device, seed=seed, tp_state=tp_state,
                        model_uri=model_uri, dtype=dtype, **(engine_kwargs or {}))
+    from .. import ops
+
+    # serving must never time GEMM candidates mid-request (a canary's latency would spike on
+    # every first-seen batch size): decide from the shipped table / nearest tuned row count
+    ops.freeze_autotune()
     if metrics is not None:
         metrics.load_seconds.labels(**metrics.labels).set(time.perf_counter() - t0)
         metrics.ready.labels(**metrics.labels).set(1)

@@ -205,6 +205,30 @@ def test_gpu_guard_hbm_regression_rolls_back():
     run(go())
 
 
+@pytest.mark.parametrize("new_attn,expect", [(0.30, "Promoted"), (0.60, "RolledBack")])
+def test_kernel_share_guard(new_attn, expect):
+    """The gate consumes the pods' kernel-time shares (mlop_kernel_time_fraction, the
+    in-process profiler's rocprof-style classes): a version whose attention kernels take
+    more than 1.5x the old share of device time is rolled back even with equal latency."""
+    async def go():
+        old = {"latency": 0.05, "kernel_shares": {"gemm": 0.65, "attention": 0.25, "other": 0.10}}
+        new = {"latency": 0.05, "kernel_shares": {"gemm": 0.65 - (new_attn - 0.25), "attention": new_attn,
+                                                  "other": 0.10}}
+        env = Env(profiles={"1": old, "2": new})
+        env.reg.set_alias("m", "champion", env.version())
+        await env.start()
+        await env.create_cr()
+        assert await env.run_until(lambda: _ready(env))
+        env.reg.set_alias("m", "champion", env.version())
+        assert await env.run_until(lambda: _phase(env, "RolledBack", "Promoted"), 3000)
+        st = await env.status()
+        assert st["phase"] == expect
+        if expect == "RolledBack":
+            assert "attention_share" in st["error"]
+        await env.stop()
+    run(go())
+
+
 def test_reference_mode_no_rollback_leaves_split():
     async def go():
         env = Env(profiles={"1": {"latency": 0.05}, "2": {"error_rate": 0.5, "latency": 0.05}}, rollback=False)

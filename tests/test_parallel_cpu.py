@@ -147,7 +147,7 @@ def ep_alltoall(rank, world):
     assert ps.tp.size == 1 and ep.size == world and ep.rank == rank
     nl = E // world
     out = moe_forward(xs[rank], router, w13[rank * nl:(rank + 1) * nl], w2[rank * nl:(rank + 1) * nl], k, ep,
-                      rank * nl, nl, mode="alltoall")
+                      rank * nl, nl, mode="alltoall", cap_tokens=max(x.shape[0] for x in xs))
     # single-rank reference with all experts
     topw, topi = ops.moe_route(torch.nn.functional.linear(xs[rank], router), k)
     ref = local_experts(xs[rank], topw, topi, w13, w2, 0, E)
@@ -174,3 +174,45 @@ def collectives(rank, world):
 def test_group_collectives():
     for r in run_ranks("collectives"):
         assert r["ar"] == [[3.0] * 3] * 2 and r["ag"] == [[0, 1]] and r["b"] == 0.0
+
+
+def _ep_engine(rank, world):
+    """DP attention + EP MoE (config 5): every rank schedules its OWN requests; the MoE
+    layers exchange routed rows with sync-free fixed-capacity all-to-alls."""
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    cfg = get_config("tiny-mixtral")
+    full = build_model(cfg, device="cpu", dtype=torch.float32, seed=4)
+    ps = make_parallel_state(tp_size=1, ep_size=world)
+    assert ps.tp.size == 1 and ps.ep.size == world and ps.ep_cpu is not None
+    shard = build_model(cfg, device="cpu", dtype=torch.float32, pstate=ps, seed=4).load_shard_from(full)
+    assert shard.n_local_experts == cfg.num_experts // world
+    ec = EngineConfig(max_num_seqs=4, max_num_batched_tokens=32, max_model_len=128, num_kv_blocks=40,
+                      use_graphs=False)
+    # uneven load: rank 0 gets three prompts (one long: chunked prefill), the last rank none
+    mine = {0: PROMPTS, 1: [[7, 8, 9, 10, 11]]}.get(rank, []) if rank < world - 1 or world == 2 else []
+    params = SamplingParams(max_tokens=6, ignore_eos=True)
+    eng = Engine(shard, ec)
+    outs = eng.generate(mine, params)
+    ref = Engine(full, ec).generate(mine, params) if mine else []
+    return {"ep": outs, "ref": ref, "idle_steps": eng.stats["ep_idle_steps"]}
+
+
+def ep2_engine(rank, world):
+    return _ep_engine(rank, world)
+
+
+def ep4_engine(rank, world):
+    return _ep_engine(rank, world)
+
+
+@pytest.mark.parametrize("fn,world", [("ep2_engine", 2), ("ep4_engine", 4)])
+def test_ep_engine_matches_single_rank(fn, world):
+    res = run_ranks(fn, world)
+    for r in res:
+        assert r["ep"] == r["ref"]
+    assert res[-1]["idle_steps"] > 0  # the idle rank joined every step's all-to-alls

@@ -213,3 +213,32 @@ def test_process_predictor_start_failure_reports_failed(tmp_path):
         assert failed and "exited" in reason and "HIP out of memory" in reason
 
     asyncio.run(asyncio.wait_for(go(), 90))
+
+
+def test_gpu_telemetry_is_per_pod(monkeypatch):
+    """Only the GPUs exported to the pod (HIP_VISIBLE_DEVICES) are reported."""
+    from mlopamd.runtime import gpu_metrics
+
+    node = [{"gpu": i, "busy_percent": 10.0 * i, "mem_used": 1e9 * i, "mem_total": 288e9, "power_w": 500.0,
+             "source": "test"} for i in range(8)]
+    monkeypatch.setattr(gpu_metrics, "_sample_all", lambda: node)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,5")
+    assert [d["gpu"] for d in gpu_metrics.sample()] == [2, 5]
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert len(gpu_metrics.sample()) == 8  # no device list: a node-level (dev box) view
+
+
+def test_kernel_time_shares_exported():
+    from mlopamd.runtime import gpu_metrics
+    from mlopamd.runtime.metrics import RuntimeMetrics
+
+    ev = [("void mlop::gemm_pp_kernel<0, false, false>(...)", 600.0), ("mlop::paged_attn_kernel<4>", 300.0),
+          ("mlop::rmsnorm_wave_kernel<8, true>", 50.0), ("Cijk_Alik_Bljk_BBS", 0.0), ("memcpy", 50.0)]
+    sh = gpu_metrics.shares_from_events(ev)
+    assert abs(sum(sh.values()) - 1.0) < 1e-9 and sh["gemm"] == 0.6 and sh["attention"] == 0.3
+    m = RuntimeMetrics(deployment="d", predictor="v1", namespace="n")
+    m.update_kernel_shares(sh)
+    txt = m.exposition().decode()
+    assert 'mlop_kernel_time_fraction{' in txt and 'kernel="attention"' in txt
