@@ -45,8 +45,11 @@ class MixtralModel(LlamaModel):
         # TP attention (tokens replicated on the EP group): partial sums, summed by the
         # layer's TP all-reduce.  DP attention (tp == 1, ep > 1): all-to-all dispatch.
         mode = "alltoall" if (self.ps.ep.size > 1 and self.ps.tp.size == 1) else "allreduce"
+        # all-to-all capacity: the group's agreed token count of this step (engine.EPSync)
+        cap = getattr(self, "moe_capacity_tokens", None)
         return moe_forward(x, L["router"], L["w13"], L["w2"], self.cfg.top_k, self.ps.ep,
-                           self.expert_start, self.n_local_experts, mode=mode)
+                           self.expert_start, self.n_local_experts, mode=mode,
+                           cap_tokens=max(cap or 0, x.shape[0]))
 
     def post_attention(self, i, o, residual, eps):
         """MoE block in the decode forward: the router / grouped GEMM take a normed x."""
@@ -77,8 +80,3 @@ class MixtralModel(LlamaModel):
                                         self.n_local_experts, residual, next_norm, eps, pre=(o, L["post_norm"]))
         return super().attn_out_mlp(i, a, residual, next_norm, eps)
 
-    def forward(self, ids, meta, kv):
-        # MoE output is already complete per token (EP combine) -> no TP all-reduce
-        # when attention runs TP=1 inside an EP group; the base forward all-reduces
-        # over the TP group which is a no-op at tp=1.
-        return super().forward(ids, meta, kv)

@@ -1108,6 +1108,8 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     launch_gemv_rope(A, lda, B, M, N, K, re, st);
     return true;
   }
+  if (g_big_variant == 4 && M >= 512 && launch_gemm4w(A, lda, B, K, nullptr, 0, M, N, K, EPI_ROPE, st, &re))
+    return true;
   Plan p = plan(M, N, K, false, 0, 0);
   if (!(p.BM == 256 && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
     float* ws = sk_buf()->ws;
@@ -1152,6 +1154,8 @@ void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ld
     }
     return;
   }
+  // variant 4: the four-wave 256x256 body (gemm4w.hip) for the large-M shapes it takes
+  if (g_big_variant == 4 && M >= 512 && launch_gemm4w(A, lda, B, ldb, C, ldc, M, N, K, epi, st, nullptr)) return;
   Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits > 1 && (long)p.splits * M * N > ws_floats) { p.splits = 1; p.k_chunk = K; }
   if (epi == EPI_NONE)

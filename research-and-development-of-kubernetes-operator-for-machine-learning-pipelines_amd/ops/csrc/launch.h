@@ -46,6 +46,11 @@ struct RopeEpi {
 // split-K reduce fused in: small-M launch_gemm_rope)
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
 long gemm_workspace_floats(int M, int N, int K, int epi);
+// four-wave 256x256 large-M GEMM body (gemm4w.hip); epi 0 none, 1 silu-mul, 3 rope (re != null).
+// false = shape not taken (nothing launched)
+bool gemm4w_supported(int M, int N, int K, int lda, int ldb);
+bool launch_gemm4w(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                   int epi, hipStream_t st, const RopeEpi* re);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);

@@ -85,6 +85,7 @@ class Group:
 class ParallelState:
     tp: Group
     ep: Group
+    ep_cpu: object = None  # gloo group over the EP ranks: per-step control (engine.EPSync)
 
     @property
     def tp_size(self) -> int:
@@ -125,6 +126,13 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
     # EP over the TP ranks (tokens replicated by TP attention, partial MoE outputs summed by
     # the TP all-reduce) or over its own block of ranks (all-to-all dispatch / combine)
     ep = tp if ep_size == tp_size else Group(rank=rank % ep_size, size=ep_size, handle=groups(ep_size))
+    ep_cpu = None
+    if ep_size > 1 and tp_size == 1:  # DP attention + EP: a CPU group for the per-step agreement
+        for start in range(0, world, ep_size):
+            ranks = list(range(start, start + ep_size))
+            h = dist.new_group(ranks, backend="gloo")
+            if rank in ranks:
+                ep_cpu = h
     car_env = os.environ.get("MLOP_CUSTOM_AR", "1")
     backend_ok = dist.get_backend(tp_handle) == "nccl" or car_env == "force"  # force: gloo + GPU tests
     if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() and backend_ok and car_env != "0":
@@ -132,4 +140,4 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
 
         tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
                                  group=tp_handle)
-    return ParallelState(tp=tp, ep=ep)
+    return ParallelState(tp=tp, ep=ep, ep_cpu=ep_cpu)

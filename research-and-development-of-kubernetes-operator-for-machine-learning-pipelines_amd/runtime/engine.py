@@ -82,6 +82,30 @@ class _Tokens:
         return _Tokens(self.ids[k])
 
 
+class EPSync:
+    """Lock-step agreement of a data-parallel-attention / expert-parallel group (config 5, CL4).
+
+    Every rank schedules its OWN requests, but each MoE layer is an all-to-all over the whole
+    group, so every rank must run a forward in the same step, with the same MoE capacity, and
+    either all replay a decode graph of the same bucket or all run eager.  Once per step every
+    rank calls ``agree`` (a 4-int MAX all-reduce on a CPU gloo group: no GPU sync):
+    [has_work, wants_eager, tokens, bucket] -> what the whole group does this step.  A rank with
+    nothing to do joins with a padding-only forward."""
+
+    def __init__(self, group, cpu_group):
+        self.g, self.cpu = group, cpu_group
+        self.last_any = 1
+
+    def agree(self, has_work: int, eager: int, tokens: int, bucket: int):
+        import torch.distributed as dist
+
+        t = torch.tensor([has_work, eager, tokens, bucket], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.cpu)
+        any_work, any_eager, t_max, b_max = t.tolist()
+        self.last_any = any_work
+        return any_work, any_eager, t_max, b_max
+
+
 class Status(Enum):
     WAITING = 0
     PREFILL = 1
@@ -207,6 +231,8 @@ class Engine:
         nb = cfg.num_kv_blocks or self._auto_blocks()
         tp = model.ps.tp
         self.step_sync = StepSync(tp) if tp.size > 1 else None
+        ep = model.ps.ep
+        self.ep_sync = EPSync(ep, model.ps.ep_cpu) if (tp.size == 1 and ep.size > 1) else None
         if tp.size > 1:  # every rank must address the same page ids: agree on the minimum
             t = torch.tensor([nb], dtype=torch.int64, device=self.device)
             import torch.distributed as dist
@@ -401,6 +427,30 @@ class Engine:
         return out
 
     def _step(self):
+        kind, out = self._step_local()
+        if self.ep_sync is not None and kind == "idle":
+            self._ep_idle()  # no local work: still join this step's all-to-alls
+        return kind, out
+
+    def _ep_idle(self):
+        """EP rank with nothing scheduled: agree, then run a padding-only forward (one row
+        that attends nothing) eagerly, or replay the agreed decode graph on padding rows."""
+        any_work, eager, t_max, bucket = self.ep_sync.agree(0, 0, 0, 0)
+        if not any_work:
+            return
+        empty = np.zeros(0, dtype=np.int32)
+        if eager or bucket not in self.graphs:
+            self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=1)
+            self.meta.upload(1, 1)
+            self.model.moe_capacity_tokens = t_max
+            self.model.forward(self.meta.ids_d[:1], self.meta.meta(1, 1, 1, 32, 1), self.kv)
+        else:
+            self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=bucket)
+            self.meta.upload(bucket, bucket)
+            self.graphs[bucket][0].replay()
+        self.stats["ep_idle_steps"] += 1
+
+    def _step_local(self):
         if self.alloc.available < self.alloc.num_blocks and not self.kv.fill_failed:
             self.alloc.grow(self.kv.ready_blocks())  # lazily backed KV chunks became ready
             if self.kv.fill_failed:
@@ -640,6 +690,7 @@ class Engine:
         greedy = getattr(params, "all_greedy", False)
         if g is not None:
             self.meta.fill_decode(rows, ctx, last, pad_to=bucket)
+            self._repad = (rows, ctx, last, int(ctx.max()))
             t1 = time.perf_counter()
             logits = self._launch(KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket, greedy=greedy)[:B]
             self.stats["graph_steps"] += 1
@@ -725,6 +776,8 @@ class Engine:
         (SURVEY §2.5 CL5); the other ranks run the same ``_execute`` from ``worker_loop``.
         Returns logits, or (TP, all-greedy rows) the chosen token ids already."""
         npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
+        if self.ep_sync is not None:
+            kind, T, nt, nl, part, nparts, bucket = self._ep_agree(kind, T, nt, nl, part, nparts, bucket)
         if self.step_sync is not None:
             t0 = time.perf_counter()
             self.meta.set_header([kind, T, nt, nl, part, nparts, bucket, npt, int(greedy)])
@@ -735,6 +788,24 @@ class Engine:
         else:
             self.meta.upload(T, nl)
         return self._execute(kind, T, nt, nl, part, nparts, bucket, npt, greedy)
+
+    def _ep_agree(self, kind, T, nt, nl, part, nparts, bucket):
+        """EP lock-step: the group's common step shape.  Someone eager -> everyone eager, MoE
+        capacity = the group's largest token count (a graph-planned decode runs its padded
+        rows eagerly); all graph -> everyone replays the largest agreed bucket (re-padded)."""
+        any_work, eager, t_max, b_max = self.ep_sync.agree(1, int(kind == KIND_EAGER), T, bucket)
+        if eager:
+            if kind == KIND_GRAPH:
+                rows, ctx, last, mctx = self._repad
+                part, nparts = plan_partitions(T, self.model.n_kv, mctx)
+                kind, nt, nl = KIND_EAGER, T, T
+            self.model.moe_capacity_tokens = t_max
+            return kind, T, nt, nl, part, nparts, 0
+        if b_max != bucket:
+            rows, ctx, last, _ = self._repad
+            self.meta.fill_decode(rows, ctx, last, pad_to=b_max)
+            self.stats["ep_repadded_steps"] += 1
+        return kind, b_max, b_max, b_max, part, nparts, b_max
 
     def _execute(self, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
         if kind == KIND_GRAPH:
@@ -812,6 +883,7 @@ class Engine:
             for bi, b in enumerate(sorted(self.buckets, reverse=True)):
                 self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=b)
                 self.meta.upload(b, b)
+                m.moe_capacity_tokens = b  # EP: every rank's graph of bucket b exchanges b rows
                 part, nparts = plan_partitions(b, m.n_kv, self.max_model_len)
                 meta = self.meta.meta(b, b, b, part, nparts)
                 ids = self.meta.ids_d[:b]
@@ -828,9 +900,16 @@ class Engine:
 
     # ------------------------------------------------------ offline API --
     def generate(self, prompts, params: SamplingParams | list | None = None):
+        """Offline batch API.  EP group: EVERY rank calls it (each with its own prompts, maybe
+        none) and the ranks keep stepping together until the whole group is done."""
         if not isinstance(params, list):
             params = [params or SamplingParams()] * len(prompts)
         seqs = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+        if self.ep_sync is not None:
+            while True:
+                self.step()
+                if self.ep_sync.last_any == 0 and all(s.status == Status.FINISHED for s in seqs):
+                    return [s.output for s in seqs]
         while any(s.status != Status.FINISHED for s in seqs):
             self.step()
         return [s.output for s in seqs]
