@@ -73,11 +73,18 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree per replica (config 4: --model llama3-70b --tp 8); "
                          "replicas = world / tp, each TP group's rank 0 schedules")
+    ap.add_argument("--http", action="store_true",
+                    help="drive the load through the deployed stack instead: operator + ProcessLauncher "
+                         "(a fresh predictor process: CR->ready includes its start-up) + V2 HTTP + Router "
+                         "(runtime/http_bench.py); the value is the served rate over the predictor's own "
+                         "engine steps")
     return ap.parse_args(argv)
 
 
 def main(argv=None):
     a = parse(argv)
+    if a.http:
+        return http_main(a)
     from mlopamd.parallel.comm import env_rank_info, init_distributed
     import torch.distributed as dist
 
@@ -180,6 +187,23 @@ def main(argv=None):
     if a.tp > 1:
         engine.shutdown()  # release the TP workers before the result gather
     _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine)
+
+
+def http_main(a):
+    """bench.py --http: one replica, the whole serving path in the loop (see runtime/http_bench.py)."""
+    from mlopamd.runtime import http_bench
+
+    r = http_bench.main(a)
+    res = {"metric": "served_tokens_per_sec", "value": r["served_tokens_per_sec_http"], "unit": "tokens/s",
+           "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": r["http_ms_per_step"],
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (random prompt tokens, random-init weights)",
+           "config": {"model": "Llama-3-8B" if a.model == "llama3-8b" else a.model, "global_batch": a.batch,
+                      "seq_len": a.prompt_len + a.output_len, "prompt_len": a.prompt_len,
+                      "output_len": a.output_len, "parallelism": "dp1", "path": "http"},
+           "p50_cr_ready_s": r["p50_cr_ready_process_s"], "http": r}
+    print(json.dumps(res), flush=True)
+    return res
 
 
 def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine):

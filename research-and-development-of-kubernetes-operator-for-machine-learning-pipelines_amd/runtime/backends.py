@@ -122,6 +122,10 @@ class LLMBackend:
             self.steps += 1
             now = time.perf_counter()
             self.ktime.after_step(now)
+            if self.metrics:
+                self.metrics.engine_steps.labels(**self.metrics.labels).inc()
+                if len(outs):
+                    self.metrics.engine_tokens.labels(**self.metrics.labels).inc(len(outs))
             for o in outs:
                 r = self._active.get(o.seq_id)
                 if r is None:

@@ -1,0 +1,147 @@
+"""The headline load driven end to end through the serving stack (``bench.py --http``).
+
+What ``bench.py`` measures by default is the engine's served rate with requests handed to
+``Engine.add_request`` in-process.  This mode puts every layer of the deployed path in the
+loop (reference serving path: the SeldonDeployment's ``protocol:
+kfserving`` endpoint, mlflow_operator.py:225-238):
+
+  1. registry -> MlflowModel CR -> operator -> SeldonDeployment -> the local Seldon stand-in
+     starts the predictor CONTAINER COMMAND as a fresh OS process (``ProcessLauncher``) on
+     this node's GPU: CR -> ready therefore includes process start, ``import torch``, HIP
+     init, weight init, KV pool and graph capture (``p50_cr_ready_process_s``);
+  2. ``--batch`` closed-loop HTTP clients (aiohttp) post V2 ``/v2/models/{m}/generate``
+     requests through the weighted ``Router`` (the Istio stand-in), first cohort at
+     staggered output lengths like the engine-direct bench;
+  3. the predictor exports ``mlop_engine_steps_total`` / ``mlop_engine_tokens_total``; after
+     ``warmup`` engine steps the window opens, and it closes after ``steps`` more: value =
+     generated tokens in the window / its wall time.
+"""
+from __future__ import annotations
+
+import asyncio
+import re
+import time
+
+import numpy as np
+
+
+async def _scrape(session, url) -> dict:
+    async with session.get(url) as r:
+        txt = await r.text()
+    out = {}
+    for name in ("mlop_engine_steps_total", "mlop_engine_tokens_total"):
+        m = re.search(rf"^{name}\{{[^}}]*\}} ([0-9.e+]+)$", txt, re.M)
+        out[name] = float(m.group(1)) if m else 0.0
+    return out
+
+
+async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256, output_len: int = 256,
+              steps: int = 20, warmup: int = 5, engine_env: dict | None = None, ready_timeout_s: float = 900.0,
+              ramp_timeout_s: float = 600.0) -> dict:
+    import aiohttp
+
+    from ..controller.app import make_operator
+    from ..controller.clock import RealClock
+    from ..controller.crd import GROUP, PLURAL, VERSION, OperatorSettings
+    from ..controller.kube import FakeKube
+    from ..controller.local import FakeSeldonController, GpuPool, ProcessLauncher, Router, mlflow_model_cr, wait_for
+    from ..controller.mlflow import LocalMlflowClient, SqliteRegistry
+    from ..controller.prometheus import LocalProm, MetricStore
+    from ..models.config import get_config
+
+    ns, name = "serving", "llm"
+    kube, reg = FakeKube(), SqliteRegistry()
+    reg.create_model_version(name, f"mlflow-artifacts:/1/{model}/artifacts/model",
+                             tags={"mlop.architecture": model, "mlop.runtime": "mlop-llm"})
+    reg.set_alias(name, "champion", 1)
+    op, _ = make_operator(kube, LocalMlflowClient(reg), LocalProm(MetricStore()), RealClock(), OperatorSettings())
+    env = {"MLOP_ENGINE_MAX_NUM_SEQS": str(batch), "MLOP_KERNEL_SAMPLE_S": "0"}
+    env.update(engine_env or {})
+    pool = GpuPool.detect()
+    launcher = ProcessLauncher(extra_env=env, gpus=pool if pool.devices else None, ready_timeout_s=ready_timeout_s)
+    ctl = FakeSeldonController(kube, launcher, RealClock()).start()
+    router = Router(ctl)
+    await op.start()
+    out: dict = {"mode": "http", "path": "operator + ProcessLauncher + V2 HTTP + Router"}
+    try:
+        t0 = time.perf_counter()
+        await kube.create(GROUP, VERSION, ns, PLURAL, mlflow_model_cr(name, ns, name, "champion",
+                                                                      maxNumSeqs=batch, maxModelLen=1024))
+
+        async def ready():
+            o = await kube.get(GROUP, VERSION, ns, PLURAL, name)
+            for p in ctl.pods.values():  # a predictor that cannot start fails the run now
+                if "error" in p.extra:
+                    raise RuntimeError(f"predictor {p.predictor} failed to start: {p.extra['error']}")
+            return (o.get("status") or {}).get("ready") == "True"
+
+        await wait_for(ready, ready_timeout_s, poll_s=0.05)
+        out["p50_cr_ready_process_s"] = round(time.perf_counter() - t0, 3)
+        pod = next(iter(ctl.pods.values()))
+        out["predictor_process_ready_s"] = round(pod.extra.get("ready_s", 0.0), 3)
+        out["predictor_gpus"] = pod.extra.get("gpus")
+        metrics_url = pod.endpoint + "/metrics"
+        V = get_config(model).vocab_size
+        rng = np.random.default_rng(1234)
+        lo = min(1000, V // 4)
+        stop = asyncio.Event()
+        stats = {"requests": 0, "errors": 0}
+
+        async def client(session, i):
+            first = 1 + (i * output_len) // batch  # staggered first cohort (steady-state age mix)
+            mt = first
+            while not stop.is_set():
+                ids = rng.integers(lo, V - lo, size=prompt_len).tolist()
+                payload = {"input_ids": ids, "parameters": {"max_tokens": int(mt), "ignore_eos": True}}
+                code, _, _ = await router.post(ns, name, f"/v2/models/{name}/generate", payload, session)
+                stats["requests"] += 1
+                if code != 200:
+                    stats["errors"] += 1
+                    await asyncio.sleep(0.05)
+                mt = output_len
+
+        conn = aiohttp.TCPConnector(limit=0)
+        async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as session:
+            tasks = [asyncio.get_running_loop().create_task(client(session, i)) for i in range(batch)]
+            # ramp: every client's first request admitted and the engine past its prefill wave
+            t_ramp = time.perf_counter()
+            base = await _scrape(session, metrics_url)
+            while time.perf_counter() - t_ramp < ramp_timeout_s:
+                await asyncio.sleep(0.5)
+                cur = await _scrape(session, metrics_url)
+                if cur["mlop_engine_tokens_total"] - base["mlop_engine_tokens_total"] >= batch:
+                    break
+            s_ramp = await _scrape(session, metrics_url)
+            while True:  # warmup steps
+                cur = await _scrape(session, metrics_url)
+                if cur["mlop_engine_steps_total"] >= s_ramp["mlop_engine_steps_total"] + warmup:
+                    break
+                await asyncio.sleep(0.01)
+            t_a, a = time.perf_counter(), cur
+            while True:  # the timed steps
+                cur = await _scrape(session, metrics_url)
+                if cur["mlop_engine_steps_total"] >= a["mlop_engine_steps_total"] + steps:
+                    break
+                await asyncio.sleep(0.005)
+            t_b, b = time.perf_counter(), cur
+            stop.set()
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+        n_steps = b["mlop_engine_steps_total"] - a["mlop_engine_steps_total"]
+        toks = b["mlop_engine_tokens_total"] - a["mlop_engine_tokens_total"]
+        out.update(served_tokens_per_sec_http=round(toks / (t_b - t_a), 2), http_window_steps=int(n_steps),
+                   http_ms_per_step=round(1e3 * (t_b - t_a) / max(n_steps, 1), 3),
+                   http_requests=stats["requests"], http_errors=stats["errors"])
+    finally:
+        await ctl.stop()
+        await op.stop()
+    return out
+
+
+def main(a) -> dict:
+    return asyncio.run(run(a.model, a.batch, a.prompt_len, a.output_len, a.steps, a.warmup,
+                           engine_env={"MLOP_ENGINE_MAX_NUM_BATCHED_TOKENS": str(a.max_batched_tokens),
+                                       "MLOP_ENGINE_MAX_MODEL_LEN": str(a.max_model_len),
+                                       "MLOP_ENGINE_PREFILL_MIN_BATCH": str(a.prefill_min_batch),
+                                       "MLOP_ENGINE_MAX_DECODE_GAP": str(a.max_decode_gap)}))

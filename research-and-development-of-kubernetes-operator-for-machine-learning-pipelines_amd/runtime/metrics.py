@@ -54,6 +54,8 @@ class RuntimeMetrics:
         self.gpu_mem = Gauge("mlop_gpu_memory_used_bytes", "HBM used", base + ["gpu"], registry=r)
         self.gpu_mem_total = Gauge("mlop_gpu_memory_total_bytes", "HBM total", base + ["gpu"], registry=r)
         self.gpu_power = Gauge("mlop_gpu_power_watts", "Socket power", base + ["gpu"], registry=r)
+        self.engine_steps = Counter("mlop_engine_steps", "Engine steps executed", base, registry=r)
+        self.engine_tokens = Counter("mlop_engine_tokens", "Tokens emitted by engine steps", base, registry=r)
         self.kernel_time = Gauge("mlop_kernel_time_fraction", "rocprof kernel-time share per kernel class",
                                  base + ["kernel"], registry=r)
 

@@ -63,3 +63,20 @@ def test_deploy_fails_fast_when_predictor_cannot_start():
         deploy_and_wait(model="tiny-llama", device="cpu", timeout_s=120.0,
                         engine_kwargs=dict(num_kv_blocks=1, use_graphs=False))
     assert time.time() - t0 < 60
+
+
+def test_http_bench_end_to_end_on_cpu():
+    """bench.py --http's driver on a tiny model: CR -> operator -> SD -> a fresh predictor
+    process (ProcessLauncher, container command) -> closed-loop V2 /generate clients through
+    the Router; the window is counted in the predictor's own engine steps."""
+    import asyncio
+
+    from mlopamd.runtime import http_bench
+
+    r = asyncio.run(http_bench.run(
+        "tiny-llama", batch=8, prompt_len=16, output_len=8, steps=10, warmup=3, ready_timeout_s=180,
+        ramp_timeout_s=60, engine_env={"MLOP_DEVICE": "cpu", "MLOP_DTYPE": "float32", "MLOP_ENGINE_USE_GRAPHS": "false",
+                                       "MLOP_ENGINE_NUM_KV_BLOCKS": "64", "MLOP_ENGINE_MAX_MODEL_LEN": "128",
+                                       "OMP_NUM_THREADS": "2"}))
+    assert r["http_window_steps"] >= 10 and r["served_tokens_per_sec_http"] > 0 and r["http_errors"] == 0
+    assert r["p50_cr_ready_process_s"] >= r["predictor_process_ready_s"] > 0
