@@ -426,9 +426,9 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
 
 
 # Residual add + RMSNorm as the decode GEMV's prologue (gemv.hip NORM).  Measured a wash at
-# batch 1 (315-318 vs 318 tok/s unfused, scripts/run41.sh: the two norm launches it removes
+# batch 1 (315-318 vs 318 tok/s unfused, scripts/history/run41.sh: the two norm launches it removes
 # cost what the heavier prologue adds to the two GEMVs) and a loss at batch 2-4, so it is
-# opt-in: MLOP_NORM_FUSION=1.  Re-measured with the K-split gate_up GEMV (scripts/run60.sh):
+# opt-in: MLOP_NORM_FUSION=1.  Re-measured with the K-split gate_up GEMV (scripts/history/run60.sh):
 # 302-306 fused vs 332-338 tok/s unfused at batch 1, 622 vs 617 at batch 2 — still off.
 NORM_FUSION = os.environ.get("MLOP_NORM_FUSION", "0") == "1"
 

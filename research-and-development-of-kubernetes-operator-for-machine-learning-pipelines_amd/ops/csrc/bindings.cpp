@@ -214,7 +214,6 @@ int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
 int64_t gemm_small_stages(int64_t set) { return mlop::gemm_small_stages((int)set); }
 int64_t gemm_small_tile(int64_t set) { return mlop::gemm_small_tile((int)set); }
-int64_t gemm_wsg_config(int64_t max_m, int64_t min_wg) { return mlop::wsg_config((int)max_m, (int)min_wg); }
 int64_t gemm_sk_mode(int64_t set) { return mlop::gemm_sk_mode((int)set); }
 bool gemm_sk_reserve() { return mlop::gemm_sk_reserve(); }
 int64_t gemm_sk_workgroups(int64_t M, int64_t N, int64_t K) { return mlop::gemm_sk_workgroups((int)M, (int)N, (int)K); }
@@ -545,7 +544,6 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
   m.def("gemm_small_tile(int set=-1) -> int", &gemm_small_tile);
-  m.def("gemm_wsg_config(int max_m=-1, int min_wg=-1) -> int", &gemm_wsg_config);
   m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);
   m.def("gemm_sk_reserve() -> bool", &gemm_sk_reserve);
   m.def("gemm_sk_workgroups(int M, int N, int K) -> int", &gemm_sk_workgroups);

@@ -652,14 +652,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     };
 
     // LDS-DMA schedule (barriers numbered along group 0; group 1 runs one behind):
-    //   A(t+1) -> buffer (t+1)&1 in phase 1 of t   (after the last A reads of t-1 retired)
+    //   A(t+1) -> buffer (t+1)&1 in phases 0 (rows 0-127) and 1 (rows 128-255) of t (the
+    //            last A reads of t-1, phase 2 of t-1, retired before group 1's phase-2 MFMAs,
+    //            i.e. before group 0's phase-3 barrier)
     //   B(t+2) -> buffer t&1     in phase 3 of t   (after B1(t), the last B read of t, retired)
     //   retire B(t+1) in phase 2 of t (vmcnt(4): A(t+1) stays in flight), read B0(t+1) in
     //   phase 3 of t into the other B0 register set; retire A(t+1) in phase 3 (vmcnt(4):
     //   B(t+2) stays in flight), read it from phase 0 of t+1.  Every read happens at least
     //   one barrier after the slower group's retirement; every DMA is issued at least one
     //   barrier after the last read of its destination retired.  Per phase a wave issues
-    //   8 / 4+4 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
+    //   8+2 / 4+2 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
 #pragma unroll
     for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
     if (nkp > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
@@ -673,9 +675,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       const int cur = t & 1, nxt = cur ^ 1;
       const bool m1 = t + 1 < nkp, m2 = t + 2 < nkp;
       read_a(cur, 0, fa);                                  // phase 0: quadrant (0,0)
+      if (m1) issue_half(nxt, 0, t + 1);
       phase_mma(0, 0, fa, fb0);
       read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
-      if (m1) { issue_half(nxt, 0, t + 1); issue_half(nxt, 1, t + 1); }
+      if (m1) issue_half(nxt, 1, t + 1);
       phase_mma(0, 1, fa, fb1);
       read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
       if (m1) wait_vmcnt<4>();
@@ -1108,8 +1111,6 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     launch_gemv_rope(A, lda, B, M, N, K, re, st);
     return true;
   }
-  if (g_big_variant == 4 && M >= 512 && launch_gemm4w(A, lda, B, K, nullptr, 0, M, N, K, EPI_ROPE, st, &re))
-    return true;
   Plan p = plan(M, N, K, false, 0, 0);
   if (!(p.BM == 256 && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
     float* ws = sk_buf()->ws;
@@ -1127,10 +1128,6 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {
   if (gemv_takes(M, N, K, epi)) return 0;
-  if (wsg_takes(M, N, K, epi)) {  // slabs for split-K, or one fp32 tile for the fused add + RMSNorm
-    const int s = wsg_splits(M, N, K, epi);
-    return (epi == EPI_NONE || s > 1) ? (long)s * M * N : 0;
-  }
   const Plan p = plan(M, N, K, false, 0, 0);
   return p.splits > 1 ? (long)p.splits * M * N : 0;
 }
@@ -1142,20 +1139,6 @@ void launch_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ld
     launch_gemv(A, lda, B, ldb, C, ldc, M, N, K, epi, st);
     return;
   }
-  if (wsg_takes(M, N, K, epi) && lda % 8 == 0 && ldb % 8 == 0) {
-    int s = wsg_splits(M, N, K, epi);
-    if (s > 1 && (long)s * M * N > ws_floats) s = 1;
-    s = launch_wsg(A, lda, B, ldb, C, ldc, s > 1 ? ws : nullptr, M, N, K, epi, s, st);
-    if (s > 1) {
-      const int outw = epi == EPI_NONE ? N : N / 2;
-      const int g = (int)std::min<long>(((long)M * (outw / 8) + 255) / 256, 4096);
-      if (epi == EPI_NONE) splitk_reduce_kernel<EPI_NONE><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, s);
-      else splitk_reduce_kernel<EPI_SILU_MUL><<<g, 256, 0, st>>>((uint16_t*)C, ldc, ws, M, N, s);
-    }
-    return;
-  }
-  // variant 4: the four-wave 256x256 body (gemm4w.hip) for the large-M shapes it takes
-  if (g_big_variant == 4 && M >= 512 && launch_gemm4w(A, lda, B, ldb, C, ldc, M, N, K, epi, st, nullptr)) return;
   Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits > 1 && (long)p.splits * M * N > ws_floats) { p.splits = 1; p.k_chunk = K; }
   if (epi == EPI_NONE)
@@ -1184,17 +1167,11 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
   if (M == 0) return true;
   if (gemv_takes(M, N, K, EPI_NONE)) return false;  // GEMV + add_rmsnorm
   int splits;
-  if (wsg_takes(M, N, K, EPI_NONE) && lda % 8 == 0) {  // fp32 slab(s) even without a K split
-    splits = wsg_splits(M, N, K, EPI_NONE);
-    if ((long)splits * M * N > ws_floats || N % 8) return false;
-    splits = launch_wsg(A, lda, B, K, nullptr, N, ws, M, N, K, EPI_NONE, splits, st);
-  } else {
-    const Plan p = plan(M, N, K, false, 0, 0);
-    if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
-    launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
-                                 M, N, K, nullptr, 0, st);
-    splits = p.splits;
-  }
+  const Plan p = plan(M, N, K, false, 0, 0);
+  if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
+  launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
+                               M, N, K, nullptr, 0, st);
+  splits = p.splits;
   const int nvec = N / 8;
   int vpt = 1;
   while (vpt < 8 && nvec / vpt > 512) vpt <<= 1;

@@ -46,11 +46,6 @@ struct RopeEpi {
 // split-K reduce fused in: small-M launch_gemm_rope)
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
 long gemm_workspace_floats(int M, int N, int K, int epi);
-// four-wave 256x256 large-M GEMM body (gemm4w.hip); epi 0 none, 1 silu-mul, 3 rope (re != null).
-// false = shape not taken (nothing launched)
-bool gemm4w_supported(int M, int N, int K, int lda, int ldb);
-bool launch_gemm4w(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
-                   int epi, hipStream_t st, const RopeEpi* re);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
@@ -75,12 +70,6 @@ struct NormPro {
   const uint16_t* w;
   float eps;
 };
-// K2' weight-streaming MFMA GEMM (wsgemm.hip): decode projections above the GEMV's rows, M <= 64
-bool wsg_takes(int M, int N, int K, int epi);
-int wsg_splits(int M, int N, int K, int epi);
-int launch_wsg(const void* A, int lda, const void* B, int ldb, void* C, int ldc, float* ws, int M, int N,
-               int K, int epi, int splits, hipStream_t st);
-int wsg_config(int max_m, int min_wg);  // set >= 0 overrides; returns max_m (0 = off)
 bool gemv_norm_takes(int M, int N, int K, int epi);
 bool gemv_grouped_takes(int M, int N, int K, int epi);
 void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,

@@ -115,9 +115,11 @@ def _sample_all() -> list[dict]:
 
 def classify_kernel(name: str) -> str:
     n = name.lower()
-    if "gemm" in n or "cijk" in n or "mfma" in n:
+    if "moe_" in n:  # routing / sort / gather / combine (the expert GEMMs are gemm_* below)
+        return "moe"
+    if any(k in n for k in ("gemm", "gemv", "cijk", "mfma", "wsg_", "splitk_reduce")):
         return "gemm"
-    if "attn" in n or "attention" in n:
+    if "attn" in n or "attention" in n or "flash" in n:
         return "attention"
     if "norm" in n:
         return "norm"
@@ -125,8 +127,6 @@ def classify_kernel(name: str) -> str:
         return "rope_cache"
     if "sample" in n or "argmax" in n:
         return "sampling"
-    if "moe" in n:
-        return "moe"
     return "other"
 
 

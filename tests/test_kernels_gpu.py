@@ -277,7 +277,12 @@ def test_argmax(gpu, n, V, dtype):
 @pytest.mark.parametrize("n,V", [(16, 32000), (4, 128256), (64, 32000), (8, 1000)])
 def test_sample_matches_reference(gpu, n, V):
     """n < 64: per-slice top-K pre-selection (16 workgroups per row) + the draw over the
-    candidates; n = 64: the single-stage kernel; same uniforms as the torch reference."""
+    candidates; n = 64: the single-stage kernel; same uniforms as the reference.
+
+    Exact, tie-safe check of EVERY row: the drawn token must be the candidate whose interval
+    [c_{j-1}, c_j) of the fp64 reference CDF (top-k, temperature, top-p renormalised) holds u.
+    Only when u or the top-p cut lies within 1e-5 of an interval edge -- where fp32 summation
+    order legitimately decides -- is the neighbouring candidate accepted as well."""
     torch.manual_seed(1)
     x = 3 * torch.randn(n, V, device=gpu)
     temps = torch.tensor([0.0, 0.7, 1.0, 1.3] * (n // 4), device=gpu)
@@ -285,16 +290,34 @@ def test_sample_matches_reference(gpu, n, V):
     ps = torch.tensor([1.0, 1.0, 0.9, 0.5] * (n // 4), device=gpu)
     u = torch.rand(n, device=gpu)
     got = ops.sample(x, temps, ks, ps, u).cpu()
-    exp = ref_sample = None
-    from mlopamd.runtime.sampler import sample_reference
+    from mlopamd.runtime.sampler import MAX_TOP_K
 
-    exp = sample_reference(x.cpu(), temps.cpu(), ks.cpu(), ps.cpu(), u.cpu())
-    assert (got == exp).float().mean() >= 0.9, (got, exp)
-    # temperature 0 and top_k 1 are exact argmax
-    am = x.argmax(-1).cpu()
+    eps = 1e-5
+    kmax = min(MAX_TOP_K, V)
+    vals, idx = torch.topk(x.cpu().double(), kmax, dim=-1)
     for i in range(n):
-        if float(temps[i]) == 0 or int(ks[i]) == 1:
-            assert int(got[i]) == int(am[i])
+        if float(temps[i]) <= 0 or int(ks[i]) == 1:  # greedy rows: exact argmax
+            assert int(got[i]) == int(idx[i, 0]), i
+            continue
+        k = min(int(ks[i]) or kmax, kmax)
+        pr = torch.softmax(vals[i, :k] / float(temps[i]), dim=-1)
+        c = torch.cumsum(pr, dim=-1)
+        pp, ui = float(ps[i]), float(u[i])
+        keeps = {k}
+        if pp < 1.0:
+            keep = min(int((c < pp).sum()) + 1, k)
+            keeps = {keep} | {kk for kk in (keep - 1, keep + 1) if 1 <= kk <= k and abs(float(c[kk - 1]) - pp) < eps}
+        ok = False
+        for keep in keeps:
+            cc = torch.cumsum(pr[:keep] / c[keep - 1], dim=-1)
+            pos = (idx[i, :keep] == int(got[i])).nonzero()
+            if pos.numel() == 0:
+                continue
+            j = int(pos[0])
+            lo = 0.0 if j == 0 else float(cc[j - 1])
+            hi = 1.0 if j == keep - 1 else float(cc[j])
+            ok |= lo - eps <= ui <= hi + eps
+        assert ok, (i, int(got[i]), ui)
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (7, 6144, 4096), (64, 4096, 14336),
@@ -351,7 +374,7 @@ def test_gemm_stream_k(gpu, M, N, K, epi):
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1280, 8192), (8192, 1024),
                                  (8192, 3584), (16, 1024)])
 def test_gemv(gpu, M, N, K):
-    """K2 skinny GEMV (gemv.hip, M <= 4; M = 5 / 8 take wsgemm.hip or the MFMA tiles): wave-per-row-pair
+    """K2 skinny GEMV (gemv.hip, M <= 4; M = 5 / 8 take the MFMA tiles): wave-per-row-pair
     (N >= 4096) and the 4-waves-split-K form (N = 1280 / 16: 70B TP=8 shards, tiny N), K
     not a multiple of the unrolled stride (1024, 3584); vs fp32 matmul."""
     torch.manual_seed(M * 7 + N + K)
@@ -406,11 +429,10 @@ def test_gemm_small_tiles(gpu, M, tile, N, K, epi):
 @pytest.mark.parametrize("M", [5, 8, 16, 17, 32, 40, 64])
 @pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (4096, 14336, 0), (7168, 4096, 1), (28672, 4096, 1),
                                      (1280, 8192, 0)])
-@pytest.mark.parametrize("min_wg", [1, 256, 4096])  # no K split / the default / forced slabs
-def test_wsg_gemm(gpu, M, N, K, epi, min_wg):
-    """K2' weight-streaming MFMA GEMM (wsgemm.hip, 4 < M <= 64): register-streamed B fragments,
-    4 waves interleaving K steps with an LDS sum, optional K split into fp32 slabs reduced by
-    gemm.hip (plain / SiLU-mul epilogue); ragged M (17, 40: clamped A rows); vs fp32 matmul."""
+def test_mid_m_gemm(gpu, M, N, K, epi):
+    """Decode projections above the GEMV's rows (4 < M <= 64): the row-fitted LDS-DMA MFMA tiles
+    with their split-K fp32 slabs reduced by gemm.hip (plain / SiLU-mul epilogue); ragged M
+    (17, 40: clamped A rows); NaN-filled workspace (every slab element must be written)."""
     torch.manual_seed(M * 13 + N + K + epi)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     if epi:
@@ -421,40 +443,10 @@ def test_wsg_gemm(gpu, M, N, K, epi, min_wg):
     else:
         w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
         exp = x.float() @ w.float().t()
-    prev = torch.ops.mlop.gemm_wsg_config()  # off by default (rejected on speed); forced on here
-    torch.ops.mlop.gemm_wsg_config(64, min_wg)
-    try:
-        y = torch.empty(M, N // 2 if epi else N, device=gpu, dtype=bf)
-        nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
-        torch.ops.mlop.gemm(y, x, w, torch.full((max(nws, 1),), float("nan"), device=gpu), epi)
-    finally:
-        torch.ops.mlop.gemm_wsg_config(prev, 256)
+    y = torch.empty(M, N // 2 if epi else N, device=gpu, dtype=bf)
+    nws = torch.ops.mlop.gemm_workspace(M, N, K, epi)
+    torch.ops.mlop.gemm(y, x, w, torch.full((max(nws, 1),), float("nan"), device=gpu), epi)
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("M", [8, 24, 64])
-@pytest.mark.parametrize("min_wg", [1, 256])
-def test_wsg_gemm_add_rmsnorm(gpu, M, min_wg):
-    """wsgemm's fp32 slab(s) (one split included) feeding the fused residual add + RMSNorm reduce."""
-    N, K = 4096, 4096
-    torch.manual_seed(M)
-    x = torch.randn(M, K, device=gpu, dtype=bf)
-    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
-    res = torch.randn(M, N, device=gpu, dtype=bf)
-    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
-    exp_out, exp_res = ref.add_rmsnorm((x.float() @ w.float().t()).to(bf), res, nw, 1e-5)
-    prev = torch.ops.mlop.gemm_wsg_config()
-    torch.ops.mlop.gemm_wsg_config(64, min_wg)
-    try:
-        nws = torch.ops.mlop.gemm_workspace(M, N, K, 0)
-        assert nws >= M * N
-        out = torch.empty(M, N, device=gpu, dtype=bf)
-        r2 = res.clone()
-        assert torch.ops.mlop.gemm_add_rmsnorm(out, r2, x, w, nw, torch.empty(nws, device=gpu), 1e-5)
-    finally:
-        torch.ops.mlop.gemm_wsg_config(prev, 256)
-    close(r2, exp_res, atol=3e-2, rtol=2e-2)
-    close(out, exp_out, atol=5e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("M", [1, 2, 4])

@@ -108,3 +108,27 @@ def test_mixtral_decode_fused_moe_glue(gpu):
     outs = eng.generate(prompts, SamplingParams(max_tokens=8, ignore_eos=True))
     assert eng.stats["graph_steps"] > 0
     _check_greedy(model, prompts, outs)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_kernel_time_sampler_on_engine_steps(gpu, graphs):
+    """G3: the in-process sampler (runtime/gpu_metrics.KernelTimeSampler, what the predictor
+    exports as mlop_kernel_time_fraction) sees this engine's HIP kernels -- eager launches and
+    decode-graph replays -- and splits them into the classes the canary gate guards."""
+    from mlopamd.runtime.gpu_metrics import KernelTimeSampler
+
+    model = build_model(TINY_LLAMA, device=gpu, seed=3)
+    eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=64, max_model_len=512,
+                                     num_kv_blocks=128, use_graphs=graphs, graph_buckets=(1, 2, 4, 8)))
+    for p in (torch.randint(2, 500, (n,)).tolist() for n in (5, 40, 17)):
+        eng.add_request(p, SamplingParams(max_tokens=12, ignore_eos=True))
+    for _ in range(3):  # past the prefill: the sampled step is a decode step
+        eng.step()
+    got = []
+    s = KernelTimeSampler(period_s=1e-6, on_shares=got.append)
+    s.before_step(0.0)
+    eng.step()
+    sh = s.after_step(1.0)
+    assert got and sh == got[0], sh
+    assert abs(sum(sh.values()) - 1.0) < 1e-6
+    assert sh.get("gemm", 0) > 0 and sh.get("attention", 0) > 0, sh

@@ -46,13 +46,13 @@ def _worker(rank, world, port, out_dir, cfg_name):
     try:
         # eager TP engine first, then the default one (decode hipGraphs captured with the K15
         # all-reduce inside; the vocab gather runs after each replay): replay == eager
-        for key, graphs in (("tp", False), ("tp_graph", True)):
+        for key, graphs in (("eager", False), ("graph", True)):
             ec = EngineConfig(max_num_seqs=4, max_num_batched_tokens=48, max_model_len=256, num_kv_blocks=64,
                               use_graphs=graphs, graph_buckets=(1, 2, 4))
             eng = Engine(shard, ec)
             if ps.tp_rank == 0:
                 res[key] = eng.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
-                res[key + "_graph_steps"] = eng.stats["graph_steps"]
+                res[key + "_steps_in_graphs"] = eng.stats["graph_steps"]
                 eng.shutdown()
             else:
                 eng.worker_loop()
@@ -75,10 +75,11 @@ def test_tp2_engine_on_gpu_with_custom_all_reduce(cfg_name):
     r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=False)
     r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=False)
     assert r0["car_error"] == 0 and r1["car_error"] == 0 and r1["worker_steps"] > 0
-    assert r0["tp_graph_steps"] > 0 and r0["tp_graph"] == r0["tp"]
+    assert r0["eager_steps_in_graphs"] == 0 and r0["graph_steps_in_graphs"] > 0
+    assert r0["graph"] == r0["eager"]  # decode-graph replay (K15 inside) == eager TP
     from mlopamd.models import build_model
     from mlopamd.models.config import get_config
     from test_model_gpu import _check_greedy
 
     full = build_model(get_config(cfg_name), device=torch.device("cuda", 0), seed=4)
-    _check_greedy(full, PROMPTS, r0["tp"])
+    _check_greedy(full, PROMPTS, r0["eager"])
