@@ -89,8 +89,19 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
     t_cr = time.perf_counter()
     await kube.create(GROUP, VERSION, namespace, PLURAL, cr)
 
+    last_log = [0.0]
+
     async def cr_status():
-        return (await kube.get(GROUP, VERSION, namespace, PLURAL, name)).get("status") or {}
+        st = (await kube.get(GROUP, VERSION, namespace, PLURAL, name)).get("status") or {}
+        for p in ctl.pods.values():  # a predictor process that cannot start ends the demo now
+            if "error" in p.extra and p.predictor == "v1":
+                raise RuntimeError(f"predictor {p.predictor} failed to start: {p.extra['error']}")
+        now = time.perf_counter()
+        if now - last_log[0] > 10:  # progress line (long real-size starts print nothing else)
+            last_log[0] = now
+            print(f"[llm_demo {now - t_start:7.1f}s] phase={st.get('phase')} ready={st.get('ready')} "
+                  f"pods={sorted(p.predictor for p in ctl.pods.values())}", flush=True)
+        return st
 
     async def is_ready():
         return (await cr_status()).get("ready") == "True"

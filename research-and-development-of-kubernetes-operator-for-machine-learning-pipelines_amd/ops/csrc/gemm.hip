@@ -632,7 +632,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     // partner group's MFMAs then run alone on the SIMD.  Ragged M, and above all the last
     // m-tile of every expert in the grouped (MoE) GEMM, half empty on average.
     const int rows_here = sk.skip_dead ? m_end - m0 : BM;
-    auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+    // drain: retire this phase's LDS reads BEFORE its first barrier (phase 1: lets the partner
+    // group restage the B buffer one phase later -- cdna_hip_programming.md WAR rule)
+    auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2],
+                         bool drain = false) {
+      if (drain) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -651,17 +655,18 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       raw_barrier();
     };
 
-    // LDS-DMA schedule (barriers numbered along group 0; group 1 runs one behind):
-    //   A(t+1) -> buffer (t+1)&1 in phases 0 (rows 0-127) and 1 (rows 128-255) of t (the
-    //            last A reads of t-1, phase 2 of t-1, retired before group 1's phase-2 MFMAs,
-    //            i.e. before group 0's phase-3 barrier)
-    //   B(t+2) -> buffer t&1     in phase 3 of t   (after B1(t), the last B read of t, retired)
-    //   retire B(t+1) in phase 2 of t (vmcnt(4): A(t+1) stays in flight), read B0(t+1) in
-    //   phase 3 of t into the other B0 register set; retire A(t+1) in phase 3 (vmcnt(4):
-    //   B(t+2) stays in flight), read it from phase 0 of t+1.  Every read happens at least
-    //   one barrier after the slower group's retirement; every DMA is issued at least one
-    //   barrier after the last read of its destination retired.  Per phase a wave issues
-    //   8+2 / 4+2 / 8 / 4+4 LDS reads+DMAs, so no single phase outlasts the partner's 16 MFMAs.
+    // LDS-DMA schedule: ONE half-tile (2 DMAs per wave) per phase, barriers numbered along
+    // group 0 (group 1 runs one behind):
+    //   phase 0 of t: A rows 0-127   of t+1 -> buffer (t+1)&1  (last A reads of that buffer:
+    //   phase 1 of t: A rows 128-255 of t+1                     phase 2 of t-1, long retired)
+    //   phase 2 of t: B rows 0-127   of t+2 -> buffer t&1      (last B reads of buffer t&1:
+    //   phase 3 of t: B rows 128-255 of t+2                     phase 1 of t, drained before
+    //                                                           that phase's first barrier)
+    //   phase 2 wait vmcnt(6): B(t+1) retired (A(t+1), B0(t+2) stay in flight), read from
+    //   phase 3 of t; phase 3 wait vmcnt(4): A(t+1) retired (B(t+2) in flight), read from
+    //   phase 0 of t+1.  Each wait precedes its phase's first barrier and the reads come one
+    //   phase later, i.e. after the barrier that both staggered groups pass after their
+    //   waits.  Per phase a wave issues 8+2 / 4+2 / 8+2 / 4+2 LDS reads + DMAs.
 #pragma unroll
     for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
     if (nkp > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
@@ -679,13 +684,17 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       phase_mma(0, 0, fa, fb0);
       read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
       if (m1) issue_half(nxt, 1, t + 1);
-      phase_mma(0, 1, fa, fb1);
+      phase_mma(0, 1, fa, fb1, true);
       read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
-      if (m1) wait_vmcnt<4>();
+      if (m2) {
+        issue_half(cur, 2, t + 2);
+        wait_vmcnt<6>();
+      } else if (m1) {
+        wait_vmcnt<4>();
+      }
       phase_mma(1, 1, fa, fb1);
       if (m1) read_b(nxt, 0, fb0n);                        // phase 3: quadrant (1,0)
       if (m2) {
-        issue_half(cur, 2, t + 2);
         issue_half(cur, 3, t + 2);
         wait_vmcnt<4>();
       } else {

@@ -115,6 +115,10 @@ async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256
                 if (cur["mlop_prompt_tokens_total"] >= batch * prompt_len
                         and cur["mlop_num_requests_waiting"] <= backlog):
                     break
+                if int(4 * (time.perf_counter() - t_ramp)) % 40 == 0:  # a progress line every ~10 s
+                    print(f"[http_bench] ramp {time.perf_counter() - t_ramp:.0f}s running="
+                          f"{cur['mlop_num_requests_running']:.0f} waiting={cur['mlop_num_requests_waiting']:.0f} "
+                          f"prompt_tokens={cur['mlop_prompt_tokens_total']:.0f}", flush=True)
                 await asyncio.sleep(0.25)
             out["http_ramp_s"] = round(time.perf_counter() - t_ramp, 2)
             s_ramp = cur
