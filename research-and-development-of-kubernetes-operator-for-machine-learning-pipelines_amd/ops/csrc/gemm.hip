@@ -483,7 +483,7 @@ __device__ __forceinline__ int sk_index(int Lb, int n0, int n_sk) {
   return before + (Lb - n0) / 8;
 }
 
-template <int EPI, bool GROUPED = false, bool SK = false>
+template <int EPI, bool GROUPED = false, bool SK = false, bool PH2 = false>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m,
@@ -587,7 +587,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     for (int h = 0; h < 4; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int r = (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row inside the 256-row operand tile
+        // PH2: the A halves are the mi halves (rows mi*64.. of BOTH groups' 128-row blocks)
+        const int r = (PH2 && h < 2) ? i * 128 + h * 64 + wid * 8 + prow
+                                     : (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row in the 256-row tile
         const int ch = (lane & 7) ^ swz(r);
         src[h][i] = (h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda
                            : Bg + (size_t)min(n0 + r, N - 1) * ldb) + k0 * kBK + ch * 8;
@@ -595,7 +597,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     auto issue_half = [&](int buf, int h, int kt) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + ((h & 1) * 128 + (wid + 8 * i) * 8) * kBK;
+        const int r0 = (PH2 && h < 2) ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
+        uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + r0 * kBK;
         __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
       }
     };
@@ -655,6 +658,69 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       raw_barrier();
     };
 
+    if constexpr (PH2) {
+      // Two phases per K-tile, 32 MFMAs each (half the group hand-offs of the 4-phase loop):
+      //   X(t): read A(mi 0) + B(nj 0, 1) of t | DMA A(mi 1) of t+1 -> buffer (t+1)&1
+      //   Y(t): read A(mi 1) of t             | DMA A(mi 0) + B of t+2 -> buffer t&1
+      // Every phase drains its LDS reads before its first barrier, so a buffer region can be
+      // restaged in the phase after its last read; every wait (counted vmcnt) precedes the
+      // first barrier of the phase before the reads (RAW across the staggered groups).
+      //   X(t) wait: A(mi 1, t) retired; 8 younger DMAs (A0+B of t+1, A1 of t+1) stay in flight
+      //   Y(t) wait: A(mi 0) + B of t+1 retired; A1(t+1) and A0+B(t+2) stay in flight
+      issue_half(0, 0, 0);
+      issue_half(0, 1, 0);
+      issue_half(0, 2, 0);
+      issue_half(0, 3, 0);
+      if (nkp > 1) { issue_half(1, 0, 1); issue_half(1, 2, 1); issue_half(1, 3, 1); }
+      if (nkp > 1) wait_vmcnt<6>(); else wait_vmcnt<0>();
+      raw_barrier();
+      bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+      if (grp == 1) raw_barrier();  // stagger
+      auto seg_mma = [&](int mi) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // drain before the barrier
+        raw_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp * 128 + mi * 64 < rows_here) {
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int kk = 0; kk < 2; ++kk) {
+                acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
+                acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
+              }
+          __builtin_amdgcn_s_setprio(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        raw_barrier();
+      };
+      for (int t = 0; t < nkp; ++t) {
+        const int cur = t & 1, nxt = cur ^ 1;
+        const bool m1 = t + 1 < nkp, m2 = t + 2 < nkp;
+        read_a(cur, 0, fa);  // X(t)
+        read_b(cur, 0, fb0);
+        read_b(cur, 1, fb1);
+        if (m1) {
+          issue_half(nxt, 1, t + 1);
+          wait_vmcnt<8>();
+        } else {
+          wait_vmcnt<0>();
+        }
+        seg_mma(0);
+        read_a(cur, 1, fa);  // Y(t)
+        if (m2) {
+          issue_half(cur, 0, t + 2);
+          issue_half(cur, 2, t + 2);
+          issue_half(cur, 3, t + 2);
+          wait_vmcnt<8>();
+        } else if (m1) {
+          wait_vmcnt<2>();
+        }
+        seg_mma(1);
+      }
+    } else {
     // LDS-DMA schedule: ONE half-tile (2 DMAs per wave) per phase, barriers numbered along
     // group 0 (group 1 runs one behind):
     //   phase 0 of t: A rows 0-127   of t+1 -> buffer (t+1)&1  (last A reads of that buffer:
@@ -706,6 +772,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       ktile(t, fbA, fbB);
       if (t + 1 < nkp) ktile(t + 1, fbB, fbA);
     }
+    }  // PH2
     if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
     __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
 
@@ -908,16 +975,37 @@ static SkArgs sk_plan(int T, int nk, int& n_sk) {
   return a;
 }
 
+// K-loop of the ping-pong kernel: 4 phases x 16 MFMAs per K-tile (default) or 2 x 32
+// (MLOP_GEMM_PP_PHASES=2; gemm_pp_phases op for in-process A/B)
+static int g_pp_phases = env_int("MLOP_GEMM_PP_PHASES", 4);
+int gemm_pp_phases(int set) {
+  if (set == 2 || set == 4) g_pp_phases = set;
+  return g_pp_phases;
+}
+
+template <int EPI, bool GROUPED, bool PH2>
+static void run_pp_impl(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
+                        int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets, int n_groups);
+
 template <int EPI, bool GROUPED = false>
 static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
                    int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets = nullptr,
                    int n_groups = 0) {
+  if (g_pp_phases == 2)
+    run_pp_impl<EPI, GROUPED, true>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
+  else
+    run_pp_impl<EPI, GROUPED, false>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
+}
+
+template <int EPI, bool GROUPED, bool PH2>
+static void run_pp_impl(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
+                        int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets, int n_groups) {
   constexpr size_t ring = 2ull * (256 + 256) * kBK * 2;
   constexpr size_t epi = EPI == EPI_ROPE ? 256ull * (256 + 8) * 2
                                          : 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
   constexpr size_t lds = ring > epi ? ring : epi;
   static_assert(lds <= 163840, "LDS budget");
-  auto kern = gemm_pp_kernel<EPI, GROUPED>;
+  auto kern = gemm_pp_kernel<EPI, GROUPED, false, PH2>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -943,7 +1031,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
     }
   }
   if (n_sk > 0) {
-    auto ksk = gemm_pp_kernel<EPI, GROUPED, true>;
+    auto ksk = gemm_pp_kernel<EPI, GROUPED, true, PH2>;
     static bool attr_sk = false;
     if (!attr_sk) {
       hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

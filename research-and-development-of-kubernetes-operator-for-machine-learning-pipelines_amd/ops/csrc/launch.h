@@ -49,6 +49,7 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
+int gemm_pp_phases(int set);  // ping-pong K-loop: 4 phases x 16 MFMAs or 2 x 32; set 2/4, returns current
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)
 int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fitted BM x BN
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the

@@ -156,6 +156,8 @@ class LLMBackend:
                 m.running.labels(**m.labels).set(eng.num_running)
                 m.waiting.labels(**m.labels).set(len(eng.waiting))
                 m.kv_usage.labels(**m.labels).set(eng.kv_usage())
+                m.kv_blocks.labels(**m.labels).set(eng.alloc.available)
+                m.kv_fill_failed.labels(**m.labels).set(1 if eng.stats.get("kv_fill_failed") else 0)
 
     # ----- asyncio side -----
     def submit(self, prompt_ids, params: SamplingParams, stream: bool = False) -> _Req:

@@ -48,6 +48,11 @@ class RuntimeMetrics:
         self.running = Gauge("mlop_num_requests_running", "Sequences decoding", base, registry=r)
         self.waiting = Gauge("mlop_num_requests_waiting", "Sequences queued", base, registry=r)
         self.kv_usage = Gauge("mlop_kv_cache_usage_ratio", "Fraction of KV pages in use", base, registry=r)
+        self.kv_blocks = Gauge("mlop_kv_cache_blocks", "KV pages backed by memory (lazy arena: grows while serving)",
+                               base, registry=r)
+        self.kv_fill_failed = Gauge("mlop_kv_cache_fill_failed",
+                                    "1 when the background KV fill could not back a chunk (serving continues "
+                                    "on the pages already backed)", base, registry=r)
         self.ready = Gauge("mlop_ready", "1 when the model is loaded and graphs captured", base, registry=r)
         self.load_seconds = Gauge("mlop_model_load_seconds", "Start-up time to ready", base, registry=r)
         self.gpu_busy = Gauge("mlop_gpu_busy_percent", "GPU busy %", base + ["gpu"], registry=r)

@@ -87,6 +87,8 @@ def test_llm_generate_infer_stream(llm_backend):
             assert all(o.status == 200 for o in outs)
             txt = await (await c.get("/metrics")).text()
             assert "mlop_time_to_first_token_seconds_count" in txt and "mlop_generated_tokens_total" in txt
+            assert "mlop_engine_steps_total{" in txt and "mlop_engine_tokens_total{" in txt
+            assert 'mlop_kv_cache_fill_failed{' in txt and "mlop_kv_cache_blocks{" in txt
             # engine step trace (Chrome trace events) and its summary
             tr = await (await c.get("/v2/debug/trace")).json()
             kinds = {e["name"] for e in tr["traceEvents"]}
