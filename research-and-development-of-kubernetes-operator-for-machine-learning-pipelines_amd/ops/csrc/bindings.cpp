@@ -3,7 +3,10 @@
 // Every op validates dtype / contiguity / shape on the host before launching
 // (a faulting kernel can reset every GPU of the node), runs on the current
 // HIP stream (so it is hipGraph-capturable) and mutates pre-allocated outputs
-// (no allocation inside: graph-capture safe, cdna_hip_programming.md Guideline 9).
+// (cdna_hip_programming.md Guideline 9; the one scratch tensor, gemm_rope_cache's V staging,
+// comes from PyTorch's caching allocator, which serves captures from the graph's pool).
+#include <cstdlib>
+#include <string>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -212,7 +215,6 @@ int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_
 int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
-int64_t gemm_pp_phases(int64_t set) { return mlop::gemm_pp_phases((int)set); }
 int64_t gemm_small_stages(int64_t set) { return mlop::gemm_small_stages((int)set); }
 int64_t gemm_small_tile(int64_t set) { return mlop::gemm_small_tile((int)set); }
 int64_t gemm_sk_mode(int64_t set) { return mlop::gemm_sk_mode((int)set); }
@@ -253,6 +255,10 @@ void gemm(Tensor out, Tensor a, Tensor w, Tensor ws, int64_t epi) {
 
 // QKV projection with RoPE + paged-cache stores in the GEMM epilogue; false = this M
 // does not take the fused tiling (caller runs gemm + rope_cache)
+bool gemm_rope_stages_v_op(int64_t M, int64_t N, int64_t K) {
+  return mlop::gemm_rope_stages_v((int)M, (int)N, (int)K);
+}
+
 bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor w, Tensor pos,
                      Tensor cos_sin, Tensor slots) {
   TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
@@ -275,6 +281,14 @@ bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Ten
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
+  // large-M fused path: V staged token-major, then paged by a chip-wide scatter (MLOP_V_STAGE=0:
+  // the epilogue's own 2-B page-row stores, A/B).  Caching-allocator memory: capture-safe.
+  static const bool stage_v = std::getenv("MLOP_V_STAGE") == nullptr || std::string(std::getenv("MLOP_V_STAGE")) != "0";
+  at::Tensor vtmp;
+  if (stage_v && mlop::gemm_rope_stages_v((int)M, (int)N, (int)K)) {
+    vtmp = at::empty({M, Hkv, D}, a.options());
+    re.v_tmp = (uint16_t*)vtmp.data_ptr();
+  }
   return mlop::launch_gemm_rope(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)M, (int)N, (int)K,
                                 re, cur_stream());
 }
@@ -543,7 +557,6 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
-  m.def("gemm_pp_phases(int set=-1) -> int", &gemm_pp_phases);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
   m.def("gemm_small_tile(int set=-1) -> int", &gemm_small_tile);
   m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);
@@ -557,6 +570,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("vmm_chunks_ready(Tensor flat) -> int", &vmm_chunks_ready);
   m.def("vmm_error(Tensor flat) -> int", &vmm_error);
   m.def("gemm_rope_supported(int M, int N, int K) -> bool", &gemm_rope_supported);
+  m.def("gemm_rope_stages_v(int M, int N, int K) -> bool", &gemm_rope_stages_v_op);
   m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");

@@ -398,22 +398,18 @@ int gemm_big_variant(int set) {
 }
 
 // ---------------------------------------------------------------------------
-// Ping-pong 256x256 GEMM (cdna_hip_programming.md "The 256^2 8-phase template"):
+// Ping-pong 256x256 GEMM (after cdna_hip_programming.md "The 256^2 8-phase template"):
 // 8 waves = 2 wave GROUPS (A halves) x 4 column strips, 128x64 outputs per wave.
-// Each K-tile (BK = 64) is 4 phases, one 64x32 quadrant x K=64 (16 MFMAs) each:
-//     [ds_read the quadrant's fragments | issue LDS-DMA of the NEXT K-tile]
-//     s_barrier; lgkmcnt(0); setprio(1) 16 x MFMA setprio(0); s_barrier
+// Each K-tile (BK = 64) is 2 phases, one 64x64 half of the wave's outputs x K=64 (32 MFMAs):
+//     [ds_read the half's fragments | issue LDS-DMA | drain lgkmcnt]
+//     s_barrier; setprio(1) 32 x MFMA setprio(0); s_barrier
 // Group 1 executes one extra barrier up front, so it is always one half-phase
 // behind group 0: while one group's waves issue LDS reads / DMA, the other
 // group's waves (one per SIMD each) keep the matrix cores busy — the barrier
 // and LDS latency that idles a single-group loop (27% SQ_WAIT_ANY in
 // profiles/r01_gemm_pmc.md) is overlapped by the partner group instead.
-// Two LDS buffers (K-tile parity, 2 x 64 KB), each wave retires its own DMA
-// of K-tile t+1 with vmcnt(0) in phase 3 of K-tile t; reads of buffer t&1 start
-// only after the barrier that follows every wave's retirement, and DMA into a
-// buffer starts only after every read of its previous K-tile has retired
-// (phase-window accounting in the comments below).  Quadrant order (0,0)
-// (0,1) (1,1) (1,0) reloads the A sub-tile twice and the B sub-tiles once.
+// Two LDS buffers (K-tile parity, 2 x 64 KB); the DMA schedule and its vmcnt /
+// barrier accounting are in the comment above the K-loop.
 //
 // GROUPED (MoE K13 at >= 512 rows per expert): the (expert, m-tile) slot is the fast
 // tile index (empty slots of the worst-case grid spread over all XCDs), B = W[e] and
@@ -483,7 +479,7 @@ __device__ __forceinline__ int sk_index(int Lb, int n0, int n_sk) {
   return before + (Lb - n0) / 8;
 }
 
-template <int EPI, bool GROUPED = false, bool SK = false, bool PH2 = false>
+template <int EPI, bool GROUPED = false, bool SK = false>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb,
     uint16_t* __restrict__ C, int ldc, int M, int N, int K, int n_tiles_x, int m_tiles, int group_m,
@@ -587,9 +583,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     for (int h = 0; h < 4; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        // PH2: the A halves are the mi halves (rows mi*64.. of BOTH groups' 128-row blocks)
-        const int r = (PH2 && h < 2) ? i * 128 + h * 64 + wid * 8 + prow
-                                     : (h & 1) * 128 + (wid + 8 * i) * 8 + prow;  // row in the 256-row tile
+        // A halves are the mi halves (rows mi*64.. of BOTH groups' 128-row blocks)
+        const int r = h < 2 ? i * 128 + h * 64 + wid * 8 + prow : (h & 1) * 128 + (wid + 8 * i) * 8 + prow;
         const int ch = (lane & 7) ^ swz(r);
         src[h][i] = (h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda
                            : Bg + (size_t)min(n0 + r, N - 1) * ldb) + k0 * kBK + ch * 8;
@@ -597,7 +592,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     auto issue_half = [&](int buf, int h, int kt) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int r0 = (PH2 && h < 2) ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
+        const int r0 = h < 2 ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
         uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + r0 * kBK;
         __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
       }
@@ -635,14 +630,24 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     // partner group's MFMAs then run alone on the SIMD.  Ragged M, and above all the last
     // m-tile of every expert in the grouped (MoE) GEMM, half empty on average.
     const int rows_here = sk.skip_dead ? m_end - m0 : BM;
-    // drain: retire this phase's LDS reads BEFORE its first barrier (phase 1: lets the partner
-    // group restage the B buffer one phase later -- cdna_hip_programming.md WAR rule)
-    auto phase_mma = [&](int mi, int nj, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2],
-                         bool drain = false) {
-      if (drain) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // K-loop: two phases per K-tile, 32 MFMAs each.
+    //   X(t): read A(mi 0) + B(nj 0, 1) of t | DMA A(mi 1) of t+1 -> buffer (t+1)&1
+    //   Y(t): read A(mi 1) of t             | DMA A(mi 0) + B of t+2 -> buffer t&1
+    // Group 1 runs one barrier behind group 0, so each SIMD's two waves alternate: one issues
+    // its phase's LDS reads and DMAs while the other runs 32 MFMAs.  (The guide's 4 x 16-MFMA
+    // template hands the matrix core over twice as often: 2-9 % slower on every Llama-3-8B
+    // projection, profiles/r03_gemm_fourwave.md.)  Every phase drains its LDS reads before its
+    // first barrier, so a buffer region can be restaged in the phase after its last read; every
+    // wait (counted vmcnt) precedes the first barrier of the phase before the reads (RAW across
+    // the staggered groups):
+    //   X(t) wait: A(mi 1, t) retired; 8 younger DMAs (A0+B of t+1, A1 of t+1) stay in flight
+    //   Y(t) wait: A(mi 0) + B of t+1 retired; A1(t+1) and A0+B(t+2) stay in flight
+    bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+    auto seg_mma = [&](int mi) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // drain before the barrier
       raw_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform)
       if (grp * 128 + mi * 64 < rows_here) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -650,129 +655,47 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk)
-              acc[mi * 4 + i][nj * 2 + j] = mfma16(fa[i][kk], fb[j][kk], acc[mi * 4 + i][nj * 2 + j]);
+            for (int kk = 0; kk < 2; ++kk) {
+              acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
+              acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
+            }
         __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);
       raw_barrier();
     };
-
-    if constexpr (PH2) {
-      // Two phases per K-tile, 32 MFMAs each (half the group hand-offs of the 4-phase loop):
-      //   X(t): read A(mi 0) + B(nj 0, 1) of t | DMA A(mi 1) of t+1 -> buffer (t+1)&1
-      //   Y(t): read A(mi 1) of t             | DMA A(mi 0) + B of t+2 -> buffer t&1
-      // Every phase drains its LDS reads before its first barrier, so a buffer region can be
-      // restaged in the phase after its last read; every wait (counted vmcnt) precedes the
-      // first barrier of the phase before the reads (RAW across the staggered groups).
-      //   X(t) wait: A(mi 1, t) retired; 8 younger DMAs (A0+B of t+1, A1 of t+1) stay in flight
-      //   Y(t) wait: A(mi 0) + B of t+1 retired; A1(t+1) and A0+B(t+2) stay in flight
-      issue_half(0, 0, 0);
-      issue_half(0, 1, 0);
-      issue_half(0, 2, 0);
-      issue_half(0, 3, 0);
-      if (nkp > 1) { issue_half(1, 0, 1); issue_half(1, 2, 1); issue_half(1, 3, 1); }
-      if (nkp > 1) wait_vmcnt<6>(); else wait_vmcnt<0>();
-      raw_barrier();
-      bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
-      if (grp == 1) raw_barrier();  // stagger
-      auto seg_mma = [&](int mi) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // drain before the barrier
-        raw_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (grp * 128 + mi * 64 < rows_here) {
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int kk = 0; kk < 2; ++kk) {
-                acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
-                acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
-              }
-          __builtin_amdgcn_s_setprio(0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        raw_barrier();
-      };
-      for (int t = 0; t < nkp; ++t) {
-        const int cur = t & 1, nxt = cur ^ 1;
-        const bool m1 = t + 1 < nkp, m2 = t + 2 < nkp;
-        read_a(cur, 0, fa);  // X(t)
-        read_b(cur, 0, fb0);
-        read_b(cur, 1, fb1);
-        if (m1) {
-          issue_half(nxt, 1, t + 1);
-          wait_vmcnt<8>();
-        } else {
-          wait_vmcnt<0>();
-        }
-        seg_mma(0);
-        read_a(cur, 1, fa);  // Y(t)
-        if (m2) {
-          issue_half(cur, 0, t + 2);
-          issue_half(cur, 2, t + 2);
-          issue_half(cur, 3, t + 2);
-          wait_vmcnt<8>();
-        } else if (m1) {
-          wait_vmcnt<2>();
-        }
-        seg_mma(1);
-      }
-    } else {
-    // LDS-DMA schedule: ONE half-tile (2 DMAs per wave) per phase, barriers numbered along
-    // group 0 (group 1 runs one behind):
-    //   phase 0 of t: A rows 0-127   of t+1 -> buffer (t+1)&1  (last A reads of that buffer:
-    //   phase 1 of t: A rows 128-255 of t+1                     phase 2 of t-1, long retired)
-    //   phase 2 of t: B rows 0-127   of t+2 -> buffer t&1      (last B reads of buffer t&1:
-    //   phase 3 of t: B rows 128-255 of t+2                     phase 1 of t, drained before
-    //                                                           that phase's first barrier)
-    //   phase 2 wait vmcnt(6): B(t+1) retired (A(t+1), B0(t+2) stay in flight), read from
-    //   phase 3 of t; phase 3 wait vmcnt(4): A(t+1) retired (B(t+2) in flight), read from
-    //   phase 0 of t+1.  Each wait precedes its phase's first barrier and the reads come one
-    //   phase later, i.e. after the barrier that both staggered groups pass after their
-    //   waits.  Per phase a wave issues 8+2 / 4+2 / 8+2 / 4+2 LDS reads + DMAs.
-#pragma unroll
-    for (int h = 0; h < 4; ++h) issue_half(0, h, 0);
-    if (nkp > 1) { issue_half(1, 2, 1); issue_half(1, 3, 1); }
-    if (nkp > 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
+    issue_half(0, 0, 0);
+    issue_half(0, 1, 0);
+    issue_half(0, 2, 0);
+    issue_half(0, 3, 0);
+    if (nkp > 1) { issue_half(1, 0, 1); issue_half(1, 2, 1); issue_half(1, 3, 1); }
+    if (nkp > 1) wait_vmcnt<6>(); else wait_vmcnt<0>();
     raw_barrier();
-    bf16x8 fa[4][2], fb1[2][2], fbA[2][2], fbB[2][2];
-    read_b(0, 0, fbA);
     if (grp == 1) raw_barrier();  // stagger: group 1 runs one barrier behind group 0
-
-    auto ktile = [&](int t, bf16x8 (&fb0)[2][2], bf16x8 (&fb0n)[2][2]) {
+    for (int t = 0; t < nkp; ++t) {
       const int cur = t & 1, nxt = cur ^ 1;
       const bool m1 = t + 1 < nkp, m2 = t + 2 < nkp;
-      read_a(cur, 0, fa);                                  // phase 0: quadrant (0,0)
-      if (m1) issue_half(nxt, 0, t + 1);
-      phase_mma(0, 0, fa, fb0);
-      read_b(cur, 1, fb1);                                 // phase 1: quadrant (0,1)
-      if (m1) issue_half(nxt, 1, t + 1);
-      phase_mma(0, 1, fa, fb1, true);
-      read_a(cur, 1, fa);                                  // phase 2: quadrant (1,1)
-      if (m2) {
-        issue_half(cur, 2, t + 2);
-        wait_vmcnt<6>();
-      } else if (m1) {
-        wait_vmcnt<4>();
-      }
-      phase_mma(1, 1, fa, fb1);
-      if (m1) read_b(nxt, 0, fb0n);                        // phase 3: quadrant (1,0)
-      if (m2) {
-        issue_half(cur, 3, t + 2);
-        wait_vmcnt<4>();
+      read_a(cur, 0, fa);  // X(t)
+      read_b(cur, 0, fb0);
+      read_b(cur, 1, fb1);
+      if (m1) {
+        issue_half(nxt, 1, t + 1);
+        wait_vmcnt<8>();
       } else {
         wait_vmcnt<0>();
       }
-      phase_mma(1, 0, fa, fb0);
-    };
-    for (int t = 0; t < nkp; t += 2) {
-      ktile(t, fbA, fbB);
-      if (t + 1 < nkp) ktile(t + 1, fbB, fbA);
+      seg_mma(0);
+      read_a(cur, 1, fa);  // Y(t)
+      if (m2) {
+        issue_half(cur, 0, t + 2);
+        issue_half(cur, 2, t + 2);
+        issue_half(cur, 3, t + 2);
+        wait_vmcnt<8>();
+      } else if (m1) {
+        wait_vmcnt<2>();
+      }
+      seg_mma(1);
     }
-    }  // PH2
     if (grp == 0) raw_barrier();  // barrier counts of the two groups must match
     __syncthreads();              // all LDS reads retired everywhere: the ring becomes C staging
 
@@ -975,37 +898,16 @@ static SkArgs sk_plan(int T, int nk, int& n_sk) {
   return a;
 }
 
-// K-loop of the ping-pong kernel: 4 phases x 16 MFMAs per K-tile (default) or 2 x 32
-// (MLOP_GEMM_PP_PHASES=2; gemm_pp_phases op for in-process A/B)
-static int g_pp_phases = env_int("MLOP_GEMM_PP_PHASES", 4);
-int gemm_pp_phases(int set) {
-  if (set == 2 || set == 4) g_pp_phases = set;
-  return g_pp_phases;
-}
-
-template <int EPI, bool GROUPED, bool PH2>
-static void run_pp_impl(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
-                        int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets, int n_groups);
-
 template <int EPI, bool GROUPED = false>
 static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
                    int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets = nullptr,
                    int n_groups = 0) {
-  if (g_pp_phases == 2)
-    run_pp_impl<EPI, GROUPED, true>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
-  else
-    run_pp_impl<EPI, GROUPED, false>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
-}
-
-template <int EPI, bool GROUPED, bool PH2>
-static void run_pp_impl(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
-                        int N, int K, hipStream_t st, const RopeEpi& re, const int* offsets, int n_groups) {
   constexpr size_t ring = 2ull * (256 + 256) * kBK * 2;
   constexpr size_t epi = EPI == EPI_ROPE ? 256ull * (256 + 8) * 2
                                          : 8ull * 128 * ((EPI == EPI_NONE ? 64 : 32) + 8) * 2;
   constexpr size_t lds = ring > epi ? ring : epi;
   static_assert(lds <= 163840, "LDS budget");
-  auto kern = gemm_pp_kernel<EPI, GROUPED, false, PH2>;
+  auto kern = gemm_pp_kernel<EPI, GROUPED>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1031,7 +933,7 @@ static void run_pp_impl(const uint16_t* A, int lda, const uint16_t* B, int ldb, 
     }
   }
   if (n_sk > 0) {
-    auto ksk = gemm_pp_kernel<EPI, GROUPED, true, PH2>;
+    auto ksk = gemm_pp_kernel<EPI, GROUPED, true>;
     static bool attr_sk = false;
     if (!attr_sk) {
       hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1220,7 +1122,14 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
   p.k_chunk = K;
   launch_plan<EPI_ROPE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, nullptr,
                                M, N, K, nullptr, 0, st, re);
+  if (re.v_tmp != nullptr) launch_v_scatter(re.v_tmp, re.v_cache, re.slots, M, re.Hkv, re.BS, st);
   return true;
+}
+
+bool gemm_rope_stages_v(int M, int N, int K) {
+  if (M == 0 || !gemm_rope_supported(M, N, K) || gemv_takes(M, N, K, EPI_ROPE)) return false;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  return p.BM == 256 && p.BN >= 128;
 }
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {

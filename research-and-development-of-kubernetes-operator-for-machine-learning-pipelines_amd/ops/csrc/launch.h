@@ -41,7 +41,16 @@ struct RopeEpi {
   const float* cos_sin;
   const int* slots;
   int Hq, Hkv, BS;
+  // token-major [M, Hkv, 128] staging for the V heads (large-M fused QKV epilogue): the GEMM
+  // writes it with 16-B stores and launch_v_scatter moves it into the dim-major pages over
+  // the whole chip (nullptr: the epilogue scatters V itself)
+  uint16_t* v_tmp = nullptr;
 };
+// V rows staged token-major -> dim-major paged cache ([NB, Hkv, 128, BS]); slot < 0 skipped
+void launch_v_scatter(const uint16_t* v_tmp, uint16_t* v_cache, const int* slots, int M, int Hkv, int BS,
+                      hipStream_t st);
+// true when launch_gemm_rope takes the large-M fused path, which stages V in re.v_tmp
+bool gemm_rope_stages_v(int M, int N, int K);
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
@@ -49,7 +58,6 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
-int gemm_pp_phases(int set);  // ping-pong K-loop: 4 phases x 16 MFMAs or 2 x 32; set 2/4, returns current
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)
 int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fitted BM x BN
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the

@@ -46,7 +46,7 @@ __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nhe
       cs[k][3] = row[(HALF + cq) / 4 + 1];
     }
   }
-  if (any_v && rv < rows) slot_v = re.slots[m0 + rv];
+  if (any_v && rv < rows && re.v_tmp == nullptr) slot_v = re.slots[m0 + rv];
   for (int hh = 0; hh < nheads; ++hh) {
     const int head = head0 + hh;
     if (head >= n_all) break;
@@ -77,6 +77,25 @@ __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nhe
         }
         *reinterpret_cast<u32x4*>(dst + cq) = oa;
         *reinterpret_cast<u32x4*>(dst + HALF + cq) = ob;
+      }
+    } else if (re.v_tmp != nullptr) {
+      // token-major staging: 16-B stores of whole 8-dim chunks (launch_v_scatter pages them)
+      const int kh = head - n_rope;
+#pragma unroll
+      for (int k = 0; k < QK; ++k) {
+        const int r = rq + k * (NT / 8);
+        if (r >= rows) continue;
+        uint16_t* dst = re.v_tmp + ((size_t)(m0 + r) * re.Hkv + kh) * D;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          u32x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = hh * D + half * HALF + cq + 2 * j;
+            o[j] = pack2(at(r, c), at(r, c + 1));
+          }
+          *reinterpret_cast<u32x4*>(dst + half * HALF + cq) = o;
+        }
       }
     } else {
       const int kh = head - n_rope;

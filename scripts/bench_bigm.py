@@ -35,16 +35,6 @@ def timeit(fn, iters=20):
 def with_variant(v, fn):
     def run():
         torch.ops.mlop.gemm_big_variant(v)
-        torch.ops.mlop.gemm_pp_phases(4)
-        return fn()
-    return run
-
-
-def with_phases(ph, fn):  # ping-pong K-loop: 4 x 16 or 2 x 32 MFMAs per K-tile
-    def run():
-        torch.ops.mlop.gemm_big_variant(3)
-torch.ops.mlop.gemm_pp_phases(4)
-        torch.ops.mlop.gemm_pp_phases(ph)
         return fn()
     return run
 
@@ -55,7 +45,6 @@ for M in Ms:
         w = (0.02 * torch.randn(N, K, device=dev)).to(torch.bfloat16)
         epi = ops.EPI_SILU_MUL if name == "gate_up" else ops.EPI_NONE
         cands = {"pp": with_variant(3, lambda: ops.gemm(x, w, epi=epi)),
-                 "pp2": with_phases(2, lambda: ops.gemm(x, w, epi=epi)),
                  "hipblaslt": lambda: torch.matmul(x, w.t())}
         ts = {k: [] for k in cands}
         for _ in range(3):
@@ -66,4 +55,3 @@ for M in Ms:
         print(json.dumps(dict(shape=name, M=M, N=N, K=K, **{f"{k}_us": v for k, v in best.items()},
                               **{f"{k}_tflops": round(fl / v / 1e6) for k, v in best.items()})), flush=True)
 torch.ops.mlop.gemm_big_variant(3)
-torch.ops.mlop.gemm_pp_phases(4)

@@ -466,6 +466,47 @@ def test_gemv_silu_mul(gpu, M, I, K):
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("consecutive", [False, True])
+def test_qkv_rope_fused_in_graph(gpu, consecutive):
+    """Large-M fused QKV+RoPE (V staged token-major in a caching-allocator tensor, then paged by
+    the chip-wide scatter) captured in a hipGraph and replayed with new positions / slots:
+    replay == eager reference.  Consecutive slots = a prefill chunk; random = decode rows."""
+    from mlopamd.models.layers import rope_table
+
+    M, Hq, Hkv, D, K, BS = 1024, 32, 8, 128, 4096, 16
+    N = (Hq + 2 * Hkv) * D
+    NB = M // BS + 8
+    ops._sk_reserve(torch.device(gpu))
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    pos = torch.zeros(M, device=gpu, dtype=torch.int32)
+    slots = torch.zeros(M, device=gpu, dtype=torch.int32)
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
+    assert torch.ops.mlop.gemm_rope_stages_v(M, N, K)
+    torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)  # warm-up outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
+    new_slots = (torch.arange(M, device=gpu) + 3 * BS) if consecutive else torch.randperm(NB * BS, device=gpu)[:M]
+    slots.copy_(new_slots.to(torch.int32))
+    slots[7] = -1
+    pos.copy_(torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32))
+    kc.zero_()
+    vc.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref)
+    close(kc, kr)
+    close(vc, vr)
+
+
 @pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (3, 32, 8), (4, 32, 8), (2, 8, 1), (4, 64, 8)])
 def test_gemv_rope_cache(gpu, M, Hq, Hkv):
     """Decode QKV GEMV with RoPE + paged K/V stores in its epilogue (EPI_ROPE at M <= 8)."""
