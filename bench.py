@@ -253,8 +253,10 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
         try:
             from mlopamd import ops
 
-            ch = ops.gemm_choices()
-            res["gemm_backend"] = {b: sum(1 for c in ch if c["choice"] == b) for b in ("mlop", "hipblaslt")}
+            # backend that actually RAN per projection shape (eager calls and graph captures of
+            # this process), and the configured mode
+            res["gemm_backend"] = ops.gemm_used()
+            res["gemm_mode"] = ops.GEMM_BACKEND
         except Exception:  # noqa: BLE001
             pass
         print(json.dumps(res), flush=True)

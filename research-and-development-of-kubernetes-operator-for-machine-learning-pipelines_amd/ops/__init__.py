@@ -223,7 +223,26 @@ def _gemm_hipblaslt(x2, w, o2, epi):
 
 _GEMM_IMPL = {"mlop": _gemm_mlop, "hipblaslt": _gemm_hipblaslt}
 _GEMM_CHOICE: dict = {}
-GEMM_BACKEND = os.environ.get("MLOP_GEMM_BACKEND", "auto")  # auto | mlop | hipblaslt
+# Which GEMM runs a projection: "mlop" (default) = the hand-written kernels (GEMV / MFMA tiles /
+# ping-pong 256x256 with fused epilogues) wherever their tiling contract holds; "auto" = the
+# per-shape timed choice against hipBLASLt (+ its separate epilogue op), seeded from the shipped
+# table -- kept as the A/B reference (profiles/r03_gemm_fourwave.md: equal end to end since the
+# two-phase ping-pong loop); "hipblaslt" = library only.
+GEMM_BACKEND_DEFAULT = "mlop"
+GEMM_BACKEND = os.environ.get("MLOP_GEMM_BACKEND", GEMM_BACKEND_DEFAULT)  # mlop | auto | hipblaslt
+_GEMM_USED: dict = {}  # (M bucket, N, K, epi) -> backend that actually ran (gemm_used())
+
+
+def gemm_used() -> dict:
+    """{backend: number of distinct projection shapes it ran} since the last reset."""
+    out = {"mlop": 0, "hipblaslt": 0}
+    for c in _GEMM_USED.values():
+        out[c] = out.get(c, 0) + 1
+    return out
+
+
+def reset_gemm_used() -> None:
+    _GEMM_USED.clear()
 
 
 _POW2_BUCKETS = os.environ.get("MLOP_GEMM_MBUCKET") == "pow2"  # A/B against the old keys
@@ -290,9 +309,15 @@ def _time_candidates(cands, M: int, dev, reps: int = 5, rounds: int = 3) -> dict
 
 
 def _gemm_backend(M, N, K, epi, x2, w, o2) -> str:
-    """Per-shape choice between the hand-written MFMA kernel and hipBLASLt,
-    measured once per (M bucket, N, K, epilogue) on first eager use (never
-    during graph capture).  ``gemm_choices()`` reports the table."""
+    c = _gemm_backend_choice(M, N, K, epi, x2, w, o2)
+    _GEMM_USED[(_mbucket(M), N, K, epi)] = c
+    return c
+
+
+def _gemm_backend_choice(M, N, K, epi, x2, w, o2) -> str:
+    """Per-shape choice between the hand-written MFMA kernel and hipBLASLt: the configured
+    backend, or (``auto``) measured once per (M bucket, N, K, epilogue) on first eager use
+    (never during graph capture).  ``gemm_choices()`` reports the table."""
     if N % 8 or K % 64 or (epi != EPI_NONE and N % 32):
         return "hipblaslt"  # shapes outside the MFMA kernel's tiling contract (e.g. tiny routers)
     if GEMM_BACKEND != "auto":
@@ -361,11 +386,12 @@ def gemm_add_rmsnorm(x, w, residual, norm_w, eps: float):
     def unfused(res):
         return add_rmsnorm(gemm(x2, w), res, norm_w, eps)
 
-    if nws == 0 or GEMM_BACKEND == "hipblaslt":
-        return unfused(residual)
-    if GEMM_BACKEND == "mlop":
-        return fused(residual)
     key = (_mbucket(M), N, K, EPI_ADD_RMSNORM)
+    if nws == 0 or GEMM_BACKEND == "hipblaslt":
+        return unfused(residual)  # the GEMM inside records its own backend
+    if GEMM_BACKEND == "mlop":
+        _GEMM_USED[key] = "mlop"
+        return fused(residual)
     c = _GEMM_CHOICE.get(key)
     if c is None and AUTOTUNE_FROZEN:
         c = _nearest_choice(key)
@@ -375,7 +401,10 @@ def gemm_add_rmsnorm(x, w, residual, norm_w, eps: float):
                                  M, x.device)
         c = min(times, key=times.get)
         _GEMM_CHOICE[key], _GEMM_TIMES[key] = c, times
-    return fused(residual) if c in (None, "mlop") else unfused(residual)
+    if c in (None, "mlop"):
+        _GEMM_USED[key] = "mlop"
+        return fused(residual)
+    return unfused(residual)
 
 
 EPI_ROPE = 3  # QKV projection + RoPE + paged-cache stores in the GEMM epilogue
@@ -409,11 +438,12 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
     def unfused():
         return rope_cache(gemm(x2, w), positions, cos_sin, slots, k_cache, v_cache, n_q_heads, q_out)
 
+    key = (_mbucket(M), N, K, EPI_ROPE)
     if GEMM_BACKEND == "hipblaslt" or not torch.ops.mlop.gemm_rope_supported(M, N, K):
         return unfused()
     if GEMM_BACKEND == "mlop":
+        _GEMM_USED[key] = "mlop"
         return fused()
-    key = (_mbucket(M), N, K, EPI_ROPE)
     c = _GEMM_CHOICE.get(key)
     if c is None and AUTOTUNE_FROZEN:
         c = _nearest_choice(key)
@@ -422,7 +452,10 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
         times = _time_candidates([("mlop", fused), ("hipblaslt", unfused)], M, x.device)
         c = min(times, key=times.get)
         _GEMM_CHOICE[key], _GEMM_TIMES[key] = c, times
-    return fused() if c in (None, "mlop") else unfused()
+    if c in (None, "mlop"):
+        _GEMM_USED[key] = "mlop"
+        return fused()
+    return unfused()
 
 
 # Residual add + RMSNorm as the decode GEMV's prologue (gemv.hip NORM).  Measured a wash at

@@ -576,25 +576,31 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     first_piece = false;
     const int nkp = k1 - k0;
 
-    // DMA sources: half-tile h (0 A rows 0-127, 1 A rows 128-255, 2 B rows 0-127,
-    // 3 B rows 128-255) = 16 pieces of 8 rows x 128 B; wave w moves pieces w, w+8
-    const uint16_t* src[4][2];
+    // DMA sources: half-tile h (0 A rows mi 0 = 0-63 and 128-191, 1 A rows mi 1, 2 B rows
+    // 0-127, 3 B rows 128-255) = 16 pieces of 8 rows x 128 B; wave w moves pieces w, w+8.
+    // Buffer-form LDS loads (buffer_load_dwordx4 ... lds): the per-lane byte offset into the
+    // operand is fixed per tile and the K-tile advance rides in the scalar soffset, so an issue
+    // is M0 + one VMEM instruction -- the global form needed a 64-bit VALU address add per
+    // issue, serialised through one reused register pair.
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
+    const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)Bg, 0, 0x7fffffff, 0x00020000);
+    uint32_t voff[4][2];
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        // A halves are the mi halves (rows mi*64.. of BOTH groups' 128-row blocks)
         const int r = h < 2 ? i * 128 + h * 64 + wid * 8 + prow : (h & 1) * 128 + (wid + 8 * i) * 8 + prow;
         const int ch = (lane & 7) ^ swz(r);
-        src[h][i] = (h < 2 ? A + (size_t)min(m0 + r, m_end - 1) * lda
-                           : Bg + (size_t)min(n0 + r, N - 1) * ldb) + k0 * kBK + ch * 8;
+        voff[h][i] = h < 2 ? (uint32_t)((size_t)min(m0 + r, m_end - 1) * lda * 2) + ch * 16
+                           : (uint32_t)((size_t)min(n0 + r, N - 1) * ldb * 2) + ch * 16;
       }
     auto issue_half = [&](int buf, int h, int kt) {
+      const uint32_t soff = (uint32_t)(k0 + kt) * kBK * 2;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int r0 = h < 2 ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
         uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + r0 * kBK;
-        __builtin_amdgcn_global_load_lds((const void*)(src[h][i] + kt * kBK), (lds_void_t*)dst, 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
       }
     };
     auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {

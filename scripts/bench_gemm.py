@@ -41,7 +41,7 @@ def mlop(x, w, epi):
     try:
         return ops.gemm(x, w, epi=epi)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
 
 
 tag = os.environ.get("BENCH_TAG", "")

@@ -66,7 +66,7 @@ def forced(backend, fn):
         try:
             return fn()
         finally:
-            ops.GEMM_BACKEND = "auto"
+            ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     return run
 
 

@@ -40,7 +40,7 @@ def mlop(x, w):
     try:
         return ops.gemm(x, w, epi=ops.EPI_NONE)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
 
 
 tun = torch.cuda.tunable

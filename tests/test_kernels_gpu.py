@@ -332,7 +332,7 @@ def test_gemm(gpu, M, N, K):
     try:
         y = ops.gemm(x, w)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     exp = (x.float() @ w.float().t())
     close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
 
@@ -363,7 +363,7 @@ def test_gemm_stream_k(gpu, M, N, K, epi):
         dp = ops.gemm(x, w, epi=epi)
         torch.ops.mlop.gemm_sk_mode(prev)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     tol = 3e-2 * exp.abs().max().item() / 10 + 1e-2
     for y in outs + [dp]:
         close(y, exp, atol=tol, rtol=2e-2)
@@ -461,7 +461,7 @@ def test_gemv_silu_mul(gpu, M, I, K):
     try:
         y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     gu = (x.float() @ torch.cat([g, u]).float().t()).to(bf)
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
@@ -549,7 +549,7 @@ def test_gemm_add_rmsnorm(gpu, M, N, K):
             r2 = res.clone()
             out = ops.gemm_add_rmsnorm(x, w, r2, nw, 1e-5)
         finally:
-            ops.GEMM_BACKEND = "auto"
+            ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
         close(r2, exp_res, atol=3e-2, rtol=2e-2)
         close(out, exp_out, atol=5e-2, rtol=3e-2)
 
@@ -566,7 +566,7 @@ def test_gemm_silu_mul(gpu, M, I, K):
     try:
         y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     gu = (x.float() @ torch.cat([g, u]).float().t()).to(bf)
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 

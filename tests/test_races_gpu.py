@@ -86,7 +86,7 @@ def test_stream_k_tickets_under_contention(gpu, M, N, K, epi):
     try:
         y0, bad = _under_contention(gpu, lambda: ops.gemm(x, w, epi=epi))
     finally:
-        ops.GEMM_BACKEND = "auto"
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
     assert not bad, f"stream-K result changed on launches {bad}"
     exp = x.float() @ w.float().t()
     if epi:
