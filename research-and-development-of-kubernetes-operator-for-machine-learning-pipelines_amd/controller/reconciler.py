@@ -190,10 +190,11 @@ class MlflowModelReconciler:
                     placement["node"] = node["node"]
                 if node.get("free_gpus") is not None:  # the canary's second predictor needs its own
                     node = dict(node, free_gpus=max(0, node["free_gpus"] - p.gpus * spec.replicas))
-            elif runtime == seldon.RUNTIME_LLM and spec.tensor_parallel:
-                # a checkpoint of unknown architecture (no preset): honour the requested degree
-                tp = int(spec.tensor_parallel)
-                placement = {"tensorParallel": tp, "expertParallel": int(spec.expert_parallel or 1), "gpus": tp}
+            elif runtime == seldon.RUNTIME_LLM and (spec.tensor_parallel or spec.expert_parallel):
+                # a checkpoint of unknown architecture (no preset): honour the requested degrees
+                tp = int(spec.tensor_parallel or 1)
+                ep = int(spec.expert_parallel or 1)
+                placement = {"tensorParallel": tp, "expertParallel": ep, "gpus": max(tp, ep)}
             engine_args = {}
             if spec.max_model_len:
                 engine_args["max_model_len"] = spec.max_model_len

@@ -54,7 +54,11 @@ def build_predictor(version, model_uri: str, secret: str | None, traffic: int, r
     graph["type"] = "MODEL"
     graph["endpoint"] = {"type": "REST", "httpPort": 9000}
     tp = int((placement or {}).get("tensorParallel", 1))
+    ep = int((placement or {}).get("expertParallel", 1))
     gpus = int((placement or {}).get("gpus", tp if runtime == RUNTIME_LLM else 0))
+    # EP > 1 with TP = 1: data-parallel attention + expert-parallel MoE, one engine per GPU
+    # behind one endpoint (runtime/ep_serving.py); EP = TP: experts sharded by the TP ranks
+    par = ["--ep", str(ep)] if (tp == 1 and ep > 1) else ["--tp", str(tp)]
     env = [
         {"name": "MLOP_RUNTIME", "value": runtime},
         {"name": "MLOP_MODEL_URI", "value": model_uri},
@@ -74,7 +78,7 @@ def build_predictor(version, model_uri: str, secret: str | None, traffic: int, r
         "name": graph_name(version),
         "image": image,
         "command": ["python", "-m", "mlopamd.runtime.server"],
-        "args": ["--port", "9000", "--tp", str(tp)],
+        "args": ["--port", "9000", *par],
         "env": env,
         "ports": [{"name": "http", "containerPort": 9000}],
         "readinessProbe": {"httpGet": {"path": "/v2/health/ready", "port": 9000},

@@ -427,9 +427,10 @@ class Engine:
         return out
 
     def _step(self):
+        self._launched = False
         kind, out = self._step_local()
-        if self.ep_sync is not None and kind == "idle":
-            self._ep_idle()  # no local work: still join this step's all-to-alls
+        if self.ep_sync is not None and not self._launched:
+            self._ep_idle()  # nothing launched here (idle, or nothing schedulable): still join
         return kind, out
 
     def _ep_idle(self):
@@ -775,6 +776,7 @@ class Engine:
         packed metadata buffer and broadcasts it to the TP group in ONE collective
         (SURVEY §2.5 CL5); the other ranks run the same ``_execute`` from ``worker_loop``.
         Returns logits, or (TP, all-greedy rows) the chosen token ids already."""
+        self._launched = True
         npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
         if self.ep_sync is not None:
             kind, T, nt, nl, part, nparts, bucket = self._ep_agree(kind, T, nt, nl, part, nparts, bucket)

@@ -239,7 +239,7 @@ def engine_kwargs_from_env() -> dict:
 
 
 def launch_ranks(tp: int, argv: list[str]) -> int:
-    """``--tp N`` in a container started WITHOUT a rank launcher (what the SeldonDeployment's
+    """``--tp N`` (or ``--ep N``) in a container started WITHOUT a rank launcher (what the SeldonDeployment's
     predictor command is): this process becomes the launcher of N fresh rank processes, one
     per visible GPU (``LOCAL_RANK`` indexes ``HIP_VISIBLE_DEVICES``), and never touches the GPU
     itself (no HIP call before the children exist).  Rank 0 serves HTTP on ``--port``, the
@@ -304,9 +304,14 @@ def main(argv=None):
     ap.add_argument("--version", default=os.environ.get("MLOP_MODEL_VERSION", "1"))
     ap.add_argument("--device", default=os.environ.get("MLOP_DEVICE", "cuda"))
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--ep", type=int, default=1,
+                    help="expert-parallel degree with data-parallel attention (MoE; --tp 1): one "
+                         "engine per GPU behind this endpoint (runtime/ep_serving.py)")
     a = ap.parse_args(argv)
-    if a.tp > 1 and "WORLD_SIZE" not in os.environ:
-        raise SystemExit(launch_ranks(a.tp, argv))
+    if a.tp > 1 and a.ep > 1:
+        raise SystemExit("--tp and --ep > 1 together: TP shards experts itself (EP = TP); use one")
+    if max(a.tp, a.ep) > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(max(a.tp, a.ep), argv))
 
     from aiohttp import web
 
@@ -314,6 +319,10 @@ def main(argv=None):
 
     metrics = RuntimeMetrics(model_name=a.name)
     tp_state = None
+    if a.ep > 1:
+        from .ep_serving import serve_ep
+
+        return serve_ep(a, metrics)
     if a.tp > 1 or int(os.environ.get("WORLD_SIZE", 1)) > 1:
         from .tp_worker import serve_tp
 
