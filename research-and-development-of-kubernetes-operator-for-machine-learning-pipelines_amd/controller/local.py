@@ -531,19 +531,27 @@ class Router:
     async def post(self, ns: str, sd: str, path: str, payload: dict, session=None) -> tuple[int, dict, str]:
         import aiohttp
 
-        pod = self.pick(ns, sd)
-        if pod is None or pod.endpoint is None:
-            return 503, {}, ""
         own = session is None
         session = session or aiohttp.ClientSession()
         try:
-            async with session.post(pod.endpoint + path, json=payload) as r:
-                text = await r.text()
+            # a predictor removed by a promotion / rollback while a request was in flight
+            # resets its connection: retry on a freshly picked pod (the mesh's
+            # connect-failure / reset retry policy), 502 when none answers
+            for _ in range(3):
+                pod = self.pick(ns, sd)
+                if pod is None or pod.endpoint is None:
+                    return 503, {}, ""
                 try:
-                    body = json.loads(text) if text else {}
-                except ValueError:  # error responses may be plain text
-                    body = {"error": text}
-                return r.status, body, pod.predictor
+                    async with session.post(pod.endpoint + path, json=payload) as r:
+                        text = await r.text()
+                        try:
+                            body = json.loads(text) if text else {}
+                        except ValueError:  # error responses may be plain text
+                            body = {"error": text}
+                        return r.status, body, pod.predictor
+                except aiohttp.ClientConnectionError as e:
+                    last = f"{type(e).__name__}: {e}"
+            return 502, {"error": last}, ""
         finally:
             if own:
                 await session.close()

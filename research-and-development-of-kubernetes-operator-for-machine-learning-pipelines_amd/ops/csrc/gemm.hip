@@ -391,7 +391,7 @@ int gemm_small_tile(int set) {
 
 // large-M kernel choice (plan() variants below); MLOP_GEMM_BIG_VARIANT at load, and
 // settable at run time (gemm_big_variant op) so A/B microbenches run in one process
-static int g_big_variant = env_int("MLOP_GEMM_BIG_VARIANT", 3);
+static int g_big_variant = env_int("MLOP_GEMM_BIG_VARIANT", 5);
 int gemm_big_variant(int set) {
   if (set >= 0) g_big_variant = set;
   return g_big_variant;
@@ -962,7 +962,8 @@ struct Plan {
 //   batch in one tile (weights read once), BN by how many N tiles fill the chip;
 //   large M: variant 0 = 256x128 (3-stage ring), 1 = 256x256 (2-stage, 128x64 per
 //   wave: half the LDS + L2 bytes per FLOP), 2 = 256x256 + setprio around MFMAs,
-//   3 (default) = 256x256 two-group ping-pong (gemm_pp_kernel).  (A four-wave 128x128-per-wave
+//   3 = 256x256 two-group ping-pong (gemm_pp_kernel), 5 (default) = the four-wave kernel with
+//   the hand-scheduled asm K-loop (gemm_w4.hip) where its grid fills the chip, else 3.  (A four-wave 128x128-per-wave
 //   variant was measured 10-20% slower: profiles/r02_gemm_fourwave_rejected.md.)
 // true when the stream-K tail is available here and splits ALL T (<= C / 2) tiles
 static bool sk_halves_ok(long T, int nk) {
@@ -1016,7 +1017,13 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // below pp_min_tiles the 256x256 grid leaves CUs idle, unless the stream-K tail can cut
     // every tile in two (T <= C / 2): o / down at M = 2040 (128 tiles)
     const bool pp_ok = K % kBK == 0 && (t256 >= pp_min_tiles || sk_halves_ok(t256, K / kBK));
-    if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
+    // variant 5: the four-wave kernel (no stream-K tail) where its data-parallel grid fills
+    // >= w4_min_tiles of the chip's CUs; below that (o / down at M = 2048: 128 tiles) the
+    // ping-pong kernel, whose stream-K tail splits every tile (profiles/r03_gemm_w4.md)
+    static const int w4_min_tiles = env_int("MLOP_GEMM_W4_MIN_TILES", 192);
+    if (big == 5 && !(mrows >= big_min_m && !grouped && t256 >= w4_min_tiles && gemm_w4_ok(M, N, K, K, K))) {
+      if (mrows >= big_min_m && !grouped && pp_ok) { p.BN = 256; p.variant = 3; }
+    } else if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
       p.BN = 256;
       p.variant = big;
     }
@@ -1029,7 +1036,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   const long tiles = (long)n_tiles * real_m_tiles;
   static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 256);  // run49: down -5..-15% at M 8-64
   static const int split_max_tiles = env_int("MLOP_GEMM_SPLIT_MAX_TILES", 160);
-  if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3) {
+  if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3 && p.variant != 5) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
@@ -1048,7 +1055,8 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
                                                       p.m_tiles, st, re)
   if constexpr (EPI == EPI_ROPE) {  // whole heads per staged chunk, no split-K (launch_gemm_rope)
     if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
-    else if (!GROUPED && p.variant == 3) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant == 5 && gemm_w4_ok(M, N, K, lda, ldb)) run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && (p.variant == 3 || p.variant == 5)) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
   } else {
@@ -1075,7 +1083,10 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
     else if (GROUPED && p.variant == 3)
       run_pp<EPI, true>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
-    else if (!GROUPED && p.variant == 3 && p.splits == 1) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant == 5 && p.splits == 1 && gemm_w4_ok(M, N, K, lda, ldb))
+      run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && (p.variant == 3 || p.variant == 5) && p.splits == 1)
+      run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
   }
@@ -1097,7 +1108,7 @@ int gemm_sk_workgroups(int M, int N, int K) {
 // fused into the RoPE + cache kernel (one launch instead of reduce + rope_cache).
 static bool rope_slabs_ok(const Plan& p, int M, int N) {
   const SkBuf* b = sk_buf();
-  return p.splits > 1 && p.variant != 3 && b != nullptr &&
+  return p.splits > 1 && p.variant != 3 && p.variant != 5 && b != nullptr &&
          (size_t)p.splits * M * N <= (size_t)2 * kSkMaxWg * 256 * 256;
 }
 

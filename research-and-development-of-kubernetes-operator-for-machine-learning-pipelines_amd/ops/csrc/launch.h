@@ -56,8 +56,12 @@ bool gemm_rope_stages_v(int M, int N, int K);
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
 long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
-// 8-wave, 3 ping-pong); set >= 0 overrides (in-process A/B), returns the current value
+// 8-wave, 3 ping-pong, 5 four-wave asm K-loop); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
+// variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip); epi 0 / 1 / 3
+bool gemm_w4_ok(int M, int N, int K, int lda, int ldb);
+void run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
+            int K, hipStream_t st, const RopeEpi& re);
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)
 int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fitted BM x BN
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the

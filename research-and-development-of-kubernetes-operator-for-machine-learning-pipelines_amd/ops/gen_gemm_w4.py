@@ -1,0 +1,233 @@
+"""Generator of ``csrc/gemm_w4_asm.h``: the hand-scheduled K-loop of the four-wave
+256 x 256 bf16 GEMM (``csrc/gemm_w4.hip``) as one inline-asm statement.
+
+Why asm: the loop's value is its instruction ORDER -- every MFMA followed by at most one
+LDS read or LDS-DMA issue, barriers placed between MFMAs so the matrix pipe keeps running
+while a wave waits, counted ``lgkmcnt`` per fragment and ``vmcnt`` per tile.  hipcc
+re-orders such a body (a compiler-scheduled four-wave version of the same tiling measured
+126-137 us at 4096^3 vs 103 us for the two-group ping-pong kernel,
+``profiles/r03_gemm_fourwave.md``).  With one wave per SIMD the only latency hiding is
+the interleave itself, so it is written out here instruction by instruction.
+
+Geometry (one workgroup = 4 waves = one 256 x 256 output tile, BK = 64):
+  * wave w = (wm, wn) = (w >> 1, w & 1) owns rows wm*128 .. +127, cols wn*128 .. +127:
+    8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = 256 AGPRs (a[4(8i+j) .. +3]);
+  * LDS: two 64 KiB buffers; buffer b = A rows 0-255 (32 KiB) then B rows 0-255, each row
+    128 B (64 bf16 of K), 16-B chunk c of row r at slot c ^ ((r >> 1) & 7) (the swizzle rides
+    in the DMA SOURCE address; the LDS image is lane-linear per 1 KiB piece);
+  * per K-tile a wave issues 16 LDS-DMA pieces (buffer_load_dwordx4 ... lds; piece
+    p = w + 4i, i = 0..15: i < 8 A rows 8p.., else B rows 8(p - 32)..) and 32 ds_read_b128
+    (A and B fragments for both 32-deep K halves) against 128 MFMAs.
+
+Schedule of iteration t (MFMA slot m = 0..127; H0 = k-half 0 of tile t, H1 = k-half 1):
+  m  1..31   ds_read k-half-1 fragments of tile t (FB1[0..7], FA1[0..7]) from buffer t&1
+  m  38      lgkmcnt(0) + s_barrier (B1): every wave is done reading buffer t&1
+  m 40..100  16 LDS-DMA pieces of tile t+2 into buffer t&1 (one per 4 MFMAs)
+  m  102     vmcnt(16) + s_barrier (B2): tile t+1 (issued one iteration ago) has landed
+  m 103..127 ds_read k-half-0 fragments of tile t+1 (FB0, FA0) from buffer (t+1)&1
+MFMA order: H0 = (i, j) row-major over FA0[i] x FB0[j]; H1 = the same over FA1 x FB1.
+lgkmcnt waits are derived here from the in-order LDS return queue (each MFMA waits only
+for the fragments it reads).  The last two iterations are peeled: t = nk-2 issues no DMA
+(B2 waits vmcnt(0)), t = nk-1 issues neither DMA nor next-tile reads.
+
+Hazards handled in the text (hipcc pads nothing inside an asm statement):
+  * s_mov/s_add m0 -> LDS-DMA: at least one MFMA between them;
+  * fragment registers are rewritten >= 8 MFMAs after their last MFMA reader;
+  * v_accvgpr_write (zeroing) -> first MFMA: the prologue's barrier + reads lie between;
+  * last MFMA -> v_accvgpr_read (readout statements): 3 x s_nop 7 at the end.
+
+Run ``python -m mlopamd.ops.gen_gemm_w4`` to regenerate the header (committed; the build
+does not run Python).
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+OUT = Path(__file__).resolve().parent / "csrc" / "gemm_w4_asm.h"
+
+NF = 8            # fragments per operand per k-half (8 x 16 rows / cols)
+DMA_SLOTS = [40 + 4 * k for k in range(16)]
+B1_SLOT, B2_SLOT = 38, 102
+RD1_SLOTS = [1 + 2 * k for k in range(16)]
+RD0_SLOTS = [103 + round(k * 24 / 15) for k in range(16)]
+TOGGLE1_SLOT = 60           # rA1 / rB1 -> the other buffer (after the k-half-1 reads issued)
+LOOPCTL_SLOT = 127
+
+
+def frag(name, i):
+    return f"%[{name}{i}]"
+
+
+def mfma(q, a, b):
+    return f"v_mfma_f32_16x16x32_bf16 a[{4 * q}:{4 * q + 3}], {a}, {b}, a[{4 * q}:{4 * q + 3}]"
+
+
+class Stream:
+    """Emits instructions and tracks the in-order LDS-read return queue."""
+
+    def __init__(self):
+        self.lines: list[str] = []
+        self.queue: list[str] = []   # outstanding ds_read destinations, issue order
+
+    def emit(self, s):
+        self.lines.append(s)
+
+    def read(self, dst, addr, off):
+        self.emit(f"ds_read_b128 {frag(*dst)}, %[{addr}] offset:{off}")
+        self.queue.append(dst)
+
+    def need(self, *dsts):
+        """Wait until every fragment in dsts has returned."""
+        pos = [self.queue.index(d) for d in dsts if d in self.queue]
+        if not pos:
+            return
+        p = max(pos)
+        cnt = len(self.queue) - 1 - p
+        self.emit(f"s_waitcnt lgkmcnt({min(cnt, 15)})")
+        # lgkmcnt(c) retires everything but the newest c ops (and at least the first p+1)
+        keep = min(cnt, 15)
+        self.queue = self.queue[len(self.queue) - keep:] if keep else []
+
+    def drain(self):
+        self.emit("s_waitcnt lgkmcnt(0)")
+        self.queue = []
+
+
+def reads_k1(s: Stream):
+    """ds_reads of the k-half-1 fragments (FB1 then FA1) of the current tile."""
+    ops = [(("fb1_", j), "rB1", j * 2048) for j in range(NF)] + [(("fa1_", i), "rA1", i * 2048) for i in range(NF)]
+    return ops
+
+
+def reads_k0():
+    return [(("fb0_", j), "rB0", j * 2048) for j in range(NF)] + [(("fa0_", i), "rA0", i * 2048) for i in range(NF)]
+
+
+def body(s: Stream, kind: str):
+    """One K-tile iteration. kind: steady (DMA t+2, reads t+1), nodma (reads t+1), last."""
+    dma = kind == "steady"
+    nxt = kind != "last"
+    slots: dict[int, list] = {m: [] for m in range(129)}
+    for m, op in zip(RD1_SLOTS, reads_k1(s)):
+        slots[m].append(("read", op))
+    if dma:
+        slots[B1_SLOT].append(("b1",))
+        slots[DMA_SLOTS[0] - 1].append(("emit", "s_mov_b32 m0, %[dbase]"))
+        for k, m in enumerate(DMA_SLOTS):
+            srd = "srdA" if k < 8 else "srdB"
+            slots[m].append(("emit", f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen lds"))
+            if k < 15:
+                slots[m].append(("emit", "s_add_u32 m0, m0, 0x1000"))
+        slots[DMA_SLOTS[-1] + 1].append(("emit", "s_add_u32 %[koff], %[koff], 0x80"))
+        slots[DMA_SLOTS[-1] + 1].append(("emit", "s_xor_b32 %[dbase], %[dbase], 0x10000"))
+    slots[TOGGLE1_SLOT].append(("emit", "v_xor_b32_e32 %[rA1], 0x10000, %[rA1]"))
+    slots[TOGGLE1_SLOT].append(("emit", "v_xor_b32_e32 %[rB1], 0x10000, %[rB1]"))
+    if nxt:
+        slots[B2_SLOT].append(("b2", 16 if dma else 0))
+        slots[B2_SLOT].append(("emit", "v_xor_b32_e32 %[rA0], 0x10000, %[rA0]"))
+        slots[B2_SLOT].append(("emit", "v_xor_b32_e32 %[rB0], 0x10000, %[rB0]"))
+        for m, op in zip(RD0_SLOTS, reads_k0()):
+            slots[m].append(("read", op))
+    if kind == "steady":
+        slots[LOOPCTL_SLOT].append(("emit", "s_sub_u32 %[iter], %[iter], 1"))
+        slots[LOOPCTL_SLOT].append(("emit", "s_cmp_lg_u32 %[iter], 0"))
+    for m in range(129):
+        for op in slots[m]:
+            if op[0] == "read":
+                dst, addr, off = op[1]
+                s.read(dst, addr, off)
+            elif op[0] == "emit":
+                s.emit(op[1])
+            elif op[0] == "b1":
+                s.drain()
+                s.emit("s_barrier")
+            elif op[0] == "b2":
+                s.emit(f"s_waitcnt vmcnt({op[1]})")
+                s.emit("s_barrier")
+        if m == 128:
+            break
+        h, mm = divmod(m, 64)
+        i, j = divmod(mm, 8)
+        a, b = (("fa0_", i), ("fb0_", j)) if h == 0 else (("fa1_", i), ("fb1_", j))
+        s.need(a, b)
+        s.emit(mfma(8 * i + j, frag(*a), frag(*b)))
+
+
+def prologue(s: Stream):
+    # s_nop 4: the descriptor / m0 SGPRs may come straight from v_readfirstlane
+    s.emit("s_nop 4")
+    s.emit("s_mov_b32 %[m0save], m0")
+    for t in range(2):   # tiles 0 and 1 -> buffers 0 and 1
+        s.emit("s_mov_b32 m0, %[dbase]")
+        s.emit("s_nop 0")
+        for k in range(16):
+            srd = "srdA" if k < 8 else "srdB"
+            s.emit(f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen lds")
+            if k < 15:
+                s.emit("s_add_u32 m0, m0, 0x1000")
+                s.emit("s_nop 0")
+        s.emit("s_add_u32 %[koff], %[koff], 0x80")
+        s.emit("s_xor_b32 %[dbase], %[dbase], 0x10000")
+    for r in range(256):
+        s.emit(f"v_accvgpr_write_b32 a{r}, 0")
+    s.emit("s_waitcnt vmcnt(16)")
+    s.emit("s_barrier")
+    for dst, addr, off in reads_k0():
+        s.read(dst, addr, off)
+
+
+def kloop() -> list[str]:
+    s = Stream()
+    prologue(s)
+    q0 = list(s.queue)
+    s.emit("s_cmp_eq_u32 %[iter], 0")
+    s.emit("s_cbranch_scc1 L_w4_after_%=")
+    s.emit("L_w4_loop_%=:")
+    body(s, "steady")
+    assert s.queue == q0, "steady body must leave the LDS queue as it found it"
+    s.emit("s_cbranch_scc1 L_w4_loop_%=")
+    s.emit("L_w4_after_%=:")
+    body(s, "nodma")
+    assert s.queue == q0
+    body(s, "last")
+    s.emit("s_nop 7")
+    s.emit("s_nop 7")
+    s.emit("s_nop 7")
+    s.emit("s_mov_b32 m0, %[m0save]")
+    return s.lines
+
+
+def readout(i: int) -> list[str]:
+    """v_accvgpr_read of accumulator row-block i (acc(i, 0..7), 32 AGPRs) into %0..%31."""
+    return [f"v_accvgpr_read_b32 %{k}, a{32 * i + k}" for k in range(32)]
+
+
+def render() -> str:
+    out = ["// GENERATED by mlopamd/ops/gen_gemm_w4.py -- do not edit by hand.",
+           "// The K-loop of gemm_w4_kernel (csrc/gemm_w4.hip): see the generator's docstring.",
+           "#pragma once", ""]
+    lines = kloop()
+    out.append("#define MLOP_W4_KLOOP_ASM \\")
+    for ln in lines:
+        out.append(f'  "{ln}\\n" \\')
+    out.append('  ""')
+    out.append("")
+    for i in range(8):
+        out.append(f"#define MLOP_W4_READ{i}_ASM \\")
+        for ln in readout(i):
+            out.append(f'  "{ln}\\n" \\')
+        out.append('  ""')
+        out.append("")
+    clob = ", ".join(f'"a{r}"' for r in range(256))
+    out.append(f"#define MLOP_W4_AGPR_CLOBBERS {clob}")
+    out.append("")
+    return "\n".join(out)
+
+
+def main():
+    OUT.write_text(render())
+    print(OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,8 @@
 one process, interleaved rounds; cdna_hip_programming.md §5.4 rule 24): the ping-pong 8-wave
 256x256 kernel (gemm.hip, planner variant 3) vs hipBLASLt (torch.matmul).  Plain GEMMs
 (epilogue-free) except gate_up, which the hand-written kernel runs with the fused SiLU-mul
-epilogue (hipBLASLt without it).  Env: BENCH_MS (comma list of row counts)."""
+epilogue (hipBLASLt without it).  Env: BENCH_MS (comma list of row counts), BENCH_VARIANTS
+(planner variants of the hand-written kernel: 3 ping-pong, 5 four-wave asm loop)."""
 import json
 import os
 import sys
@@ -15,6 +16,7 @@ from mlopamd import ops  # noqa: E402
 ops.load()
 dev = torch.device("cuda")
 Ms = [int(m) for m in os.environ.get("BENCH_MS", "2048,4088").split(",")]
+Vs = [int(v) for v in os.environ.get("BENCH_VARIANTS", "3").split(",")]
 ops._sk_reserve(dev)
 ops.GEMM_BACKEND = "mlop"
 
@@ -44,8 +46,8 @@ for M in Ms:
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = (0.02 * torch.randn(N, K, device=dev)).to(torch.bfloat16)
         epi = ops.EPI_SILU_MUL if name == "gate_up" else ops.EPI_NONE
-        cands = {"pp": with_variant(3, lambda: ops.gemm(x, w, epi=epi)),
-                 "hipblaslt": lambda: torch.matmul(x, w.t())}
+        cands = {f"v{v}": with_variant(v, lambda: ops.gemm(x, w, epi=epi)) for v in Vs}
+        cands["hipblaslt"] = lambda: torch.matmul(x, w.t())
         ts = {k: [] for k in cands}
         for _ in range(3):
             for k, f in cands.items():

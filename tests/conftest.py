@@ -23,3 +23,17 @@ def gpu():
 
     ops.load()  # must load: GPU tests never run on a silent fallback
     return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def pp_variant(gpu):
+    """Pin the large-M GEMM planner to the ping-pong kernel (variant 3: the one with the
+    stream-K tail) for the test, whatever the default variant is."""
+    import torch
+
+    prev = torch.ops.mlop.gemm_big_variant(-1)
+    torch.ops.mlop.gemm_big_variant(3)
+    try:
+        yield
+    finally:
+        torch.ops.mlop.gemm_big_variant(prev)

@@ -343,7 +343,7 @@ def test_gemm(gpu, M, N, K):
     (3072, 6144, 4096, 0),    # 288 tiles: 32 tail tiles in 4 ranges of 16 K-tiles
     (2100, 8320, 2048, 0),    # ragged M and N: 297 tiles, 41 tail tiles in 2 halves
 ])
-def test_gemm_stream_k(gpu, M, N, K, epi):
+def test_gemm_stream_k(gpu, pp_variant, M, N, K, epi):
     """Stream-K tail of the ping-pong GEMM (partial tiles through fp32 slots, ticket
     counters, last-arriver fixup + epilogue): vs fp32 matmul, three launches in a row
     (the counters re-arm), and against the data-parallel grid of the same kernel."""

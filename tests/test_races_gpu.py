@@ -76,7 +76,7 @@ def _under_contention(dev, launch, reps=REPS):
     (4352, 4096, 14336, 0),   # 16 tail tiles x 8 ranges (the re-read sum path)
     (3072, 6144, 4096, 0),
 ])
-def test_stream_k_tickets_under_contention(gpu, M, N, K, epi):
+def test_stream_k_tickets_under_contention(gpu, pp_variant, M, N, K, epi):
     torch.manual_seed(M)
     ops._sk_reserve(torch.device(gpu))
     assert torch.ops.mlop.gemm_sk_workgroups(M, N, K) > 0, "shape must take the stream-K tail"
@@ -143,3 +143,27 @@ def test_split_kv_fused_combine_under_contention(gpu):
     assert not bad, f"fused split-KV combine changed on launches {bad}"
     assert int(m.part_sem.abs().sum()) == 0, "semaphores not re-armed"
     torch.testing.assert_close(y0.float(), ref.paged_attention(q, kc, vc, m).float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(4088, 28672, 4096, 1), (4096, 4096, 14336, 0)])
+def test_w4_gemm_under_contention(gpu, M, N, K, epi):
+    """The four-wave GEMM's hand-counted LDS-DMA / ds_read waits (gemm_w4.hip): bit-identical
+    results over many launches while a competing stream keeps the memory system busy (a
+    read placed one wait too early shows up as rare wrong tiles under load)."""
+    torch.manual_seed(M + 1)
+    prev = torch.ops.mlop.gemm_big_variant(-1)
+    torch.ops.mlop.gemm_big_variant(5)
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        y0, bad = _under_contention(gpu, lambda: ops.gemm(x, w, epi=epi))
+    finally:
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
+        torch.ops.mlop.gemm_big_variant(prev)
+    assert not bad, f"four-wave GEMM result changed on launches {bad}"
+    exp = x.float() @ w.float().t()
+    if epi:
+        exp = ref.silu_mul(ops.deinterleave_cols(exp.to(bf)))
+    tol = 3e-2 * exp.abs().max().item() / 10 + 1e-2
+    torch.testing.assert_close(y0.float(), exp.float(), atol=tol, rtol=2e-2)
