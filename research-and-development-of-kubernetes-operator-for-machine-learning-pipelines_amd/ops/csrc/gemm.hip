@@ -1055,7 +1055,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
                                                       p.m_tiles, st, re)
   if constexpr (EPI == EPI_ROPE) {  // whole heads per staged chunk, no split-K (launch_gemm_rope)
     if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
-    else if (!GROUPED && p.variant == 5 && gemm_w4_ok(M, N, K, lda, ldb)) run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant == 5 && gemm_w4_ok(M, N, K, lda, ldb, ldc)) run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && (p.variant == 3 || p.variant == 5)) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
@@ -1083,7 +1083,7 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
     else if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
     else if (GROUPED && p.variant == 3)
       run_pp<EPI, true>(A, lda, B, ldb, C, ldc, M, N, K, st, re, offsets, n_groups);
-    else if (!GROUPED && p.variant == 5 && p.splits == 1 && gemm_w4_ok(M, N, K, lda, ldb))
+    else if (!GROUPED && p.variant == 5 && p.splits == 1 && gemm_w4_ok(M, N, K, lda, ldb, ldc))
       run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && (p.variant == 3 || p.variant == 5) && p.splits == 1)
       run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);

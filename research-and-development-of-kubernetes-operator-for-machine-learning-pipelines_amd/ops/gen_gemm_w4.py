@@ -11,7 +11,9 @@ the interleave itself, so it is written out here instruction by instruction.
 
 Geometry (one workgroup = 4 waves = one 256 x 256 output tile, BK = 64):
   * wave w = (wm, wn) = (w >> 1, w & 1) owns rows wm*128 .. +127, cols wn*128 .. +127:
-    8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = 256 AGPRs (a[4(8i+j) .. +3]);
+    8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 = 256 AGPRs (a[4(8i+j) .. +3]), computed
+    transposed (B fragment as the MFMA's A operand): acc(i, j)[r] of lane l is
+    C[16i + (l & 15)][16j + 4(l >> 4) + r];
   * LDS: two 64 KiB buffers; buffer b = A rows 0-255 (32 KiB) then B rows 0-255, each row
     128 B (64 bf16 of K), 16-B chunk c of row r at slot c ^ ((r >> 1) & 7) (the swizzle rides
     in the DMA SOURCE address; the LDS image is lane-linear per 1 KiB piece);
@@ -58,8 +60,12 @@ def frag(name, i):
     return f"%[{name}{i}]"
 
 
-def mfma(q, a, b):
-    return f"v_mfma_f32_16x16x32_bf16 a[{4 * q}:{4 * q + 3}], {a}, {b}, a[{4 * q}:{4 * q + 3}]"
+def mfma(q, a, b, zero_c=False):
+    # B fragment as the MFMA's A operand: the accumulator holds C^T, so lane l owns C row
+    # (l & 15) of the fragment and FOUR consecutive columns 4(l >> 4) .. +3 -- one 8-byte
+    # store per accumulator in the epilogue instead of four 2-byte ones
+    c = "0" if zero_c else f"a[{4 * q}:{4 * q + 3}]"
+    return f"v_mfma_f32_16x16x32_bf16 a[{4 * q}:{4 * q + 3}], {b}, {a}, {c}"
 
 
 class Stream:
@@ -103,8 +109,9 @@ def reads_k0():
     return [(("fb0_", j), "rB0", j * 2048) for j in range(NF)] + [(("fa0_", i), "rA0", i * 2048) for i in range(NF)]
 
 
-def body(s: Stream, kind: str):
-    """One K-tile iteration. kind: steady (DMA t+2, reads t+1), nodma (reads t+1), last."""
+def body(s: Stream, kind: str, first: bool = False):
+    """One K-tile iteration. kind: steady (DMA t+2, reads t+1), nodma (reads t+1), last.
+    first: the tile's K-tile 0 -- the H0 MFMAs start the accumulators from 0 (no zeroing pass)."""
     dma = kind == "steady"
     nxt = kind != "last"
     slots: dict[int, list] = {m: [] for m in range(129)}
@@ -128,7 +135,7 @@ def body(s: Stream, kind: str):
         slots[B2_SLOT].append(("emit", "v_xor_b32_e32 %[rB0], 0x10000, %[rB0]"))
         for m, op in zip(RD0_SLOTS, reads_k0()):
             slots[m].append(("read", op))
-    if kind == "steady":
+    if kind == "steady" and not first:
         slots[LOOPCTL_SLOT].append(("emit", "s_sub_u32 %[iter], %[iter], 1"))
         slots[LOOPCTL_SLOT].append(("emit", "s_cmp_lg_u32 %[iter], 0"))
     for m in range(129):
@@ -150,36 +157,48 @@ def body(s: Stream, kind: str):
         i, j = divmod(mm, 8)
         a, b = (("fa0_", i), ("fb0_", j)) if h == 0 else (("fa1_", i), ("fb1_", j))
         s.need(a, b)
-        s.emit(mfma(8 * i + j, frag(*a), frag(*b)))
+        s.emit(mfma(8 * i + j, frag(*a), frag(*b), zero_c=first and h == 0))
 
 
-def prologue(s: Stream):
-    # s_nop 4: the descriptor / m0 SGPRs may come straight from v_readfirstlane
-    s.emit("s_nop 4")
-    s.emit("s_mov_b32 %[m0save], m0")
-    for t in range(2):   # tiles 0 and 1 -> buffers 0 and 1
-        s.emit("s_mov_b32 m0, %[dbase]")
+def issue_two(s: Stream, vo: str):
+    """LDS-DMA of a tile's K-tiles 0 and 1 into buffers 0 and 1 (per-lane offsets %[{vo}k])."""
+    for t in range(2):
+        s.emit("s_mov_b32 m0, %[dbase]" if t == 0 else "s_xor_b32 m0, %[dbase], 0x10000")
         s.emit("s_nop 0")
         for k in range(16):
             srd = "srdA" if k < 8 else "srdB"
-            s.emit(f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen lds")
+            soff = "0" if t == 0 else "%[k128]"
+            s.emit(f"buffer_load_dwordx4 %[{vo}{k}], %[{srd}], {soff} offen lds")
             if k < 15:
                 s.emit("s_add_u32 m0, m0, 0x1000")
                 s.emit("s_nop 0")
-        s.emit("s_add_u32 %[koff], %[koff], 0x80")
-        s.emit("s_xor_b32 %[dbase], %[dbase], 0x10000")
-    for r in range(256):
-        s.emit(f"v_accvgpr_write_b32 a{r}, 0")
+
+
+def kloop(n_stores: int) -> list[str]:
+    """One output tile.  Entry: %[first] != 0 -> issue this tile's K-tiles 0 / 1 here; else
+    the previous tile's statement issued them, followed by exactly n_stores epilogue store
+    instructions (vmcnt counts both in issue order).  Exit: %[has_next] != 0 -> K-tiles 0 / 1
+    of the next tile (offsets %[vn*]) are issued into the freed buffers before returning, so
+    their latency hides behind this tile's epilogue."""
+    s = Stream()
+    # s_nop 4: the descriptor / m0 SGPRs may come straight from v_readfirstlane
+    s.emit("s_nop 4")
+    s.emit("s_mov_b32 %[m0save], m0")
+    s.emit("s_cmp_eq_u32 %[first], 0")
+    s.emit("s_cbranch_scc1 L_w4_pref_%=")
+    issue_two(s, "vo")
     s.emit("s_waitcnt vmcnt(16)")
+    s.emit("s_branch L_w4_go_%=")
+    s.emit("L_w4_pref_%=:")
+    assert 16 + n_stores <= 63
+    s.emit(f"s_waitcnt vmcnt({16 + n_stores})")
+    s.emit("L_w4_go_%=:")
     s.emit("s_barrier")
     for dst, addr, off in reads_k0():
         s.read(dst, addr, off)
-
-
-def kloop() -> list[str]:
-    s = Stream()
-    prologue(s)
     q0 = list(s.queue)
+    body(s, "steady", first=True)
+    assert s.queue == q0
     s.emit("s_cmp_eq_u32 %[iter], 0")
     s.emit("s_cbranch_scc1 L_w4_after_%=")
     s.emit("L_w4_loop_%=:")
@@ -190,6 +209,13 @@ def kloop() -> list[str]:
     body(s, "nodma")
     assert s.queue == q0
     body(s, "last")
+    # every wave's LDS reads of this tile are retired (the last MFMAs consumed them): after
+    # this barrier both buffers are free for the next tile's K-tiles 0 / 1
+    s.emit("s_barrier")
+    s.emit("s_cmp_eq_u32 %[has_next], 0")
+    s.emit("s_cbranch_scc1 L_w4_end_%=")
+    issue_two(s, "vn")
+    s.emit("L_w4_end_%=:")
     s.emit("s_nop 7")
     s.emit("s_nop 7")
     s.emit("s_nop 7")
@@ -206,12 +232,14 @@ def render() -> str:
     out = ["// GENERATED by mlopamd/ops/gen_gemm_w4.py -- do not edit by hand.",
            "// The K-loop of gemm_w4_kernel (csrc/gemm_w4.hip): see the generator's docstring.",
            "#pragma once", ""]
-    lines = kloop()
-    out.append("#define MLOP_W4_KLOOP_ASM \\")
-    for ln in lines:
-        out.append(f'  "{ln}\\n" \\')
-    out.append('  ""')
-    out.append("")
+    # one K-loop per epilogue store count: plain (32 x 16-B stores per wave), SiLU-mul (16),
+    # RoPE (0: LDS-staged epilogue, never prefetches a next tile)
+    for ns in (32, 16, 0):
+        out.append(f"#define MLOP_W4_KLOOP_S{ns}_ASM \\")
+        for ln in kloop(ns):
+            out.append(f'  "{ln}\\n" \\')
+        out.append('  ""')
+        out.append("")
     for i in range(8):
         out.append(f"#define MLOP_W4_READ{i}_ASM \\")
         for ln in readout(i):

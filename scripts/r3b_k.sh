@@ -1,0 +1,4 @@
+#!/bin/bash
+source scripts/gpu_check.sh
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+step ksweep 400 python -u scripts/bench_w4_k.py
