@@ -48,12 +48,30 @@ from pathlib import Path
 OUT = Path(__file__).resolve().parent / "csrc" / "gemm_w4_asm.h"
 
 NF = 8            # fragments per operand per k-half (8 x 16 rows / cols)
-DMA_SLOTS = [40 + 4 * k for k in range(16)]
-B1_SLOT, B2_SLOT = 38, 102
-RD1_SLOTS = [1 + 2 * k for k in range(16)]
-RD0_SLOTS = [103 + round(k * 24 / 15) for k in range(16)]
-TOGGLE1_SLOT = 60           # rA1 / rB1 -> the other buffer (after the k-half-1 reads issued)
 LOOPCTL_SLOT = 127
+
+
+class Sched:
+    """Slot placement of one K-tile iteration (slot m = before MFMA m)."""
+
+    def __init__(self, rd1, b1, dma, b2, rd0, toggle1=60):
+        self.rd1, self.b1, self.dma, self.b2, self.rd0, self.toggle1 = rd1, b1, dma, b2, rd0, toggle1
+        assert len(rd1) == 16 and len(rd0) == 16 and len(dma) == 16
+        assert max(rd1) < b1 < min(dma) and b2 < min(rd0) and max(rd0) <= 127 and toggle1 > max(rd1)
+        self.dma_before_b2 = sum(1 for m in dma if m < b2)
+
+
+# S0: all 16 DMAs between the barriers (one per 4 MFMAs), next-tile reads packed at the end
+# S1: earlier B2 (86): DMAs one per 3 MFMAs, next-tile reads one per 2 MFMAs
+# S2: hipBLASLt-like split: 8 DMAs in each half, B2 at the half boundary (64)
+SCHEDS = [
+    Sched(rd1=[1 + 2 * k for k in range(16)], b1=38, dma=[40 + 4 * k for k in range(16)], b2=102,
+          rd0=[103 + round(k * 24 / 15) for k in range(16)]),
+    Sched(rd1=[1 + 2 * k for k in range(16)], b1=36, dma=[38 + 3 * k for k in range(16)], b2=86,
+          rd0=[88 + 2 * k for k in range(16)]),
+    Sched(rd1=[1 + 2 * k for k in range(16)], b1=36, dma=[38 + 3 * k for k in range(8)] + [98 + 3 * k for k in range(8)],
+          b2=64, rd0=[66 + 2 * k for k in range(16)]),
+]
 
 
 def frag(name, i):
@@ -109,31 +127,31 @@ def reads_k0():
     return [(("fb0_", j), "rB0", j * 2048) for j in range(NF)] + [(("fa0_", i), "rA0", i * 2048) for i in range(NF)]
 
 
-def body(s: Stream, kind: str, first: bool = False):
+def body(s: Stream, sc: Sched, kind: str, first: bool = False):
     """One K-tile iteration. kind: steady (DMA t+2, reads t+1), nodma (reads t+1), last.
     first: the tile's K-tile 0 -- the H0 MFMAs start the accumulators from 0 (no zeroing pass)."""
     dma = kind == "steady"
     nxt = kind != "last"
     slots: dict[int, list] = {m: [] for m in range(129)}
-    for m, op in zip(RD1_SLOTS, reads_k1(s)):
+    for m, op in zip(sc.rd1, reads_k1(s)):
         slots[m].append(("read", op))
     if dma:
-        slots[B1_SLOT].append(("b1",))
-        slots[DMA_SLOTS[0] - 1].append(("emit", "s_mov_b32 m0, %[dbase]"))
-        for k, m in enumerate(DMA_SLOTS):
+        slots[sc.b1].append(("b1",))
+        slots[sc.dma[0] - 1].append(("emit", "s_mov_b32 m0, %[dbase]"))
+        for k, m in enumerate(sc.dma):
             srd = "srdA" if k < 8 else "srdB"
             slots[m].append(("emit", f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen lds"))
             if k < 15:
                 slots[m].append(("emit", "s_add_u32 m0, m0, 0x1000"))
-        slots[DMA_SLOTS[-1] + 1].append(("emit", "s_add_u32 %[koff], %[koff], 0x80"))
-        slots[DMA_SLOTS[-1] + 1].append(("emit", "s_xor_b32 %[dbase], %[dbase], 0x10000"))
-    slots[TOGGLE1_SLOT].append(("emit", "v_xor_b32_e32 %[rA1], 0x10000, %[rA1]"))
-    slots[TOGGLE1_SLOT].append(("emit", "v_xor_b32_e32 %[rB1], 0x10000, %[rB1]"))
+        slots[sc.dma[-1] + 1].append(("emit", "s_add_u32 %[koff], %[koff], 0x80"))
+        slots[sc.dma[-1] + 1].append(("emit", "s_xor_b32 %[dbase], %[dbase], 0x10000"))
+    slots[sc.toggle1].append(("emit", "v_xor_b32_e32 %[rA1], 0x10000, %[rA1]"))
+    slots[sc.toggle1].append(("emit", "v_xor_b32_e32 %[rB1], 0x10000, %[rB1]"))
     if nxt:
-        slots[B2_SLOT].append(("b2", 16 if dma else 0))
-        slots[B2_SLOT].append(("emit", "v_xor_b32_e32 %[rA0], 0x10000, %[rA0]"))
-        slots[B2_SLOT].append(("emit", "v_xor_b32_e32 %[rB0], 0x10000, %[rB0]"))
-        for m, op in zip(RD0_SLOTS, reads_k0()):
+        slots[sc.b2].append(("b2", sc.dma_before_b2 if dma else 0))
+        slots[sc.b2].append(("emit", "v_xor_b32_e32 %[rA0], 0x10000, %[rA0]"))
+        slots[sc.b2].append(("emit", "v_xor_b32_e32 %[rB0], 0x10000, %[rB0]"))
+        for m, op in zip(sc.rd0, reads_k0()):
             slots[m].append(("read", op))
     if kind == "steady" and not first:
         slots[LOOPCTL_SLOT].append(("emit", "s_sub_u32 %[iter], %[iter], 1"))
@@ -160,6 +178,12 @@ def body(s: Stream, kind: str, first: bool = False):
         s.emit(mfma(8 * i + j, frag(*a), frag(*b), zero_c=first and h == 0))
 
 
+def suffix(q, q0):
+    """lgkmcnt(N) = 'all but the N newest LDS ops returned': waits derived for the queue q0
+    stay correct for any actual queue that is a suffix of q0 (older entries already retired)."""
+    return q0[len(q0) - len(q):] == q
+
+
 def issue_two(s: Stream, vo: str):
     """LDS-DMA of a tile's K-tiles 0 and 1 into buffers 0 and 1 (per-lane offsets %[{vo}k])."""
     for t in range(2):
@@ -174,7 +198,7 @@ def issue_two(s: Stream, vo: str):
                 s.emit("s_nop 0")
 
 
-def kloop(n_stores: int) -> list[str]:
+def kloop(n_stores: int, sc: Sched) -> list[str]:
     """One output tile.  Entry: %[first] != 0 -> issue this tile's K-tiles 0 / 1 here; else
     the previous tile's statement issued them, followed by exactly n_stores epilogue store
     instructions (vmcnt counts both in issue order).  Exit: %[has_next] != 0 -> K-tiles 0 / 1
@@ -197,18 +221,18 @@ def kloop(n_stores: int) -> list[str]:
     for dst, addr, off in reads_k0():
         s.read(dst, addr, off)
     q0 = list(s.queue)
-    body(s, "steady", first=True)
-    assert s.queue == q0
+    body(s, sc, "steady", first=True)
+    assert suffix(s.queue, q0)
     s.emit("s_cmp_eq_u32 %[iter], 0")
     s.emit("s_cbranch_scc1 L_w4_after_%=")
     s.emit("L_w4_loop_%=:")
-    body(s, "steady")
-    assert s.queue == q0, "steady body must leave the LDS queue as it found it"
+    body(s, sc, "steady")
+    assert suffix(s.queue, q0), "steady body must leave the LDS queue as it found it"
     s.emit("s_cbranch_scc1 L_w4_loop_%=")
     s.emit("L_w4_after_%=:")
-    body(s, "nodma")
-    assert s.queue == q0
-    body(s, "last")
+    body(s, sc, "nodma")
+    assert suffix(s.queue, q0)
+    body(s, sc, "last")
     # every wave's LDS reads of this tile are retired (the last MFMAs consumed them): after
     # this barrier both buffers are free for the next tile's K-tiles 0 / 1
     s.emit("s_barrier")
@@ -234,12 +258,13 @@ def render() -> str:
            "#pragma once", ""]
     # one K-loop per epilogue store count: plain (32 x 16-B stores per wave), SiLU-mul (16),
     # RoPE (0: LDS-staged epilogue, never prefetches a next tile)
-    for ns in (32, 16, 0):
-        out.append(f"#define MLOP_W4_KLOOP_S{ns}_ASM \\")
-        for ln in kloop(ns):
-            out.append(f'  "{ln}\\n" \\')
-        out.append('  ""')
-        out.append("")
+    for si, sc in enumerate(SCHEDS):
+        for ns in (32, 16, 0):
+            out.append(f"#define MLOP_W4_KLOOP_S{ns}_P{si}_ASM \\")
+            for ln in kloop(ns, sc):
+                out.append(f'  "{ln}\\n" \\')
+            out.append('  ""')
+            out.append("")
     for i in range(8):
         out.append(f"#define MLOP_W4_READ{i}_ASM \\")
         for ln in readout(i):
