@@ -884,6 +884,23 @@ static SkBuf* sk_buf() {
   return b.ws && b.cus > 0 ? &b : nullptr;
 }
 
+// partial-tile scratch for the four-wave kernel's split tail (gemm_w4.hip): the same per-device
+// slot buffer and a rotated ticket-counter region; false when the buffers are not reserved
+bool gemm_sk_scratch(float** ws, int** cnt, int* cus) {
+  SkBuf* b = sk_buf();
+  if (!b) return false;
+  *ws = b->ws;
+  *cnt = b->cnt + (size_t)(b->next++ % kCntRegions) * kSkMaxWg;
+  *cus = b->cus;
+  return true;
+}
+
+bool gemm_sk_available(int* cus) {
+  SkBuf* b = sk_buf();
+  if (b && cus) *cus = b->cus;
+  return b != nullptr;
+}
+
 static SkArgs sk_plan(int T, int nk, int& n_sk) {
   SkArgs a{T, T, 1, 0, nullptr, nullptr, T, 256, sk_min_half(), g_skip_dead};
   n_sk = 0;
@@ -1017,11 +1034,12 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // below pp_min_tiles the 256x256 grid leaves CUs idle, unless the stream-K tail can cut
     // every tile in two (T <= C / 2): o / down at M = 2040 (128 tiles)
     const bool pp_ok = K % kBK == 0 && (t256 >= pp_min_tiles || sk_halves_ok(t256, K / kBK));
-    // variant 5: the four-wave kernel (no stream-K tail) where its data-parallel grid fills
-    // >= w4_min_tiles of the chip's CUs; below that (o / down at M = 2048: 128 tiles) the
-    // ping-pong kernel, whose stream-K tail splits every tile (profiles/r03_gemm_w4.md)
+    // variant 5: the four-wave kernel where its grid fills the chip: >= w4_min_tiles tiles, or
+    // a tail it can cut in K-halves (o / down at M = 2048: 128 tiles -> 256 half-tiles); else
+    // the ping-pong kernel with its general stream-K tail
     static const int w4_min_tiles = env_int("MLOP_GEMM_W4_MIN_TILES", 192);
-    if (big == 5 && !(mrows >= big_min_m && !grouped && t256 >= w4_min_tiles && gemm_w4_ok(M, N, K, K, K))) {
+    const bool w4_fills = t256 >= w4_min_tiles || gemm_w4_split_ok((int)t256, K / kBK);
+    if (big == 5 && !(mrows >= big_min_m && !grouped && w4_fills && gemm_w4_ok(M, N, K, K, K))) {
       if (mrows >= big_min_m && !grouped && pp_ok) { p.BN = 256; p.variant = 3; }
     } else if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
       p.BN = 256;

@@ -61,6 +61,10 @@ int gemm_big_variant(int set);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip); epi 0 / 1 / 3
 bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
 int gemm_w4_sched(int set);  // K-loop slot schedule variant (0..2); set >= 0 changes it
+// the four-wave kernel cuts its r = T % CUs tail tiles into K-halves (2r <= CUs, nk even)
+bool gemm_w4_split_ok(int T, int nk);
+bool gemm_sk_scratch(float** ws, int** cnt, int* cus);
+bool gemm_sk_available(int* cus);
 void run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
             int K, hipStream_t st, const RopeEpi& re);
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)

@@ -35,9 +35,12 @@ def w4(gpu, request):
 # every shape has >= 192 256x256 tiles (the planner's threshold for the 256x256 kernels)
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (2048, 6144, 4096), (4088, 4096, 14336),
                                    (3000, 4096, 256), (3000, 4352, 192), (2100, 8448, 2048),
-                                   (5000, 3072, 512), (4096, 16384, 1024), (4088, 28672, 320)])
+                                   (5000, 3072, 512), (4096, 16384, 1024), (4088, 28672, 320),
+                                   # K-half tail items: 384 = 256 + 2 x 128, 128 -> 256 halves
+                                   (4088, 6144, 4096), (2048, 4096, 4096), (2048, 4096, 14336)])
 def test_w4_gemm(gpu, w4, M, N, K):
     torch.manual_seed(M + N + K)
+    ops._sk_reserve(torch.device(gpu))  # the tail split's partial slots / tickets
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.05 * torch.randn(N, K, device=gpu)).to(bf)
     y = ops.gemm(x, w)
@@ -47,9 +50,10 @@ def test_w4_gemm(gpu, w4, M, N, K):
     close(y, y2, atol=0, rtol=0)  # deterministic, no stale LDS between launches
 
 
-@pytest.mark.parametrize("M,I,K", [(4088, 14336, 4096), (3000, 4096, 1024)])
+@pytest.mark.parametrize("M,I,K", [(4088, 14336, 4096), (3000, 4096, 1024), (2040, 14336, 4096)])
 def test_w4_silu_mul(gpu, w4, M, I, K):
     torch.manual_seed(M + I)
+    ops._sk_reserve(torch.device(gpu))
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.05 * torch.randn(2 * I, K, device=gpu)).to(bf)
     y = ops.gemm(x, w, epi=ops.EPI_SILU_MUL)
@@ -65,6 +69,7 @@ def test_w4_qkv_rope_cache(gpu, w4, M, Hq, Hkv):
     N = (Hq + 2 * Hkv) * D
     NB = M // BS + 8
     torch.manual_seed(M)
+    ops._sk_reserve(torch.device(gpu))
     cs = rope_table(D, 8192, 5e5, device=gpu)
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)

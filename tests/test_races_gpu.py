@@ -145,12 +145,15 @@ def test_split_kv_fused_combine_under_contention(gpu):
     torch.testing.assert_close(y0.float(), ref.paged_attention(q, kc, vc, m).float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,N,K,epi", [(4088, 28672, 4096, 1), (4096, 4096, 14336, 0)])
+@pytest.mark.parametrize("M,N,K,epi", [(4088, 28672, 4096, 1), (4096, 4096, 14336, 0),
+                                      (4088, 6144, 4096, 0), (2040, 28672, 4096, 1)])
 def test_w4_gemm_under_contention(gpu, M, N, K, epi):
     """The four-wave GEMM's hand-counted LDS-DMA / ds_read waits (gemm_w4.hip): bit-identical
     results over many launches while a competing stream keeps the memory system busy (a
-    read placed one wait too early shows up as rare wrong tiles under load)."""
+    read placed one wait too early shows up as rare wrong tiles under load), and the K-half
+    tail tiles' sc1 partial hand-off (the last two shapes)."""
     torch.manual_seed(M + 1)
+    ops._sk_reserve(torch.device(gpu))
     prev = torch.ops.mlop.gemm_big_variant(-1)
     torch.ops.mlop.gemm_big_variant(5)
     x = torch.randn(M, K, device=gpu, dtype=bf)
