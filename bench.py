@@ -54,6 +54,8 @@ def parse(argv=None):
     ap.add_argument("--prefill-min-batch", type=int, default=8)
     ap.add_argument("--max-decode-gap", type=int, default=24)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-async", action="store_true",
+                    help="synchronous scheduling (default: step t+1 is launched before step t's tokens are read)")
     ap.add_argument("--no-mixed", action="store_true",
                     help="separate prefill steps instead of prompt chunks riding in the decode step")
     ap.add_argument("--mixed-min-chunk", type=int, default=64)
@@ -101,7 +103,7 @@ def main(argv=None):
                max_model_len=a.max_model_len, use_graphs=not a.no_graphs,
                prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
                mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk,
-               enable_prefix_caching=not a.no_prefix_cache)
+               enable_prefix_caching=not a.no_prefix_cache, async_scheduling=not a.no_async)
     t0 = time.perf_counter()
     leader = True
     if a.tp > 1:
@@ -242,6 +244,7 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
                        "prompt_len": a.prompt_len, "output_len": a.output_len,
                        "parallelism": f"dp{world // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
                        "graphs": not a.no_graphs, "mixed_prefill": not a.no_mixed,
+                       "async_scheduling": not a.no_async,
                        "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap,
                        "shared_prefix": a.shared_prefix, "prefix_cache": not a.no_prefix_cache},
             "p50_cr_ready_s": round(p50_ready, 3),

@@ -165,6 +165,9 @@ class EngineConfig:
     mixed_min_chunk: int = 64     # below this many free token slots, decode alone
     seed: int = 0
     enable_prefix_caching: bool = True  # share computed prompt pages between requests (same prefix)
+    # one-step-ahead scheduling (TP = EP = 1, mixed prefill): step t+1 is built and launched
+    # while step t still runs on the device; step t's tokens are read back afterwards
+    async_scheduling: bool = True
 
 
 @dataclass
@@ -267,6 +270,8 @@ class Engine:
         self.r_nblk = np.zeros(R, np.int64)     # KV pages held
         self.r_sid = np.zeros(R, np.int64)
         self.r_random = np.zeros(R, bool)       # non-greedy sampling
+        self.r_epoch = np.zeros(R, np.int64)    # bumped when a row is released (async: stale results)
+        self.r_tokidx = np.zeros(R, np.int64)   # async: the row's pending token in the in-flight step
         # rows of ``self.running`` in order, and their output lists (kept in step with the
         # list: appended rows go to ``_rows_add``, finished rows are masked out in
         # ``_decode_finish``, a preempted one popped off the end; anything else sets dirty)
@@ -284,6 +289,19 @@ class Engine:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.stats = collections.Counter()
+        # one-step-ahead (async) scheduling state: the in-flight step, its token read-back
+        # buffers (two pinned, alternating) and the event after its metadata upload
+        self._async = (cfg.async_scheduling and cfg.mixed_prefill and self.step_sync is None
+                       and self.ep_sync is None)
+        self._pending = None
+        self._ids_gather = None
+        self._meta_ev = None
+        cuda = self.device.type == "cuda"
+        nmax = self.meta.max_tokens
+        self._toks_h = [torch.zeros(nmax, dtype=torch.int64, pin_memory=cuda) for _ in range(2)]
+        self._toks_flip = 0
+        self._src_h = torch.zeros(R, dtype=torch.int64, pin_memory=cuda)
+        self._src_d = torch.zeros(R, dtype=torch.int64, device=self.device)
         self.stats["kv_alloc_ms"] = kv_alloc_ms
         self.stats.update(self.kv.timing_ms)
         self.tracer = StepTracer()
@@ -342,7 +360,7 @@ class Engine:
         self._finish(seq, "abort")
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.prefilling or self.running)
+        return bool(self.waiting or self.prefilling or self.running or self._pending_alive())
 
     @property
     def num_running(self) -> int:
@@ -372,6 +390,7 @@ class Engine:
         seq.n_reg = 0
         if seq.row >= 0:
             self.r_nblk[seq.row] = 0
+            self.r_epoch[seq.row] += 1  # an in-flight step's result for this row is stale
             self.free_rows.append(seq.row)
             seq.row = -1
         seq.num_cached = 0
@@ -457,6 +476,8 @@ class Engine:
             if self.kv.fill_failed:
                 self.stats["kv_fill_failed"] = 1
                 self.stats["kv_blocks_backed"] = self.alloc.available
+        if self._async and (self._pending is not None or self.running):
+            return self._async_step()
         if self._want_prefill():
             if self.running and self.cfg.mixed_prefill:
                 kind, out = "mixed", self._mixed_step()
@@ -629,6 +650,227 @@ class Engine:
         return StepBatch(np.concatenate([d_out.seq_ids, p.seq_ids]), np.concatenate([d_out.tokens, p.tokens]),
                          np.concatenate([d_out.fin, p.fin]), reasons)
 
+    # ------------------------------------------------- async scheduling --
+    # Step t+1 is built from the scheduler state as it stands after step t's LAUNCH: every
+    # running row decodes again (a row whose step-t token turns out to be EOS / a stop token
+    # is computed once more and its result dropped), its input id is gathered on the device
+    # from step t's sampled tokens, and lengths / page needs are advanced at launch time (they
+    # do not depend on token values).  Step t's tokens are read back (pinned copy + event,
+    # so the read waits for step t only, never for the step queued behind it) and applied
+    # after step t+1 is queued: the host's bookkeeping and the next step's preparation run
+    # while the device computes, and the device never waits for the host between steps.
+    # A row's results are stale once it was released (finish, abort, preemption): r_epoch.
+
+    def _pending_alive(self) -> bool:
+        p = self._pending
+        if p is None:
+            return False
+        rows, ep = p["rows"], p["epochs"]
+        return bool(len(rows)) and bool((self.r_epoch[rows] == ep).any())
+
+    def _wait_meta(self):
+        """The previous step's metadata H2D has executed: the host buffers may be rewritten."""
+        ev, self._meta_ev = self._meta_ev, None
+        if ev is not None:
+            ev.synchronize()
+
+    def _async_step(self):
+        prev, self._pending = self._pending, None
+        kind, pend = "idle", None
+        if self.running:
+            self._wait_meta()
+            if self._want_prefill():
+                pend = self._async_launch(prev, mixed=True)
+                if pend is not None:
+                    kind = "mixed"
+                    self._decode_since_prefill = 0
+            if pend is None:
+                self._decode_since_prefill += 1
+                pend = self._async_launch(prev, mixed=False)
+                kind = "decode" if pend is not None else kind
+        self._pending = pend
+        out = self._async_post(prev) if prev is not None else StepBatch.from_list([])
+        return kind, out
+
+    def _async_launch(self, prev, mixed: bool):
+        """Build, launch and advance one step; returns its pending record (None: nothing to run)."""
+        t0 = time.perf_counter()
+        rows, ctx_d = self._decode_rows()
+        B = len(rows)
+        if B == 0:
+            return None
+        ctx_d = ctx_d.astype(np.int32)
+        batch, chunks = [], []
+        if mixed:
+            budget = self.cfg.max_num_batched_tokens - B
+            if budget < self.cfg.mixed_min_chunk:
+                return None
+            batch, chunks = self._collect_prefill(budget)
+            if not batch:
+                return None
+        # decode input ids: on the device from the in-flight step, else the host's last token
+        gather = prev is not None and prev.get("toks_d") is not None
+        last = np.zeros(B, np.int64) if gather else self.r_last[rows]
+        dparams = self._params_of_running()
+        greedy = getattr(dparams, "all_greedy", False)
+        if mixed:
+            p_rows = [s.row for s in batch]
+            p_ctx = [s.num_cached + n for s, n in zip(batch, chunks)]
+            p_toks = [s.tokens(s.num_cached, c) for s, c in zip(batch, p_ctx)]
+            done = [c == s.length for s, c in zip(batch, p_ctx)]
+            T, nt, nl = self.meta.fill_mixed(rows, ctx_d, last, p_rows, chunks, p_ctx, p_toks, want_logits=done)
+            part, nparts = plan_partitions(nt, self.model.n_kv, max(int(ctx_d.max()), max(p_ctx)))
+            done_seqs = [s for s, d in zip(batch, done) if d]
+            if greedy and all(s.params.greedy for s in done_seqs):
+                params = _ALL_GREEDY
+            else:
+                params = _ParamsList([s.params for s in self.running] + [s.params for s in done_seqs])
+            launch = (KIND_EAGER, T, nt, nl, part, nparts, 0)
+            greedy = getattr(params, "all_greedy", False)
+        else:
+            done_seqs = []
+            params = dparams
+            bucket = next((b for b in self.buckets if b >= B), None)
+            if bucket is not None and self.graphs.get(bucket) is not None:
+                self.meta.fill_decode(rows, ctx_d, last, pad_to=bucket)
+                launch = (KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket)
+            else:
+                self.meta.fill_decode(rows, ctx_d, last, pad_to=B)
+                part, nparts = plan_partitions(B, self.model.n_kv, int(ctx_d.max()))
+                launch = (KIND_EAGER, B, B, B, part, nparts, 0)
+        if gather:
+            self._src_h[:B].copy_(torch.from_numpy(self.r_tokidx[rows]))
+            self._ids_gather = (B, prev["toks_d"])
+        t1 = time.perf_counter()
+        logits = self._launch(*launch, greedy=greedy)
+        if launch[0] == KIND_GRAPH:
+            logits = logits[:B]
+        toks_d = self._sample(logits, params)
+        n = int(toks_d.shape[0])
+        toks_h = self._toks_h[self._toks_flip][:n]
+        self._toks_flip ^= 1
+        ev = None
+        if self.device.type == "cuda":
+            toks_h.copy_(toks_d, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            toks_h.copy_(toks_d)
+        # advance what does not depend on token values: decode rows gained a token (pending)
+        seqs_d = list(self.running)  # aligned with rows (_decode_rows synced them)
+        self.r_len[rows] += 1
+        self.r_gen[rows] += 1
+        self.r_tokidx[rows] = np.arange(B)
+        self.stats["decode_tokens"] += B
+        if mixed:
+            self.stats["mixed_steps"] += 1
+            self.stats["prefill_tokens"] += T - B
+            self._prefill_advance(batch, p_ctx, done, B)
+        elif launch[0] == KIND_GRAPH:
+            self.stats["graph_steps"] += 1
+            self.stats["decode_steps"] += 1
+        else:
+            self.stats["eager_decode_steps"] += 1
+            self.stats["decode_steps"] += 1
+        snap_rows = np.concatenate([rows, np.asarray([s.row for s in done_seqs], dtype=rows.dtype)])
+        pend = {"rows": snap_rows, "epochs": self.r_epoch[snap_rows].copy(), "seqs": seqs_d + done_seqs,
+                "toks_d": toks_d, "toks_h": toks_h, "ev": ev, "retire": set()}
+        self._retire_by_length(pend)
+        self.stats["async_host_us"] += int(1e6 * (t1 - t0 + time.perf_counter() - t1))
+        return pend
+
+    def _prefill_advance(self, batch, ctx, done, B):
+        """Prompt chunks of a launched step: cached lengths, prefix pages, and the sequences
+        whose prompt completed join the running rows (their first token is pending)."""
+        j = 0
+        for s, c, d in zip(batch, ctx, done):
+            s.num_cached = c
+            if self.cfg.enable_prefix_caching:
+                self._register_prefix(s, c)
+            if d:
+                self.prefilling.remove(s)
+                s.status = Status.RUNNING
+                self.running.append(s)
+                r, p = s.row, s.params
+                self.r_random[r] = not p.greedy
+                self.r_len[r], self.r_gen[r], self.r_maxgen[r] = s.length + 1, len(s.output) + 1, p.max_tokens
+                self.r_ignore[r], self.r_hasstop[r], self.r_sid[r] = p.ignore_eos, bool(p.stop_token_ids), s.seq_id
+                self.r_tokidx[r] = B + j
+                self._rows_add.append(r)
+                j += 1
+
+    def _retire_by_length(self, pend):
+        """Rows whose pending token is their last (max_tokens / max_model_len) leave the
+        running set now; they finish when that token is applied."""
+        rows = self._sync_rows()
+        fin = (self.r_gen[rows] >= self.r_maxgen[rows]) | (self.r_len[rows] >= self.max_model_len)
+        if not fin.any():
+            return
+        run = self.running
+        fi = np.nonzero(fin)[0]
+        pend["retire"] = {run[i].seq_id for i in fi.tolist()}
+        keep = np.nonzero(~fin)[0]
+        get = operator.itemgetter(*keep.tolist()) if len(keep) > 1 else None
+        if len(keep) == 0:
+            self.running, self._outs = [], []
+        elif len(keep) == 1:
+            self.running, self._outs = [run[keep[0]]], [self._outs[keep[0]]]
+        else:
+            self.running, self._outs = list(get(run)), list(get(self._outs))
+        self._rows = rows[keep]
+
+    def _async_post(self, pend) -> StepBatch:
+        """Apply an in-flight step's tokens (waits for that step only)."""
+        t0 = time.perf_counter()
+        if pend["ev"] is not None:
+            pend["ev"].synchronize()
+        rows = pend["rows"]
+        n = len(rows)
+        toks = pend["toks_h"][:n].numpy().copy() if n else np.zeros(0, np.int64)
+        alive = self.r_epoch[rows] == pend["epochs"]
+        if not alive.all():
+            ai = np.nonzero(alive)[0]
+            rows, toks = rows[ai], toks[ai]
+            seqs = [pend["seqs"][i] for i in ai.tolist()]
+        else:
+            seqs = pend["seqs"]
+        if not len(rows):
+            return StepBatch.from_list([])
+        now = time.perf_counter()
+        for s in seqs:
+            if s.first_token_time is None:
+                s.first_token_time = now
+        collections.deque(map(list.append, [s.output for s in seqs], toks.tolist()), maxlen=0)
+        self.r_last[rows] = toks
+        eos = self.model.cfg.eos_ids
+        is_eos = (toks == eos[0]) if len(eos) == 1 else np.isin(toks, eos)
+        fin_stop = (~self.r_ignore[rows]) & is_eos
+        for i in np.nonzero(self.r_hasstop[rows])[0].tolist():
+            if int(toks[i]) in seqs[i].params.stop_token_ids:
+                fin_stop[i] = True
+        retire = pend["retire"]
+        fin_len = np.zeros(len(rows), bool)
+        if retire:
+            fin_len = np.fromiter((s.seq_id in retire for s in seqs), dtype=bool, count=len(seqs))
+        fin = fin_stop | fin_len
+        sids = self.r_sid[rows].copy()
+        reasons = {}
+        fi = np.nonzero(fin)[0]
+        if len(fi):
+            done = [seqs[i] for i in fi.tolist()]
+            stopped = set()
+            for i, s in zip(fi.tolist(), done):
+                reasons[s.seq_id] = "stop" if fin_stop[i] else "length"
+                if s.seq_id not in retire:
+                    stopped.add(s.seq_id)
+            if stopped:  # still in the running set (speculatively decoding again)
+                self.running = [s for s in self.running if s.seq_id not in stopped]
+                self._rows_dirty = True
+            for s in done:
+                self._finish(s, reasons[s.seq_id])
+        self.stats["async_host_us"] += int(1e6 * (time.perf_counter() - t0))
+        return StepBatch(sids, toks, fin, reasons)
+
     # ----------------------------------------------------------- decode --
     def _decode_rows(self):
         """Rows of the running batch with a KV slot for their next token: only rows
@@ -652,7 +894,8 @@ class Engine:
             ok = True
             for i in need.tolist():
                 s = self.running[i]
-                if not self._ensure_blocks(s, s.length):
+                # the row's length (async: it counts the in-flight step's token, s.length not yet)
+                if not self._ensure_blocks(s, int(ctx[i])):
                     self._preempt(self.running.pop())  # newest goes back to the queue
                     self._rows = self._rows[:-1]
                     self._outs.pop()
@@ -789,6 +1032,17 @@ class Engine:
             self.stats["tp_sync_calls"] += 1
         else:
             self.meta.upload(T, nl)
+        g = self._ids_gather
+        if g is not None:
+            # async: decode rows' input ids = the previous (in-flight) step's sampled tokens,
+            # gathered on the device after the metadata H2D (which carried placeholders)
+            self._ids_gather = None
+            B, toks_d = g
+            self._src_d[:B].copy_(self._src_h[:B], non_blocking=True)
+            self.meta.ids_d[:B].copy_(toks_d.index_select(0, self._src_d[:B]))
+        if self._async and self.device.type == "cuda":
+            self._meta_ev = torch.cuda.Event()
+            self._meta_ev.record()
         return self._execute(kind, T, nt, nl, part, nparts, bucket, npt, greedy)
 
     def _ep_agree(self, kind, T, nt, nl, part, nparts, bucket):

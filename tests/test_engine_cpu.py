@@ -351,3 +351,41 @@ def test_multiple_eos_ids_stop_generation(tiny):
                                  use_graphs=False))
     (out,) = eng.generate([prompt], SamplingParams(max_tokens=6))
     assert out == free[:3]
+
+
+@pytest.mark.parametrize("graphs_like_bucket", [False, True])
+def test_async_scheduling_matches_sync(tiny, graphs_like_bucket):
+    """One-step-ahead scheduling (step t+1 launched before step t's tokens are applied; decode
+    ids gathered on the device from the in-flight step; EOS / stop-token rows decoded once
+    more and their stale result dropped; aborts and preemption mid-flight) produces exactly
+    the synchronous engine's outputs and finish reasons."""
+    rng = np.random.default_rng(11)
+    prompts = [rng.integers(2, 500, size=int(rng.integers(3, 50))).tolist() for _ in range(14)]
+    # stop tokens that will actually fire: each odd request stops at its own 3rd greedy token
+    probe = Engine(tiny, EngineConfig(max_num_seqs=8, max_model_len=256, num_kv_blocks=64, use_graphs=False,
+                                      async_scheduling=False))
+    third = probe.generate(prompts, SamplingParams(max_tokens=3, ignore_eos=True))
+    params = [SamplingParams(max_tokens=int(4 + i % 9), ignore_eos=True,
+                             stop_token_ids=[third[i][2]] if i % 2 else []) for i in range(len(prompts))]
+
+    def run(asy):
+        eng = Engine(tiny, EngineConfig(max_num_seqs=5, max_num_batched_tokens=40, max_model_len=256,
+                                        num_kv_blocks=14, use_graphs=False, mixed_min_chunk=8,
+                                        async_scheduling=asy, prefill_min_batch=1 if graphs_like_bucket else 2))
+        seqs, i, it = [], 0, 0
+        while i < len(prompts) or eng.has_work():
+            if i < len(prompts) and it % 2 == 0:
+                seqs.append(eng.add_request(prompts[i], params[i]))
+                i += 1
+            if it == 12:
+                eng.abort(seqs[-1].seq_id)  # just admitted: prefilling or with a token in flight
+            eng.step()
+            it += 1
+        assert eng.alloc.num_free == eng.alloc.available - 1
+        return [(s.output, s.finish_reason) for s in seqs], eng.stats
+
+    sync, _ = run(False)
+    asy, st = run(True)
+    assert st["async_host_us"] > 0
+    assert asy == sync
+    assert any(r == "stop" for _, r in asy) and any(r == "abort" for _, r in asy)
