@@ -256,10 +256,9 @@ def render() -> str:
     out = ["// GENERATED by mlopamd/ops/gen_gemm_w4.py -- do not edit by hand.",
            "// The K-loop of gemm_w4_kernel (csrc/gemm_w4.hip): see the generator's docstring.",
            "#pragma once", ""]
-    # one K-loop per epilogue store count: plain (32 x 16-B stores per wave), SiLU-mul (16),
-    # RoPE (0: LDS-staged epilogue, never prefetches a next tile)
+    # one K-loop per epilogue store count: plain and RoPE (32 x 16-B stores per wave), SiLU-mul (16)
     for si, sc in enumerate(SCHEDS):
-        for ns in (32, 16, 0):
+        for ns in (32, 16):
             out.append(f"#define MLOP_W4_KLOOP_S{ns}_P{si}_ASM \\")
             for ln in kloop(ns, sc):
                 out.append(f'  "{ln}\\n" \\')
