@@ -115,10 +115,14 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// SiLU of a bf16-rounded gate, rounded to bf16 (the GEMM epilogues' rounding)
+// SiLU of a bf16-rounded gate, rounded to bf16 (the GEMM epilogues' rounding).  The quotient
+// is v_rcp_f32 x v_mul (1 ulp reciprocal, invisible after the bf16 rounding): an
+// IEEE '/' expands to a ~10-instruction div_scale / div_fmas / div_fixup sequence, which in the
+// four-wave GEMM's SiLU-mul epilogue (128 quotients per lane per tile, nothing to overlap
+// with) was several microseconds per tile.  Large negative gates: exp -> inf, rcp -> 0, -0.
 __device__ __forceinline__ float silu_bf(float g) {
   const float gb = bf2f(f2bf(g));
-  return bf2f(f2bf(gb / (1.f + __expf(-gb))));
+  return bf2f(f2bf(gb * __builtin_amdgcn_rcpf(1.f + __expf(-gb))));
 }
 
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -26,8 +26,8 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(uint16_t* __restrict__ ou
     for (int j = 0; j < 4; ++j) {
       // HF computes silu in bf16 then multiplies in bf16: round after silu
       float g0 = lo_bf(g[j]), g1 = hi_bf(g[j]);
-      float s0 = bf2f(f2bf(g0 / (1.f + __expf(-g0))));
-      float s1 = bf2f(f2bf(g1 / (1.f + __expf(-g1))));
+      float s0 = bf2f(f2bf(g0 * __builtin_amdgcn_rcpf(1.f + __expf(-g0))));
+      float s1 = bf2f(f2bf(g1 * __builtin_amdgcn_rcpf(1.f + __expf(-g1))));
       o[j] = pack2(s0 * lo_bf(u[j]), s1 * hi_bf(u[j]));
     }
     *reinterpret_cast<u32x4*>(out + m * (long)I + c) = o;
