@@ -57,4 +57,5 @@ for M in [int(m) for m in os.environ.get("BENCH_MS", "4088,2048").split(",")]:
         t = timeit(lambda: ops.rope_cache(qkv, pos, cs, slots, kc, vc, Hq, q))
         res["rope_cache_only"] = min(res.get("rope_cache_only", 1e9), t)
     torch.ops.mlop.gemm_big_variant(5)
-    print(json.dumps({"M": M, **{k: round(v, 1) for k, v in res.items()}}), flush=True)
+    print(json.dumps({"M": M, "v_stage": os.environ.get("MLOP_V_STAGE", "1"),
+                      **{k: round(v, 1) for k, v in res.items()}}), flush=True)
