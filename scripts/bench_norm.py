@@ -1,5 +1,8 @@
 """add + RMSNorm / RMSNorm at the headline's row counts (Llama-3-8B hidden 4096): us per call
-and the implied bytes/s (x, residual read + written, out written; weight from L2)."""
+and the implied bytes/s (x, residual read + written, out written; weight from L2).  Measured
+2026-10-17 (scripts/r3b_norm.sh): add + RMSNorm 19.9 us at M = 4088 = 6.7 TB/s, RMSNorm 10.9 us
+= 6.1 TB/s, i.e. at the HBM roof; loading the weight with the row (one round trip instead of
+two) changed nothing (19.85 vs 19.93 us) and was not kept."""
 import json
 import os
 import sys
