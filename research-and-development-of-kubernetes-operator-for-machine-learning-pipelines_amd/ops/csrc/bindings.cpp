@@ -215,7 +215,6 @@ int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_
 int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
-int64_t gemm_w4_sched(int64_t set) { return mlop::gemm_w4_sched((int)set); }
 int64_t gemm_small_stages(int64_t set) { return mlop::gemm_small_stages((int)set); }
 int64_t gemm_small_tile(int64_t set) { return mlop::gemm_small_tile((int)set); }
 int64_t gemm_sk_mode(int64_t set) { return mlop::gemm_sk_mode((int)set); }
@@ -558,7 +557,6 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
-  m.def("gemm_w4_sched(int set=-1) -> int", &gemm_w4_sched);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
   m.def("gemm_small_tile(int set=-1) -> int", &gemm_small_tile);
   m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);

@@ -60,7 +60,6 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 int gemm_big_variant(int set);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip); epi 0 / 1 / 3
 bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
-int gemm_w4_sched(int set);  // K-loop slot schedule variant (0..2); set >= 0 changes it
 // the four-wave kernel cuts its r = T % CUs tail tiles into K-halves (2r <= CUs, nk even)
 bool gemm_w4_split_ok(int T, int nk);
 bool gemm_sk_scratch(float** ws, int** cnt, int* cus);

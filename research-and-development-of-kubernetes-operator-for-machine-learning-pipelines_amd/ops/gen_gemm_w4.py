@@ -54,24 +54,20 @@ LOOPCTL_SLOT = 127
 class Sched:
     """Slot placement of one K-tile iteration (slot m = before MFMA m)."""
 
-    def __init__(self, rd1, b1, dma, b2, rd0, toggle1=60):
+    def __init__(self, rd1, b1, dma, b2, rd0, toggle1=60, pol_a="", pol_b=""):
         self.rd1, self.b1, self.dma, self.b2, self.rd0, self.toggle1 = rd1, b1, dma, b2, rd0, toggle1
+        self.pol = {"srdA": pol_a, "srdB": pol_b}  # cache-policy bits of each operand's LDS-DMA
         assert len(rd1) == 16 and len(rd0) == 16 and len(dma) == 16
         assert max(rd1) < b1 < min(dma) and b2 < min(rd0) and max(rd0) <= 127 and toggle1 > max(rd1)
         self.dma_before_b2 = sum(1 for m in dma if m < b2)
 
 
-# S0: all 16 DMAs between the barriers (one per 4 MFMAs), next-tile reads packed at the end
-# S1: earlier B2 (86): DMAs one per 3 MFMAs, next-tile reads one per 2 MFMAs
-# S2: hipBLASLt-like split: 8 DMAs in each half, B2 at the half boundary (64)
-SCHEDS = [
-    Sched(rd1=[1 + 2 * k for k in range(16)], b1=38, dma=[40 + 4 * k for k in range(16)], b2=102,
-          rd0=[103 + round(k * 24 / 15) for k in range(16)]),
-    Sched(rd1=[1 + 2 * k for k in range(16)], b1=36, dma=[38 + 3 * k for k in range(16)], b2=86,
-          rd0=[88 + 2 * k for k in range(16)]),
-    Sched(rd1=[1 + 2 * k for k in range(16)], b1=36, dma=[38 + 3 * k for k in range(8)] + [98 + 3 * k for k in range(8)],
-          b2=64, rd0=[66 + 2 * k for k in range(16)]),
-]
+# All 16 DMAs between the barriers (one per 4 MFMAs), next-tile reads packed at the end.
+# Measured and dropped (profiles/r03_gemm_w4.md): B2 at MFMA 86 with one DMA per 3 MFMAs, a
+# hipBLASLt-like 8 + 8 DMA split around B2 at the half boundary (both within 1 %), and
+# non-temporal weight / activation DMAs (2-8 % slower).
+SCHEDS = [Sched(rd1=[1 + 2 * k for k in range(16)], b1=38, dma=[40 + 4 * k for k in range(16)], b2=102,
+                rd0=[103 + round(k * 24 / 15) for k in range(16)])]
 
 
 def frag(name, i):
@@ -140,7 +136,7 @@ def body(s: Stream, sc: Sched, kind: str, first: bool = False):
         slots[sc.dma[0] - 1].append(("emit", "s_mov_b32 m0, %[dbase]"))
         for k, m in enumerate(sc.dma):
             srd = "srdA" if k < 8 else "srdB"
-            slots[m].append(("emit", f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen lds"))
+            slots[m].append(("emit", f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen{sc.pol[srd]} lds"))
             if k < 15:
                 slots[m].append(("emit", "s_add_u32 m0, m0, 0x1000"))
         slots[sc.dma[-1] + 1].append(("emit", "s_add_u32 %[koff], %[koff], 0x80"))
@@ -184,7 +180,7 @@ def suffix(q, q0):
     return q0[len(q0) - len(q):] == q
 
 
-def issue_two(s: Stream, vo: str):
+def issue_two(s: Stream, vo: str, sc: Sched):
     """LDS-DMA of a tile's K-tiles 0 and 1 into buffers 0 and 1 (per-lane offsets %[{vo}k])."""
     for t in range(2):
         s.emit("s_mov_b32 m0, %[dbase]" if t == 0 else "s_xor_b32 m0, %[dbase], 0x10000")
@@ -192,7 +188,7 @@ def issue_two(s: Stream, vo: str):
         for k in range(16):
             srd = "srdA" if k < 8 else "srdB"
             soff = "0" if t == 0 else "%[k128]"
-            s.emit(f"buffer_load_dwordx4 %[{vo}{k}], %[{srd}], {soff} offen lds")
+            s.emit(f"buffer_load_dwordx4 %[{vo}{k}], %[{srd}], {soff} offen{sc.pol[srd]} lds")
             if k < 15:
                 s.emit("s_add_u32 m0, m0, 0x1000")
                 s.emit("s_nop 0")
@@ -210,7 +206,7 @@ def kloop(n_stores: int, sc: Sched) -> list[str]:
     s.emit("s_mov_b32 %[m0save], m0")
     s.emit("s_cmp_eq_u32 %[first], 0")
     s.emit("s_cbranch_scc1 L_w4_pref_%=")
-    issue_two(s, "vo")
+    issue_two(s, "vo", sc)
     s.emit("s_waitcnt vmcnt(16)")
     s.emit("s_branch L_w4_go_%=")
     s.emit("L_w4_pref_%=:")
@@ -238,7 +234,7 @@ def kloop(n_stores: int, sc: Sched) -> list[str]:
     s.emit("s_barrier")
     s.emit("s_cmp_eq_u32 %[has_next], 0")
     s.emit("s_cbranch_scc1 L_w4_end_%=")
-    issue_two(s, "vn")
+    issue_two(s, "vn", sc)
     s.emit("L_w4_end_%=:")
     s.emit("s_nop 7")
     s.emit("s_nop 7")

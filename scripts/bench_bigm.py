@@ -17,7 +17,6 @@ ops.load()
 dev = torch.device("cuda")
 Ms = [int(m) for m in os.environ.get("BENCH_MS", "2048,4088").split(",")]
 Vs = [int(v) for v in os.environ.get("BENCH_VARIANTS", "3").split(",")]
-Ss = [int(v) for v in os.environ.get("BENCH_W4_SCHEDS", "-1").split(",")]  # four-wave slot schedules
 ops._sk_reserve(dev)
 ops.GEMM_BACKEND = "mlop"
 
@@ -35,10 +34,9 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3
 
 
-def with_variant(v, fn, sched=-1):
+def with_variant(v, fn):
     def run():
         torch.ops.mlop.gemm_big_variant(v)
-        torch.ops.mlop.gemm_w4_sched(sched)
         return fn()
     return run
 
@@ -48,10 +46,7 @@ for M in Ms:
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = (0.02 * torch.randn(N, K, device=dev)).to(torch.bfloat16)
         epi = ops.EPI_SILU_MUL if name == "gate_up" else ops.EPI_NONE
-        cands = {}
-        for v in Vs:
-            for sc in (Ss if v == 5 else [-1]):
-                cands[f"v{v}" + (f"s{sc}" if sc >= 0 else "")] = with_variant(v, lambda: ops.gemm(x, w, epi=epi), sc)
+        cands = {f"v{v}": with_variant(v, lambda: ops.gemm(x, w, epi=epi)) for v in Vs}
         cands["hipblaslt"] = lambda: torch.matmul(x, w.t())
         ts = {k: [] for k in cands}
         for _ in range(3):

@@ -16,19 +16,15 @@ def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=lambda v: f"sched{v}")
-def w4(gpu, request):
-    """variant 5 with each K-loop slot schedule (gen_gemm_w4.py SCHEDS)"""
+@pytest.fixture
+def w4(gpu):
     prev = torch.ops.mlop.gemm_big_variant(-1)
-    prev_s = torch.ops.mlop.gemm_w4_sched(-1)
     torch.ops.mlop.gemm_big_variant(5)
-    torch.ops.mlop.gemm_w4_sched(request.param)
     ops.GEMM_BACKEND = "mlop"
     try:
         yield
     finally:
         torch.ops.mlop.gemm_big_variant(prev)
-        torch.ops.mlop.gemm_w4_sched(prev_s)
         ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
 
 
