@@ -59,6 +59,9 @@ class LlamaModel:
         self.final_norm = init_norm(H, self.device, dtype)
         self.lm_head = self.embed if cfg.tie_embeddings else w(self.vocab_local, H)
         self.cos_sin = rope_table(D, cfg.max_position, cfg.rope_theta, cfg.rope_scaling, self.device)
+        # in_norm / post_norm weights all ones (random init, or after fold_norms()): the large-M
+        # TP=1 forward may then run the norm chain (ops.gemm_res_ss / gemm_rs)
+        self.unit_norms = True
 
     # ---------------------------------------------------------- sharding --
     @torch.no_grad()
@@ -87,7 +90,25 @@ class LlamaModel:
         cp(self.final_norm, full.final_norm)
         if self.lm_head is not self.embed:
             cp(self.lm_head, full.lm_head[vs[0]:vs[1]])
+        self.unit_norms = all(bool((L[k] == 1).all()) for L in self.layers for k in ("in_norm", "post_norm"))
         return self
+
+    @torch.no_grad()
+    def fold_norms(self) -> "LlamaModel":
+        """Fold each RMSNorm weight into the projection that consumes it (in_norm -> qkv,
+        post_norm -> gate_up: W[:, k] *= g[k]) and set the norm weights to ones, so the large-M
+        forward can apply the normalisation as a per-row factor after the GEMM (norm chain).
+        The same function up to the bf16 rounding of g * W."""
+        for L in self.layers:
+            for norm, proj in self._folds():
+                g = L[norm].float()
+                L[proj].copy_((L[proj].float() * g[None, :]).to(L[proj].dtype))
+                L[norm].fill_(1)
+        self.unit_norms = all(bool((L[k] == 1).all()) for L in self.layers for k in ("in_norm", "post_norm"))
+        return self
+
+    def _folds(self):
+        return (("in_norm", "qkv"), ("post_norm", "gate_up"))
 
     def _shard_mlp(self, L, F):
         r, I = self.ps.tp_rank, self.inter
@@ -175,11 +196,20 @@ class LlamaModel:
         tp.all_reduce(h)
         residual = h
         x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
+        chain = tp.size == 1 and self._chain_ok(ids.shape[0])
+        ss = None  # norm chain: x is None and ss holds the residual's row partials
         for i, L in enumerate(self.layers):
-            q = ops.qkv_rope_cache(x, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i],
-                                   self.n_q)
+            if ss is None:
+                q = ops.qkv_rope_cache(x, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i],
+                                       self.n_q)
+            else:
+                q = ops.qkv_rope_cache_rs(residual, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i],
+                                          kv.v[i], self.n_q, ss, eps)
             a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
+            if chain:
+                x, ss = self._chain_layer(i, a.view(a.shape[0], -1), residual, i + 1 == len(self.layers), eps)
+                continue
             if tp.size == 1:
                 x = self.attn_out_mlp(i, a.view(a.shape[0], -1), residual, nxt, eps)
                 continue
@@ -190,6 +220,31 @@ class LlamaModel:
             tp.all_reduce(m)
             x = ops.add_rmsnorm(m, residual, nxt, eps)
         return x
+
+    # --------------------------------------------------------- norm chain --
+    def _chain_ok(self, M: int) -> bool:
+        """Large-M TP=1 layers without add + RMSNorm passes: every GEMM of the chain on the
+        four-wave kernel (ops.norm_chain_ok) and unit norm weights (folded into qkv / gate_up)."""
+        if not self.unit_norms or M < 2 or len(self.layers) < 1:
+            return False
+        cfg, H = self.cfg, self.cfg.hidden_size
+        return ops.norm_chain_ok(M, H, ((self.layers[0]["qkv"].shape[0], H), (H, self.n_q * cfg.head_dim),
+                                        (2 * self.inter, H), (H, self.inter)))
+
+    def _chain_layer(self, i, a, residual, last, eps):
+        """O (+= residual, row partials), gate_up + SiLU on the row-scaled residual, down (+=
+        residual, row partials; the last layer's down does the final add + RMSNorm instead).
+        Returns (x, ss): x normalised hidden states (last layer) or None with the partials."""
+        L = self.layers[i]
+        M, H = residual.shape
+        ss_post = ops.ss_buffer(M, H, residual.device)
+        ops.gemm_res_ss(a, L["o"], residual, ss_post)
+        act = ops.gemm_rs(residual, L["gate_up"], ss_post, eps, ops.EPI_SILU_MUL)
+        if last:
+            return ops.gemm_add_rmsnorm(act, L["down"], residual, self.final_norm, eps), None
+        ss = ops.ss_buffer(M, H, residual.device)
+        ops.gemm_res_ss(act, L["down"], residual, ss)
+        return None, ss
 
     def logits_local(self, hidden: torch.Tensor) -> torch.Tensor:
         """[n, H] -> this rank's vocab shard of the logits [n, V/TP] (model dtype)."""

@@ -38,6 +38,12 @@ class MixtralModel(LlamaModel):
         L["w13"].copy_(F["w13"][e0:e0 + n].to(self.device, self.dtype))
         L["w2"].copy_(F["w2"][e0:e0 + n].to(self.device, self.dtype))
 
+    def _folds(self):
+        return (("in_norm", "qkv"),)  # post_norm feeds the router and the experts
+
+    def _chain_ok(self, M: int) -> bool:
+        return False  # the norm chain is the dense MLP's (gate_up / down on the four-wave kernel)
+
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         from ..parallel.moe import moe_forward
 

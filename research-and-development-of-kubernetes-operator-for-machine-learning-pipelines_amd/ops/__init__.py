@@ -458,6 +458,96 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
     return unfused()
 
 
+# ---- norm chain (large-M TP=1 decoder): the add + RMSNorm passes folded into the GEMMs ----
+# O / down run C = residual += x @ w^T and leave the new residual's per-row sums of squares in
+# an ss buffer (ss_buffer: [M, N / 128] partials, one per 128 columns, written not accumulated,
+# then the [M] row totals, summed in a fixed order by the last tile of each row band:
+# deterministic); gate_up / QKV read the un-normalised residual and scale each accumulator row
+# by rsqrt(total / K + eps) =
+# RMSNorm after the GEMM, with the norm weight folded into their weights (LlamaModel.fold_norms).
+# "1" (default): on where every GEMM of the chain runs on the four-wave kernel; "0" off;
+# "force": also on CPU / any shape through the torch reference below (plumbing tests).
+NORM_CHAIN = os.environ.get("MLOP_NORM_CHAIN", "1")
+
+
+def norm_chain_ok(M: int, H: int, shapes) -> bool:
+    """True when the chain can run at M rows: hidden size H (ss groups of 128 columns, 16 per
+    quad of lanes) and every (N, K) GEMM of the chain on the four-wave kernel."""
+    if NORM_CHAIN == "force":
+        return H % 128 == 0
+    if NORM_CHAIN == "0" or GEMM_BACKEND != "mlop" or H % 256:
+        return False
+    _need_gpu()
+    return all(bool(torch.ops.mlop.w4_chain_ok(M, N, K)) for N, K in shapes)
+
+
+def ss_buffer(M: int, H: int, device) -> torch.Tensor:
+    """fp32 [M * (H / 128 + 1)]: the [M, H / 128] partials, then the [M] row totals."""
+    return torch.empty(M * (H // 128 + 1), dtype=torch.float32, device=device)
+
+
+def ss_parts(ss: torch.Tensor, M: int, H: int):
+    """(partials [M, H / 128], totals [M]) views of an ss_buffer."""
+    G = H // 128
+    return ss[:M * G].view(M, G), ss[M * G:M * (G + 1)]
+
+
+def _rinv_ref(ss: torch.Tensor, M: int, K: int, eps: float) -> torch.Tensor:
+    return torch.rsqrt(ss_parts(ss, M, K)[1].view(M, 1) / K + eps)
+
+
+def gemm_res_ss(x, w, residual, ss_out):
+    """residual [M, N] += x @ w^T in place (bf16); ss_out (ss_buffer(M, N)) <- the new residual
+    rows' partial sums of squares and totals.  The four-wave kernel's W4_ADD_SS epilogue on GPU."""
+    if x.is_cuda and NORM_CHAIN != "force":
+        _need_gpu()
+        _sk_reserve(x.device)
+        if not torch.ops.mlop.gemm_res_ss(residual, x, w, ss_out):
+            raise RuntimeError("norm chain: shape not on the four-wave kernel")
+        _GEMM_USED[(_mbucket(x.shape[0]), w.shape[0], w.shape[1], EPI_ADD_SS)] = "mlop"
+        return residual
+    residual.copy_((residual.float() + x.float() @ w.float().t()).to(residual.dtype))
+    M, N = residual.shape
+    part, tot = ss_parts(ss_out, M, N)
+    part.copy_(residual.float().pow(2).view(M, N // 128, 128).sum(-1))
+    tot.copy_(part.sum(-1))
+    return residual
+
+
+def gemm_rs(x, w, ss, eps: float, epi: int = EPI_NONE):
+    """epi(rmsnorm_unit(x) @ w^T) with the row factors from ss (gemm_res_ss's partials): the
+    normalisation is applied to the accumulators (W4_RS), x is the raw residual."""
+    M, K = x.shape
+    N = w.shape[0]
+    if x.is_cuda and NORM_CHAIN != "force":
+        _need_gpu()
+        _sk_reserve(x.device)
+        out = torch.empty(M, N if epi == EPI_NONE else N // 2, dtype=x.dtype, device=x.device)
+        if not torch.ops.mlop.gemm_rs(out, x, w, ss, eps, epi):
+            raise RuntimeError("norm chain: shape not on the four-wave kernel")
+        _GEMM_USED[(_mbucket(M), N, K, epi | EPI_RS)] = "mlop"
+        return out
+    return gemm((x.float() * _rinv_ref(ss, M, K, eps)).to(x.dtype), w, epi=epi)
+
+
+def qkv_rope_cache_rs(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads: int, ss, eps: float):
+    """qkv_rope_cache of rmsnorm_unit(x) with the row factors from ss (norm chain)."""
+    M, K = x.shape
+    if x.is_cuda and NORM_CHAIN != "force":
+        _need_gpu()
+        _sk_reserve(x.device)
+        q_out = torch.empty(M, n_q_heads, k_cache.shape[3], dtype=x.dtype, device=x.device)
+        if not torch.ops.mlop.gemm_rs_rope(q_out, k_cache, v_cache, x, w, positions, cos_sin, slots, ss, eps):
+            raise RuntimeError("norm chain: shape not on the four-wave kernel")
+        _GEMM_USED[(_mbucket(M), w.shape[0], K, EPI_ROPE | EPI_RS)] = "mlop"
+        return q_out
+    return rope_cache(gemm((x.float() * _rinv_ref(ss, M, K, eps)).to(x.dtype), w), positions, cos_sin, slots, k_cache,
+                      v_cache, n_q_heads)
+
+
+EPI_ADD_SS, EPI_RS = 4, 8  # norm-chain epilogue flags (gemm_used() keys; gemm_w4.hip W4_ADD_SS / W4_RS)
+
+
 # Residual add + RMSNorm as the decode GEMV's prologue (gemv.hip NORM).  Measured a wash at
 # batch 1 (315-318 vs 318 tok/s unfused, scripts/history/run41.sh: the two norm launches it removes
 # cost what the heavier prologue adds to the two GEMVs) and a loss at batch 2-4, so it is

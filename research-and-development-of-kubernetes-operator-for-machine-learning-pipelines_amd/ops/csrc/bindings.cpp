@@ -297,6 +297,91 @@ bool gemm_rope_supported(int64_t M, int64_t N, int64_t K) {
   return mlop::gemm_rope_supported((int)M, (int)N, (int)K);
 }
 
+// ---- norm chain on the four-wave GEMM (large-M TP=1 decoder, unit norm weights) ----
+// residual [M, N] += a . w^T in place; ss (f32, M * (N / 128 + 1)) = [M, N / 128] per-row,
+// per-128-column partial sums of squares of the new residual, then the [M] row totals; false =
+// the shape does not run on the four-wave kernel
+bool w4_chain_ok_op(int64_t M, int64_t N, int64_t K) { return mlop::w4_chain_ok((int)M, (int)N, (int)K); }
+
+static void check_ss(const Tensor& ss, int64_t M, int64_t H, const char* name) {
+  TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.is_contiguous() &&
+                  ss.numel() == M * (H / 128 + 1), name, " must be f32 [M * (H / 128 + 1)] contiguous");
+}
+
+bool gemm_res_ss(Tensor residual, Tensor a, Tensor w, Tensor ss_out) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(residual, "residual");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "w [N, K]");
+  TORCH_CHECK(residual.dim() == 2 && residual.size(0) == M && residual.size(1) == N && residual.stride(1) == 1 &&
+                  residual.stride(0) % 8 == 0, "residual [M, N]");
+  TORCH_CHECK(N % 128 == 0, "N % 128");
+  check_ss(ss_out, M, N, "ss");
+  mlop::RopeEpi re{};
+  re.ss_out = ss_out.data_ptr<float>();
+  re.ss_tot = re.ss_out + M * (N / 128);
+  c10::DeviceGuard g(a.device());
+  return mlop::launch_w4_chain(4, a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(),
+                               (int)residual.stride(0), (int)M, (int)N, (int)K, re, cur_stream());
+}
+
+// out = epi(diag(rsqrt(ss / K + eps)) . a . w^T): a is the un-normalised residual, ss_in its
+// partial sums of squares (gemm_res_ss), w the consumer weight with the norm weight folded in
+bool gemm_rs(Tensor out, Tensor a, Tensor w, Tensor ss_in, double eps, int64_t epi) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(out, "out");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "w [N, K]");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == (epi == 0 ? N : N / 2) && out.stride(1) == 1 &&
+                  out.stride(0) % 8 == 0, "out [M, N or N/2]");
+  TORCH_CHECK(K % 128 == 0, "K % 128");
+  check_ss(ss_in, M, K, "ss");
+  mlop::RopeEpi re{};
+  re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
+  re.ss_inv_k = 1.f / (float)K;
+  re.ss_eps = (float)eps;
+  c10::DeviceGuard g(a.device());
+  return mlop::launch_w4_chain((int)epi | 8, a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(),
+                               (int)out.stride(0), (int)M, (int)N, (int)K, re, cur_stream());
+}
+
+// QKV projection of the norm chain: rows scaled as gemm_rs, then RoPE + paged K / staged V
+bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor w, Tensor pos, Tensor cos_sin,
+                  Tensor slots, Tensor ss_in, double eps) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(q_out, "q_out"); check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache"); check_i32(pos, "pos"); check_i32(slots, "slots");
+  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous(), "cos_sin f32");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && K % 64 == 0, "w [N, K], K % 64");
+  TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "ranks");
+  const int64_t Hq = q_out.size(1), D = q_out.size(2), Hkv = k_cache.size(1), BS = k_cache.size(2);
+  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
+                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
+              "head_dim 128; k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D && q_out.size(0) == M, "qkv width / q_out rows");
+  TORCH_CHECK(pos.numel() == M && slots.numel() == M, "pos/slots length");
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin [max_pos, D]");
+  TORCH_CHECK(K % 128 == 0, "K % 128");
+  check_ss(ss_in, M, K, "ss");
+  if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
+  mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
+                   (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                   slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
+  at::Tensor vtmp = at::empty({M, Hkv, D}, a.options());  // token-major V, paged by launch_v_scatter
+  re.v_tmp = (uint16_t*)vtmp.data_ptr();
+  re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
+  re.ss_inv_k = 1.f / (float)K;
+  re.ss_eps = (float)eps;
+  c10::DeviceGuard g(a.device());
+  return mlop::launch_w4_chain(3 | 8, a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N,
+                               (int)K, re, cur_stream());
+}
+
 // out = rmsnorm(residual += a . w^T) * norm_w through the split-K path; false = not taken
 bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor norm_w, Tensor ws,
                       double eps) {
@@ -570,6 +655,11 @@ TORCH_LIBRARY(mlop, m) {
   m.def("vmm_chunks_ready(Tensor flat) -> int", &vmm_chunks_ready);
   m.def("vmm_error(Tensor flat) -> int", &vmm_error);
   m.def("gemm_rope_supported(int M, int N, int K) -> bool", &gemm_rope_supported);
+  m.def("w4_chain_ok(int M, int N, int K) -> bool", &w4_chain_ok_op);
+  m.def("gemm_res_ss(Tensor(a!) residual, Tensor a, Tensor w, Tensor(b!) ss_out) -> bool");
+  m.def("gemm_rs(Tensor(a!) out, Tensor a, Tensor w, Tensor ss_in, float eps, int epi) -> bool");
+  m.def("gemm_rs_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
+        "Tensor pos, Tensor cos_sin, Tensor slots, Tensor ss_in, float eps) -> bool");
   m.def("gemm_rope_stages_v(int M, int N, int K) -> bool", &gemm_rope_stages_v_op);
   m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");
@@ -621,6 +711,9 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);
+  m.impl("gemm_res_ss", &gemm_res_ss);
+  m.impl("gemm_rs", &gemm_rs);
+  m.impl("gemm_rs_rope", &gemm_rs_rope);
   m.impl("gemm_rope_cache", &gemm_rope_cache);
   m.impl("gemm_norm", &gemm_norm);
   m.impl("gemm_norm_rope", &gemm_norm_rope);

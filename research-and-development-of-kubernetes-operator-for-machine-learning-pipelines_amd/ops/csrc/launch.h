@@ -45,6 +45,17 @@ struct RopeEpi {
   // writes it with 16-B stores and launch_v_scatter moves it into the dim-major pages over
   // the whole chip (nullptr: the epilogue scatters V itself)
   uint16_t* v_tmp = nullptr;
+  // four-wave norm chain (run_w4 only; the large-M TP=1 decoder with unit norm weights, see
+  // launch_w4_chain).  Producer (C += A.B^T): ss_out = [M, N / 128] partial sums of squares of
+  // the updated residual rows (one per row and wave column block), then ss_tot [M] = their row
+  // sums, added in a fixed order by the last tile of each 256-row band (ss_cnt: one ticket per
+  // band).  Consumer: ss_in = a producer's ss_tot; the accumulators of row r are scaled by
+  // rsqrt(ss_in[r] * ss_inv_k + ss_eps) = RMSNorm applied after the GEMM.
+  const float* ss_in = nullptr;
+  float* ss_out = nullptr;
+  float* ss_tot = nullptr;
+  int* ss_cnt = nullptr;
+  float ss_inv_k = 0.f, ss_eps = 0.f;
 };
 // V rows staged token-major -> dim-major paged cache ([NB, Hkv, 128, BS]); slot < 0 skipped
 void launch_v_scatter(const uint16_t* v_tmp, uint16_t* v_cache, const int* slots, int M, int Hkv, int BS,
@@ -66,6 +77,11 @@ bool gemm_sk_scratch(float** ws, int** cnt, int* cus);
 bool gemm_sk_available(int* cus);
 void run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
             int K, hipStream_t st, const RopeEpi& re);
+// norm chain on the four-wave kernel (epi flags: 4 = C += A.B^T with ss partials, 8 = rows scaled
+// by re.ss_in; 4, 0|8, 1|8, 3|8 are built): true when every such GEMM of this shape runs there
+bool w4_chain_ok(int M, int N, int K);
+bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K,
+                     const RopeEpi& re, hipStream_t st);
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)
 int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fitted BM x BN
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the

@@ -1,0 +1,4 @@
+#!/bin/bash
+source scripts/gpu_check.sh
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+step bench_chain 300 python -u scripts/bench_chain.py

@@ -1,0 +1,131 @@
+"""Norm chain on the four-wave GEMM (gemm_w4.hip W4_ADD_SS / W4_RS) vs the fp32 PyTorch
+oracle at the Llama-3-8B shapes: O / down add into the residual in place and write per-row,
+per-128-column sums of squares; gate_up (SiLU-mul) and QKV (RoPE + paged cache) read the raw
+residual and scale each accumulator row by rsqrt(sum / K + eps).  Also: bit-identical
+relaunches (partials are written, never accumulated) and a 2-layer 8B forward with the chain
+on vs off."""
+import pytest
+import torch
+
+from mlopamd import ops
+from mlopamd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+bf = torch.bfloat16
+H, I, EPS = 4096, 14336, 1e-5
+
+
+def close(a, b, atol=2e-2, rtol=2e-2):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+@pytest.fixture
+def w4(gpu):
+    prev = torch.ops.mlop.gemm_big_variant(-1)
+    torch.ops.mlop.gemm_big_variant(5)
+    ops.GEMM_BACKEND = "mlop"
+    ops._sk_reserve(torch.device(gpu))
+    try:
+        yield
+    finally:
+        torch.ops.mlop.gemm_big_variant(prev)
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
+
+
+def _unit_norm(r):
+    rf = r.float()
+    return rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + EPS)
+
+
+@pytest.mark.parametrize("M,K", [(4088, H), (2048, H), (4088, I), (2040, I)])
+def test_gemm_res_ss(gpu, w4, M, K):
+    torch.manual_seed(M + K)
+    assert torch.ops.mlop.w4_chain_ok(M, H, K)
+    a = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(H, K, device=gpu)).to(bf)
+    res = torch.randn(M, H, device=gpu, dtype=bf)
+    exp = res.float() + a.float() @ w.float().t()
+    r = res.clone()
+    ss = ops.ss_buffer(M, H, gpu).fill_(float("nan"))
+    ops.gemm_res_ss(a, w, r, ss)
+    close(r, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=2e-2)
+    # the partials are the sums of squares of the STORED (bf16) residual, group by group, and
+    # the totals their row sums (the band's last tile)
+    part, tot = ops.ss_parts(ss, M, H)
+    close(part, r.float().pow(2).view(M, H // 128, 128).sum(-1), atol=1e-3, rtol=1e-4)
+    close(tot, r.float().pow(2).sum(-1), atol=1e-2, rtol=1e-4)
+    r2, ss2 = res.clone(), torch.empty_like(ss)
+    ops.gemm_res_ss(a, w, r2, ss2)
+    assert torch.equal(r, r2) and torch.equal(ss, ss2)  # deterministic
+
+
+@pytest.mark.parametrize("M", [4088, 2048])
+def test_gemm_rs_silu(gpu, w4, M):
+    torch.manual_seed(M)
+    x = (3 * torch.randn(M, H, device=gpu)).to(bf)
+    w = (0.02 * torch.randn(2 * I, H, device=gpu)).to(bf)
+    ss = ops.ss_buffer(M, H, gpu).fill_(float("nan"))
+    ops.ss_parts(ss, M, H)[1].copy_(x.float().pow(2).sum(-1))
+    y = ops.gemm_rs(x, w, ss, EPS, ops.EPI_SILU_MUL)
+    exp = ref.silu_mul(ops.deinterleave_cols((_unit_norm(x) @ w.float().t()).to(bf)))
+    close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [4088, 2048])
+def test_gemm_rs_rope(gpu, w4, M):
+    from mlopamd.models.layers import rope_table
+
+    Hq, Hkv, D, BS = 32, 8, 128, 16
+    N = (Hq + 2 * Hkv) * D
+    NB = M // BS + 8
+    torch.manual_seed(M)
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    x = (3 * torch.randn(M, H, device=gpu)).to(bf)
+    w = (0.02 * torch.randn(N, H, device=gpu)).to(bf)
+    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
+    slots[7] = -1
+    ss = ops.ss_buffer(M, H, gpu).fill_(float("nan"))
+    ops.ss_parts(ss, M, H)[1].copy_(x.float().pow(2).sum(-1))
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    q = ops.qkv_rope_cache_rs(x, w, pos, cs, slots, kc, vc, Hq, ss, EPS)
+    qkv_ref = (_unit_norm(x) @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref)
+    close(kc, kr)
+    close(vc, vr)
+
+
+def test_llama_forward_chain_on_off(gpu, w4, monkeypatch):
+    """2-layer Llama-3-8B-wide forward over a 2048-token prefill batch: the chain (no add +
+    RMSNorm launches between the projections) and the unfused layers agree to bf16 noise."""
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.models.reference import dense_logits
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    cfg = get_config("llama3-8b", num_layers=2)
+    model = build_model(cfg, device=gpu, seed=5)
+    assert model._chain_ok(2048)
+    prompts = [torch.randint(1000, 100000, (256,)).tolist() for _ in range(8)]
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(ops, "NORM_CHAIN", mode)
+        eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=2048, max_model_len=512,
+                                         num_kv_blocks=8 * 32 + 1, use_graphs=False))
+        ops._GEMM_USED.clear()
+        outs[mode] = eng.generate(prompts, SamplingParams(max_tokens=2, ignore_eos=True))
+        used = set(k[3] for k in ops._GEMM_USED)
+        assert (ops.EPI_ADD_SS in used) == (mode == "1"), used
+    # both against the fp32 dense oracle (first token: the 2048-row chain step; second: decode)
+    for mode in ("0", "1"):
+        for p, o in zip(prompts[:4], outs[mode][:4]):
+            toks = list(p)
+            for t in o:
+                lg = dense_logits(model, toks)[-1]
+                best = int(lg.argmax())
+                assert t == best or float(lg[best] - lg[t]) < 0.1 * float(lg.std()), (mode, len(toks), best, t)
+                toks.append(t)
