@@ -1121,6 +1121,8 @@ class Engine:
 
         if dist.is_initialized():
             dist.barrier()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)  # the barrier's own collective, on both sides
 
     def shutdown(self):
         if self.step_sync is not None and self.step_sync.is_leader:
