@@ -252,9 +252,11 @@ def render() -> str:
     out = ["// GENERATED by mlopamd/ops/gen_gemm_w4.py -- do not edit by hand.",
            "// The K-loop of gemm_w4_kernel (csrc/gemm_w4.hip): see the generator's docstring.",
            "#pragma once", ""]
-    # one K-loop per epilogue store count: plain and RoPE (32 x 16-B stores per wave), SiLU-mul (16)
+    # one K-loop per count of VMEM ops issued after the prefetched K-tiles: plain and RoPE (32 x
+    # 16-B stores per wave), SiLU-mul (16), and +2 for the row-scaled variants (W4_RS: two LDS-DMA
+    # loads of the row sums of squares issued just before the K-loop)
     for si, sc in enumerate(SCHEDS):
-        for ns in (32, 16):
+        for ns in (32, 16, 34, 18):
             out.append(f"#define MLOP_W4_KLOOP_S{ns}_P{si}_ASM \\")
             for ln in kloop(ns, sc):
                 out.append(f'  "{ln}\\n" \\')

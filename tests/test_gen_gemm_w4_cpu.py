@@ -13,7 +13,7 @@ def test_header_matches_generator():
 
 def test_loop_invariants():
     for sc in gen.SCHEDS:
-        for ns in (32, 16):
+        for ns in (32, 16, 34, 18):
             lines = gen.kloop(ns, sc)
             text = "\n".join(lines)
             # 128 MFMAs per K-tile body: first + steady + nodma + last = 4 bodies
