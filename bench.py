@@ -37,7 +37,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node to use; > 1 without a torch.distributed launcher (no WORLD_SIZE in "
+                         "the env): this process becomes the launcher of N rank processes, one per GPU, "
+                         "before it makes any HIP call")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--model", default="llama3-8b")
@@ -80,17 +83,115 @@ def parse(argv=None):
                          "(a fresh predictor process: CR->ready includes its start-up) + V2 HTTP + Router "
                          "(runtime/http_bench.py); the value is the served rate over the predictor's own "
                          "engine steps")
+    ap.add_argument("--cr-ready-samples", type=int, default=1,
+                    help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
+                         "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
+                         "their median is p50_cr_ready_s.  0: report the in-process deploy time instead")
     return ap.parse_args(argv)
 
 
+def _gpu_count() -> int:
+    """Visible GPUs WITHOUT initialising HIP (``device_count`` does not on this image): the
+    launcher parent must never touch the GPU before its rank children exist."""
+    try:
+        return torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def _process_ready(a, device_index: int | None) -> dict:
+    """p50 CR->ready over ``--cr-ready-samples`` fresh predictor processes (runtime/http_bench.py),
+    on one GPU, before this process touches HIP.  CPU: a float32 predictor without graphs."""
+    import asyncio
+
+    from mlopamd.runtime import http_bench
+
+    env = {"MLOP_ENGINE_MAX_NUM_BATCHED_TOKENS": str(a.max_batched_tokens),
+           "MLOP_ENGINE_MAX_MODEL_LEN": str(a.max_model_len)}
+    if device_index is None:
+        env.update({"MLOP_DEVICE": "cpu", "MLOP_DTYPE": "float32", "MLOP_ENGINE_USE_GRAPHS": "false",
+                    "MLOP_ENGINE_NUM_KV_BLOCKS": "64", "OMP_NUM_THREADS": "2"})
+    t0 = time.perf_counter()
+    r = asyncio.run(http_bench.cr_ready_process(a.model, a.batch, env, samples=a.cr_ready_samples,
+                                                gpus=[device_index] if device_index is not None else 8))
+    r["probe_wall_s"] = round(time.perf_counter() - t0, 2)
+    return r
+
+
+def launch(a, argv) -> int:
+    """``--gpus N`` with no launcher around us: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their env, LOCAL_RANK = the GPU index), wait for them, and exit
+    with the first failing rank's status (the others are terminated).  Rank 0 prints the ONE
+    JSON line.  Same pattern as the predictor's own ``--tp N`` (runtime/server.py launch_ranks)."""
+    import signal
+    import socket
+    import subprocess
+
+    n = a.gpus
+    ngpu = _gpu_count()
+    if ngpu and ngpu < n:
+        raise SystemExit(f"--gpus {n}: only {ngpu} GPUs visible")
+    extra = {}
+    if a.cr_ready_samples > 0 and not a.no_operator:
+        extra["MLOP_BENCH_PROCESS_READY"] = json.dumps(_process_ready(a, 0 if ngpu else None))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   MLOP_BENCH_LAUNCHER="1", **extra)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                break
+            time.sleep(0.2)
+        else:
+            rc = next((p.returncode for p in procs if p.returncode), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+    return rc
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
     if a.http:
         return http_main(a)
     from mlopamd.parallel.comm import env_rank_info, init_distributed
     import torch.distributed as dist
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch(a, argv))
     rank, local_rank, world = env_rank_info()
+    if world != a.gpus:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE {world}: reporting the {world} ranks that ran",
+              file=sys.stderr, flush=True)
+    proc_ready = None
+    if rank == 0 and a.cr_ready_samples > 0 and not a.no_operator:
+        if os.environ.get("MLOP_BENCH_PROCESS_READY"):  # measured by our launcher parent
+            proc_ready = json.loads(os.environ["MLOP_BENCH_PROCESS_READY"])
+        else:  # before this process makes its first HIP call (the probe's predictor uses this GPU)
+            proc_ready = _process_ready(a, local_rank if _gpu_count() else None)
     if world > 1:
         init_distributed()
     dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
@@ -126,7 +227,7 @@ def main(argv=None):
         deploy_info[k] = engine.stats.get(k, 0)
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()
-        _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine)
+        _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine, None)
         return
     from mlopamd.runtime.sampler import SamplingParams
 
@@ -188,7 +289,7 @@ def main(argv=None):
     stats = {k: engine.stats[k] - s0.get(k, 0) for k in engine.stats}
     if a.tp > 1:
         engine.shutdown()  # release the TP workers before the result gather
-    _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine)
+    _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine, proc_ready)
 
 
 def http_main(a):
@@ -208,7 +309,7 @@ def http_main(a):
     return res
 
 
-def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine):
+def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine, proc_ready=None):
     import torch.distributed as dist
 
     tot = torch.tensor([float(gen), elapsed, ready_s, float(stats.get("prefill_tokens", 0))], dtype=torch.float64)
@@ -247,8 +348,20 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
                        "async_scheduling": not a.no_async,
                        "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap,
                        "shared_prefix": a.shared_prefix, "prefix_cache": not a.no_prefix_cache},
-            "p50_cr_ready_s": round(p50_ready, 3),
+            # CR -> ready with the predictor as a fresh OS process when measured (the honest
+            # figure: process start + imports + HIP init inside); the in-process deploy time
+            # (operator -> predictor built inside this already-running process) beside it
+            "p50_cr_ready_s": (proc_ready["p50_cr_ready_process_s"] if proc_ready else round(p50_ready, 3)),
+            "cr_ready_path": "fresh predictor process" if proc_ready else "in-process",
+            "p50_cr_ready_in_process_s": round(p50_ready, 3),
+            "cr_ready_process": proc_ready,
             "served_tokens_per_sec_per_gpu": round(value / world, 2),
+            "per_rank_tokens_per_sec": [round(float(g[0]) / float(g[1]), 2) if float(g[1]) > 0 else 0.0
+                                        for g in gathered],
+            "dist": {"world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
+                     "launcher": "bench.py" if os.environ.get("MLOP_BENCH_LAUNCHER") else
+                     ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else
+                      ("external" if world > 1 else "none"))},
             "prefill_tokens_per_sec": round(total_prefill / max_t, 2),
             "step_mix": stats,
             "deploy": deploy_info,

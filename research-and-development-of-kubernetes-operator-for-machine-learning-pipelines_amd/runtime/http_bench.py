@@ -24,6 +24,8 @@ import time
 
 import numpy as np
 
+_NS, _NAME = "serving", "llm"
+
 
 async def _scrape(session, url) -> dict:
     async with session.get(url) as r:
@@ -36,51 +38,95 @@ async def _scrape(session, url) -> dict:
     return out
 
 
+async def _start_stack(model: str, batch: int, engine_env: dict | None, ready_timeout_s: float, gpus=None):
+    """registry + operator + the local Seldon stand-in with a ProcessLauncher (fresh predictor
+    processes) + the weighted Router.  ``gpus``: device indices the launcher may hand out
+    (default: every visible GPU)."""
+    from ..controller.app import make_operator
+    from ..controller.clock import RealClock
+    from ..controller.crd import OperatorSettings
+    from ..controller.kube import FakeKube
+    from ..controller.local import FakeSeldonController, GpuPool, ProcessLauncher, Router
+    from ..controller.mlflow import LocalMlflowClient, SqliteRegistry
+    from ..controller.prometheus import LocalProm, MetricStore
+
+    kube, reg = FakeKube(), SqliteRegistry()
+    reg.create_model_version(_NAME, f"mlflow-artifacts:/1/{model}/artifacts/model",
+                             tags={"mlop.architecture": model, "mlop.runtime": "mlop-llm"})
+    reg.set_alias(_NAME, "champion", 1)
+    op, _ = make_operator(kube, LocalMlflowClient(reg), LocalProm(MetricStore()), RealClock(), OperatorSettings())
+    env = {"MLOP_ENGINE_MAX_NUM_SEQS": str(batch), "MLOP_KERNEL_SAMPLE_S": "0"}
+    env.update(engine_env or {})
+    pool = GpuPool(gpus) if gpus is not None else GpuPool.detect()
+    launcher = ProcessLauncher(extra_env=env, gpus=pool if pool.devices else None, ready_timeout_s=ready_timeout_s)
+    ctl = FakeSeldonController(kube, launcher, RealClock()).start()
+    await op.start()
+    return kube, op, ctl, Router(ctl)
+
+
+async def _create_and_wait_ready(kube, ctl, batch: int, ready_timeout_s: float) -> dict:
+    """MlflowModel CR -> ... -> the predictor process answers /v2/health/ready and the CR
+    reports ready; the clock runs from the CR create."""
+    from ..controller.crd import GROUP, PLURAL, VERSION
+    from ..controller.local import mlflow_model_cr, wait_for
+
+    t0 = time.perf_counter()
+    await kube.create(GROUP, VERSION, _NS, PLURAL, mlflow_model_cr(_NAME, _NS, _NAME, "champion",
+                                                                   maxNumSeqs=batch, maxModelLen=1024))
+
+    async def ready():
+        o = await kube.get(GROUP, VERSION, _NS, PLURAL, _NAME)
+        for p in ctl.pods.values():  # a predictor that cannot start fails the run now
+            if "error" in p.extra:
+                raise RuntimeError(f"predictor {p.predictor} failed to start: {p.extra['error']}")
+        return (o.get("status") or {}).get("ready") == "True"
+
+    await wait_for(ready, ready_timeout_s, poll_s=0.05)
+    cr_ready = time.perf_counter() - t0
+    pod = next(iter(ctl.pods.values()))
+    return {"cr_ready_process_s": round(cr_ready, 3), "predictor_process_ready_s": round(pod.extra.get("ready_s", 0.0), 3),
+            "predictor_gpus": pod.extra.get("gpus"), "pod": pod}
+
+
+async def cr_ready_process(model: str = "llama3-8b", batch: int = 2048, engine_env: dict | None = None,
+                           samples: int = 1, gpus=None, ready_timeout_s: float = 900.0) -> dict:
+    """CR -> ready with the predictor as a FRESH OS process (process start, imports, HIP init,
+    weights, KV pool, graph capture all inside), ``samples`` times on a fresh stack each; the
+    predictor is torn down again.  The default ``bench.py`` line reports its median as
+    ``p50_cr_ready_s``."""
+    vals, last = [], {}
+    for _ in range(max(1, samples)):
+        kube, op, ctl, _router = await _start_stack(model, batch, engine_env, ready_timeout_s, gpus)
+        try:
+            last = await _create_and_wait_ready(kube, ctl, batch, ready_timeout_s)
+            vals.append(last["cr_ready_process_s"])
+        finally:
+            await ctl.stop()
+            await op.stop()
+    vals.sort()
+    n = len(vals)
+    p50 = vals[n // 2] if n % 2 else 0.5 * (vals[n // 2 - 1] + vals[n // 2])
+    return {"p50_cr_ready_process_s": round(p50, 3), "cr_ready_process_samples_s": vals,
+            "predictor_process_ready_s": last.get("predictor_process_ready_s"),
+            "predictor_gpus": last.get("predictor_gpus")}
+
+
 async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256, output_len: int = 256,
               steps: int = 20, warmup: int = 5, engine_env: dict | None = None, ready_timeout_s: float = 900.0,
               ramp_timeout_s: float = 600.0) -> dict:
     import aiohttp
 
-    from ..controller.app import make_operator
-    from ..controller.clock import RealClock
-    from ..controller.crd import GROUP, PLURAL, VERSION, OperatorSettings
-    from ..controller.kube import FakeKube
-    from ..controller.local import FakeSeldonController, GpuPool, ProcessLauncher, Router, mlflow_model_cr, wait_for
-    from ..controller.mlflow import LocalMlflowClient, SqliteRegistry
-    from ..controller.prometheus import LocalProm, MetricStore
     from ..models.config import get_config
 
-    ns, name = "serving", "llm"
-    kube, reg = FakeKube(), SqliteRegistry()
-    reg.create_model_version(name, f"mlflow-artifacts:/1/{model}/artifacts/model",
-                             tags={"mlop.architecture": model, "mlop.runtime": "mlop-llm"})
-    reg.set_alias(name, "champion", 1)
-    op, _ = make_operator(kube, LocalMlflowClient(reg), LocalProm(MetricStore()), RealClock(), OperatorSettings())
-    env = {"MLOP_ENGINE_MAX_NUM_SEQS": str(batch), "MLOP_KERNEL_SAMPLE_S": "0"}
-    env.update(engine_env or {})
-    pool = GpuPool.detect()
-    launcher = ProcessLauncher(extra_env=env, gpus=pool if pool.devices else None, ready_timeout_s=ready_timeout_s)
-    ctl = FakeSeldonController(kube, launcher, RealClock()).start()
-    router = Router(ctl)
-    await op.start()
+    ns, name = _NS, _NAME
+    kube, op, ctl, router = await _start_stack(model, batch, engine_env, ready_timeout_s)
     out: dict = {"mode": "http", "path": "operator + ProcessLauncher + V2 HTTP + Router"}
     try:
-        t0 = time.perf_counter()
-        await kube.create(GROUP, VERSION, ns, PLURAL, mlflow_model_cr(name, ns, name, "champion",
-                                                                      maxNumSeqs=batch, maxModelLen=1024))
-
-        async def ready():
-            o = await kube.get(GROUP, VERSION, ns, PLURAL, name)
-            for p in ctl.pods.values():  # a predictor that cannot start fails the run now
-                if "error" in p.extra:
-                    raise RuntimeError(f"predictor {p.predictor} failed to start: {p.extra['error']}")
-            return (o.get("status") or {}).get("ready") == "True"
-
-        await wait_for(ready, ready_timeout_s, poll_s=0.05)
-        out["p50_cr_ready_process_s"] = round(time.perf_counter() - t0, 3)
-        pod = next(iter(ctl.pods.values()))
-        out["predictor_process_ready_s"] = round(pod.extra.get("ready_s", 0.0), 3)
-        out["predictor_gpus"] = pod.extra.get("gpus")
+        r = await _create_and_wait_ready(kube, ctl, batch, ready_timeout_s)
+        pod = r.pop("pod")
+        out["p50_cr_ready_process_s"] = r["cr_ready_process_s"]
+        out["predictor_process_ready_s"] = r["predictor_process_ready_s"]
+        out["predictor_gpus"] = r["predictor_gpus"]
         metrics_url = pod.endpoint + "/metrics"
         V = get_config(model).vocab_size
         rng = np.random.default_rng(1234)

@@ -36,16 +36,41 @@ def test_bench_single_process_json():
     assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["value"] > 0
     assert d["config"]["parallelism"] == "dp1" and d["higher_is_better"] is True
     assert d["deploy"]["path"] == "operator" and d["p50_cr_ready_s"] > 0
+    # CR -> ready measured with the predictor as a fresh OS process
+    assert d["cr_ready_path"] == "fresh predictor process"
+    assert d["p50_cr_ready_s"] == d["cr_ready_process"]["p50_cr_ready_process_s"]
+    assert d["p50_cr_ready_s"] >= d["cr_ready_process"]["predictor_process_ready_s"] > 0
 
 
 def test_bench_two_ranks_gloo():
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-              os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS])
+              os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0", *ARGS])
+    assert d["dist"] == {"world_size": 2, "backend": "gloo", "launcher": "torch.distributed.run"}
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["global_batch"] == 16 and d["value"] > 0
     # whole-job aggregate over ranks = per-GPU value x N
     assert abs(d["served_tokens_per_sec_per_gpu"] * 2 - d["value"]) < 1e-3 * d["value"] + 0.02
+
+
+def test_bench_self_launches_n_ranks():
+    """``python bench.py --gpus 2`` with no torchrun around it (the driver's plain command):
+    bench.py launches the 2 rank processes itself, both replicas' tokens are counted, and
+    the line says which world actually ran."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["dist"] == {"world_size": 2, "backend": "gloo", "launcher": "bench.py"}
+    assert len(d["per_rank_tokens_per_sec"]) == 2 and min(d["per_rank_tokens_per_sec"]) > 0
+    assert d["cr_ready_path"] == "fresh predictor process"  # probed once by the launcher parent
+
+
+def test_bench_self_launches_tp_group():
+    """``bench.py --gpus 2 --tp 2``: one TP=2 replica over the 2 self-launched ranks."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--tp", "2",
+              "--cr-ready-samples", "0", *ARGS])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp1-tp2" and d["value"] > 0
+    assert d["config"]["global_batch"] == 8 and d["deploy"]["tp"] == 2
+    assert d["dist"]["world_size"] == 2 and d["dist"]["launcher"] == "bench.py"
 
 
 def test_deploy_fails_fast_when_predictor_cannot_start():
