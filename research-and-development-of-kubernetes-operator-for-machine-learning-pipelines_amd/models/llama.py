@@ -229,7 +229,7 @@ class LlamaModel:
             return False
         cfg, H = self.cfg, self.cfg.hidden_size
         return ops.norm_chain_ok(M, H, ((self.layers[0]["qkv"].shape[0], H), (H, self.n_q * cfg.head_dim),
-                                        (2 * self.inter, H), (H, self.inter)))
+                                        (2 * self.inter, H), (H, self.inter)), device=self.device)
 
     def _chain_layer(self, i, a, residual, last, eps):
         """O (+= residual, row partials), gate_up + SiLU on the row-scaled residual, down (+=

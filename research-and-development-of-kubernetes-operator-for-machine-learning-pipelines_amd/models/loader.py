@@ -187,6 +187,11 @@ def load_pretrained(path: str | os.PathLike, device="cuda", dtype=torch.bfloat16
     model = build_model(cfg, device=device, dtype=dtype, pstate=pstate)
     with torch.no_grad():
         model.load_shard_from(HFWeights(path, cfg))
+    # checkpoints carry trained (non-unit) RMSNorm weights: fold them into the projections that
+    # consume them so the large-M forward can run the norm chain (LlamaModel._chain_ok needs unit
+    # norms).  The same function up to the bf16 rounding of g * W; MLOP_FOLD_NORMS=0 keeps them.
+    if os.environ.get("MLOP_FOLD_NORMS", "1") != "0":
+        model.fold_norms()
     return model
 
 

@@ -470,14 +470,19 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
 NORM_CHAIN = os.environ.get("MLOP_NORM_CHAIN", "1")
 
 
-def norm_chain_ok(M: int, H: int, shapes) -> bool:
+def norm_chain_ok(M: int, H: int, shapes, device=None) -> bool:
     """True when the chain can run at M rows: hidden size H (ss groups of 128 columns, 16 per
-    quad of lanes) and every (N, K) GEMM of the chain on the four-wave kernel."""
+    quad of lanes) and every (N, K) GEMM of the chain on the four-wave kernel, with the band
+    tickets' scratch reserved on ``device`` and one ticket per 256-row band (w4_chain_ok checks
+    everything launch_w4_chain does, so the chain is decided once per forward and never refused
+    after a residual was updated in place)."""
     if NORM_CHAIN == "force":
         return H % 128 == 0
     if NORM_CHAIN == "0" or GEMM_BACKEND != "mlop" or H % 256:
         return False
     _need_gpu()
+    if device is not None and torch.device(device).type == "cuda":
+        _sk_reserve(torch.device(device))
     return all(bool(torch.ops.mlop.w4_chain_ok(M, N, K)) for N, K in shapes)
 
 
@@ -684,14 +689,22 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def sample(logits, temps, top_ks, top_ps, uniform) -> torch.Tensor:
+SAMPLE_MAX_CAND = 1024  # sampling.hip kMaxCand: top_k above this (or 0) draws from the whole row
+
+
+def sample(logits, temps, top_ks, top_ps, uniform, full: bool | None = None) -> torch.Tensor:
+    """temperature / top-k / top-p draw per row (K10).  ``full``: whether any non-greedy row has
+    top_k = 0 or > SAMPLE_MAX_CAND (those rows are drawn from the whole vocabulary); None =
+    find out from ``top_ks`` / ``temps`` (one device sync)."""
     if not logits.is_cuda:
         from ..runtime.sampler import sample_reference
 
         return sample_reference(logits, temps, top_ks, top_ps, uniform)
     _need_gpu()
+    if full is None:
+        full = bool((((top_ks <= 0) | (top_ks > SAMPLE_MAX_CAND)) & (temps > 0)).any())
     out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
-    torch.ops.mlop.sample(out, logits, temps, top_ks, top_ps, uniform)
+    torch.ops.mlop.sample(out, logits, temps, top_ks, top_ps, uniform, bool(full))
     return out
 
 

@@ -579,7 +579,7 @@ void argmax(Tensor out, Tensor logits) {
                       (int)logits.size(1), logits.stride(0), cur_stream());
 }
 
-void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, Tensor uniform) {
+void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, Tensor uniform, bool full) {
   check_logits(logits);
   const int64_t n = logits.size(0);
   TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == n, "out int64 [n]");
@@ -595,7 +595,7 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
   mlop::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), (int)n,
                       (int)logits.size(1), logits.stride(0), temps.data_ptr<float>(),
                       top_ks.data_ptr<int>(), top_ps.data_ptr<float>(), uniform.data_ptr<float>(),
-                      wsb > 0 ? ws.data_ptr() : nullptr, cur_stream());
+                      wsb > 0 ? ws.data_ptr() : nullptr, full, cur_stream());
 }
 
 
@@ -685,7 +685,7 @@ TORCH_LIBRARY(mlop, m) {
         "Tensor norm_w, float eps) -> bool");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_ps, "
-        "Tensor uniform) -> ()");
+        "Tensor uniform, bool full) -> ()");
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor x, Tensor w, float eps) -> ()");
   m.def("rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor qkv, "

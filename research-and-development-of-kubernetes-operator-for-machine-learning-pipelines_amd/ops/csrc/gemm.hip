@@ -1164,8 +1164,14 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
 // The large-M decoder's norm chain: O / down add into the residual and leave per-row sums of
 // squares (W4_ADD_SS), gate_up / QKV scale their rows by the RMSNorm factor (W4_RS), so the
 // add + RMSNorm passes over [M, H] disappear (norm weights folded into the consumer weights).
+// Everything launch_w4_chain needs, so the caller decides the chain ONCE per forward (before the
+// first in-place residual update) and never meets a refusal mid-layer: the shape on the
+// four-wave kernel, the stream-K scratch that holds the band tickets reserved, and one ticket
+// per 256-row band.
 bool w4_chain_ok(int M, int N, int K) {
   if (M <= 0 || gemv_takes(M, N, K, EPI_NONE) || gemv_takes(M, N, K, EPI_ROPE)) return false;
+  int cus = 0;
+  if (!gemm_sk_available(&cus) || cus <= 0 || (M + 255) / 256 > kSkMaxWg) return false;
   const Plan p = plan(M, N, K, false, 0, 0);
   return p.variant == 5 && p.splits == 1 && p.BM == 256 && p.BN == 256 && gemm_w4_ok(M, N, K, K, K, N);
 }
@@ -1173,11 +1179,8 @@ bool w4_chain_ok(int M, int N, int K) {
 bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K,
                      const RopeEpi& re, hipStream_t st) {
   if (M == 0) return true;
-  int cus = 0;
-  if (!w4_chain_ok(M, N, K) || !gemm_w4_ok(M, N, K, lda, K, ldc) || !gemm_sk_available(&cus) ||
-      (M + 255) / 256 > kSkMaxWg)
-    return false;
-  run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re);
+  if (!w4_chain_ok(M, N, K) || !gemm_w4_ok(M, N, K, lda, K, ldc)) return false;
+  if (!run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re)) return false;
   if ((epi & 3) == EPI_ROPE && re.v_tmp != nullptr) launch_v_scatter(re.v_tmp, re.v_cache, re.slots, M, re.Hkv, re.BS, st);
   return true;
 }

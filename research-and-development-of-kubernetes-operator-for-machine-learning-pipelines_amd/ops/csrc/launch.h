@@ -75,7 +75,7 @@ bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
 bool gemm_w4_split_ok(int T, int nk);
 bool gemm_sk_scratch(float** ws, int** cnt, int* cus);
 bool gemm_sk_available(int* cus);
-void run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
+bool run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
             int K, hipStream_t st, const RopeEpi& re);
 // norm chain on the four-wave kernel (epi flags: 4 = C += A.B^T with ss partials, 8 = rows scaled
 // by re.ss_in; 4, 0|8, 1|8, 3|8 are built): true when every such GEMM of this shape runs there
@@ -142,7 +142,8 @@ void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, vo
 // (sample_workspace_bytes(n, V) bytes, 0 = not needed)
 long sample_workspace_bytes(int n, int V);
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
-                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, hipStream_t st);
+                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, bool full,
+                   hipStream_t st);
 
 // lazily backed KV arenas (vmm.hip): reserve VA, back chunks synchronously or on a native
 // worker thread; the returned owner must outlive every use of the range

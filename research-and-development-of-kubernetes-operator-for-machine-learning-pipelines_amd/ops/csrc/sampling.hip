@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(kSampleThreads) sample_kernel(
     return;
   }
   int K = top_ks[row_id];
-  if (K <= 0 || K > kMaxCand) K = kMaxCand;
+  if (K <= 0 || K > kMaxCand) return;  // full-vocabulary rows: sample_full_kernel
   if (K > V) K = V;
 
   // ---- exact radix select of the K-th largest key (4 x 8-bit digits, MSB first)
@@ -323,8 +323,9 @@ __global__ void __launch_bounds__(kSampleThreads) sample_presel_kernel(
   const float* row = logits + row_id * ld + j0;
   for (int j = threadIdx.x; j < len; j += blockDim.x) sl[j] = row[j];
   int K = top_ks[row_id];
-  if (K <= 0 || K > kMaxCand) K = kMaxCand;
-  if (temps[row_id] <= 0.f) K = 1;  // greedy row: its slice max is all stage 2 needs
+  // greedy row: its slice max is all stage 2 needs; full-vocabulary rows (top_k = 0 or > kMaxCand)
+  // are drawn by sample_full_kernel from the row itself, stage 2 skips them
+  if (temps[row_id] <= 0.f || K <= 0 || K > kMaxCand) K = 1;
   if (K > len) K = len;
   __syncthreads();
   uint32_t prefix = 0, mask = 0, remaining = (uint32_t)K;
@@ -371,6 +372,188 @@ __global__ void __launch_bounds__(kSampleThreads) sample_presel_kernel(
   }
 }
 
+// ---- full-vocabulary draw: top_k = 0 (or top_k > kMaxCand) -------------------------------
+// The candidate kernels above draw from the top <= kMaxCand logits; a row without a top-k bound
+// must draw from the softmax over the WHOLE vocabulary (with top-p: its nucleus over the full
+// mass).  One workgroup per row, every pass a sweep over the row (L2-resident after the first):
+//   1. row max (argmax pass);
+//   2. top_k > kMaxCand: the K-th largest key by an exact 4 x 8-bit radix count select (members:
+//      keys >= it; ties at the K-th value all kept);
+//   3. top_p < 1: the nucleus threshold by a radix select on MASS instead of count: 4 passes of
+//      256-bucket histograms of the members' fixed-point weights w = exp((l - max) / T) * 2^40
+//      (u64 LDS atomics: integer sums, so the result does not depend on the order in which the
+//      threads add -- a seeded request draws the same token every time); the threshold key's
+//      ties are taken in vocabulary order until the mass reaches p of the total;
+//   4. the draw: inverse CDF over the nucleus in VOCABULARY order (any fixed order gives the
+//      same distribution), each thread owning one contiguous chunk: per-thread tie counts and
+//      masses, two block scans, and the thread whose mass interval holds u * total walks its chunk.
+// Weights below 2^-40 of the max's round to 0 (<= V * 2^-40 ~ 1e-7 of the mass for a 128k vocab).
+constexpr float kFixOne = 1099511627776.0f;  // 2^40: the row max's fixed-point weight
+
+__device__ __forceinline__ unsigned long long fix_w(float x, float vmax, float invT) {
+  return (unsigned long long)(__expf((x - vmax) * invT) * kFixOne);
+}
+
+__device__ __forceinline__ float key_float(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ void __launch_bounds__(kSampleThreads) sample_full_kernel(
+    long* __restrict__ out, const float* __restrict__ logits, int V, long ld, const float* __restrict__ temps,
+    const int* __restrict__ top_ks, const float* __restrict__ top_ps, const float* __restrict__ uniform) {
+  __shared__ unsigned long long hm[256];
+  __shared__ uint32_t hc[256];
+  __shared__ unsigned long long tm[kSampleThreads];
+  __shared__ uint32_t tcnt[kSampleThreads];
+  __shared__ float sv[kSampleThreads / 64];
+  __shared__ int si[kSampleThreads / 64];
+  __shared__ uint32_t s_prefix, s_rem;
+  __shared__ unsigned long long s_need, s_total;
+
+  const int row_id = blockIdx.x, tid = threadIdx.x;
+  const float T = temps[row_id];
+  const int K = top_ks[row_id];
+  if (T <= 0.f || (K > 0 && K <= kMaxCand)) return;  // sample_kernel's rows
+  const float* row = logits + row_id * ld;
+  float vmax;
+  int imax;
+  block_argmax(row, V, sv, si, vmax, imax);
+  const float invT = 1.f / T;
+
+  // 2. members: keys >= thr_k
+  uint32_t thr_k = 0;
+  if (K > 0 && K < V) {
+    uint32_t prefix = 0, mask = 0, remaining = (uint32_t)K;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int b = tid; b < 256; b += blockDim.x) hc[b] = 0;
+      __syncthreads();
+      for (int j = tid; j < V; j += blockDim.x) {
+        const uint32_t k = fkey(row[j]);
+        if ((k & mask) == prefix) atomicAdd(&hc[(k >> shift) & 0xff], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t above = 0;
+        int d = 255;
+        for (; d > 0; --d) {
+          if (above + hc[d] >= remaining) break;
+          above += hc[d];
+        }
+        s_prefix = prefix | ((uint32_t)d << shift);
+        s_rem = remaining - above;
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      remaining = s_rem;
+      mask |= 0xffu << shift;
+    }
+    thr_k = prefix;
+  }
+
+  // 3. nucleus: keys > thr, plus the first n_eq keys == thr in vocabulary order
+  uint32_t thr = thr_k, n_eq = 0xffffffffu;
+  const float p = top_ps[row_id];
+  if (p < 1.f) {
+    uint32_t prefix = 0, mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      for (int b = tid; b < 256; b += blockDim.x) { hm[b] = 0; hc[b] = 0; }
+      __syncthreads();
+      for (int j = tid; j < V; j += blockDim.x) {
+        const float x = row[j];
+        const uint32_t k = fkey(x);
+        if (k >= thr_k && (k & mask) == prefix) {
+          const uint32_t d = (k >> shift) & 0xff;
+          atomicAdd(&hm[d], fix_w(x, vmax, invT));
+          atomicAdd(&hc[d], 1u);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned long long need;
+        if (shift == 24) {
+          unsigned long long tot = 0;
+          for (int b = 0; b < 256; ++b) tot += hm[b];
+          need = (unsigned long long)ceil((double)p * (double)tot);
+          if (need == 0) need = 1;
+        } else {
+          need = s_need;
+        }
+        unsigned long long above = 0;
+        int d = 255;
+        for (; d > 0; --d) {
+          if (above + hm[d] >= need) break;
+          above += hm[d];
+        }
+        s_prefix = prefix | ((uint32_t)d << shift);
+        s_need = need > above ? need - above : 1;
+        s_rem = hc[d];
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      mask |= 0xffu << shift;
+    }
+    thr = prefix;
+    const unsigned long long wt = fix_w(key_float(thr), vmax, invT);
+    n_eq = s_rem;
+    if (wt > 0) {
+      const unsigned long long t = (s_need + wt - 1) / wt;
+      if (t < n_eq) n_eq = (uint32_t)(t < 1 ? 1 : t);
+    }
+  }
+
+  // 4. the draw, vocabulary order
+  const int ch = (V + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int j0 = min(V, tid * ch), j1 = min(V, j0 + ch);
+  uint32_t ties = 0;
+  for (int j = j0; j < j1; ++j) ties += fkey(row[j]) == thr;
+  tcnt[tid] = ties;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int t = 0; t < (int)blockDim.x; ++t) { const uint32_t v = tcnt[t]; tcnt[t] = acc; acc += v; }
+  }
+  __syncthreads();
+  const uint32_t tie0 = tcnt[tid];
+  unsigned long long m = 0;
+  uint32_t tr = tie0;
+  for (int j = j0; j < j1; ++j) {
+    const float x = row[j];
+    const uint32_t k = fkey(x);
+    const bool in = k > thr || (k == thr && tr++ < n_eq);
+    if (in) m += fix_w(x, vmax, invT);
+  }
+  tm[tid] = m;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long acc = 0;
+    for (int t = 0; t < (int)blockDim.x; ++t) { const unsigned long long v = tm[t]; tm[t] = acc; acc += v; }
+    s_total = acc;
+  }
+  __syncthreads();
+  const unsigned long long total = s_total;
+  unsigned long long target = (unsigned long long)((double)uniform[row_id] * (double)total);
+  if (target >= total) target = total > 0 ? total - 1 : 0;
+  const unsigned long long base = tm[tid];
+  if (total == 0) {
+    if (tid == 0) out[row_id] = imax == 0x7fffffff ? 0 : imax;
+    return;
+  }
+  if (m > 0 && base <= target && target < base + m) {
+    unsigned long long cum = base;
+    tr = tie0;
+    int pick = j1 - 1;
+    for (int j = j0; j < j1; ++j) {
+      const float x = row[j];
+      const uint32_t k = fkey(x);
+      const bool in = k > thr || (k == thr && tr++ < n_eq);
+      if (!in) continue;
+      cum += fix_w(x, vmax, invT);
+      if (cum > target) { pick = j; break; }
+    }
+    out[row_id] = pick;
+  }
+}
+
 // workgroups per row of the pre-selection (1 = sample_kernel alone over the full row)
 int sample_splits(int n, int V) {
   if (n <= 0 || n >= 64) return 1;
@@ -404,8 +587,12 @@ void launch_argmax_bf16(long* out, const void* logits, int n, int V, long ld, vo
 }
 
 void launch_sample(long* out, const float* logits, int n, int V, long ld, const float* temps,
-                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, hipStream_t st) {
+                   const int* top_ks, const float* top_ps, const float* uniform, void* ws, bool full,
+                   hipStream_t st) {
   if (n == 0) return;
+  // rows with top_k = 0 / > kMaxCand (the caller knows whether there are any): drawn from the
+  // whole row; the candidate kernels below skip them
+  if (full) sample_full_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld, temps, top_ks, top_ps, uniform);
   const int S = ws ? sample_splits(n, V) : 1;
   if (S <= 1) {
     sample_kernel<<<n, kSampleThreads, 0, st>>>(out, logits, V, ld, temps, top_ks, top_ps, uniform);

@@ -594,7 +594,8 @@ class Engine:
                               greedy=all(p.greedy for p in done_params))
         tokens = None
         if nl:
-            tokens = self._sample(logits, done_params).tolist()
+            tokens = self._sample(logits, done_params,
+                                  lambda: [len(s.output) for s, d in zip(batch, done) if d]).tolist()
         else:
             torch.cuda.synchronize() if self.device.type == "cuda" else None
         self.stats["prefill_steps"] += 1
@@ -633,7 +634,7 @@ class Engine:
             params = _ParamsList([s.params for s in self.running] + [s.params for s in done_seqs])
         logits = self._launch(KIND_EAGER, T, nt, nl, part, nparts, 0,
                               greedy=getattr(params, "all_greedy", False))
-        toks = self._sample(logits, params).cpu().numpy().astype(np.int64)
+        toks = self._sample(logits, params, lambda: self._gen_index(rows, done_seqs)).cpu().numpy().astype(np.int64)
         t2 = time.perf_counter()
         self.stats["mixed_steps"] += 1
         self.stats["decode_tokens"] += B
@@ -745,7 +746,7 @@ class Engine:
         logits = self._launch(*launch, greedy=greedy)
         if launch[0] == KIND_GRAPH:
             logits = logits[:B]
-        toks_d = self._sample(logits, params)
+        toks_d = self._sample(logits, params, lambda: self._gen_index(rows, done_seqs))
         n = int(toks_d.shape[0])
         toks_h = self._toks_h[self._toks_flip][:n]
         self._toks_flip ^= 1
@@ -944,7 +945,7 @@ class Engine:
             t1 = time.perf_counter()
             logits = self._launch(KIND_EAGER, B, B, B, part, nparts, 0, greedy=greedy)
             self.stats["eager_decode_steps"] += 1
-        toks = self._sample(logits, params).cpu().numpy().astype(np.int64)
+        toks = self._sample(logits, params, lambda: self._gen_index(rows, ())).cpu().numpy().astype(np.int64)
         t2 = time.perf_counter()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += B
@@ -1091,8 +1092,13 @@ class Engine:
         best = allp[:, :, 0].argmax(dim=1)  # first max: the lowest rank = the lowest vocab index
         return _Tokens(allp[torch.arange(allp.shape[0], device=allp.device), best, 1].to(torch.int64))
 
-    def _sample(self, out, params):
-        return out.ids if isinstance(out, _Tokens) else self.sampler(out, params)
+    def _sample(self, out, params, gen_index=None):
+        return out.ids if isinstance(out, _Tokens) else self.sampler(out, params, gen_index)
+
+    def _gen_index(self, rows, done_seqs):
+        """Output position of each row's draw (seeded sampling): decode rows' generated count
+        (it counts an in-flight token under async scheduling), then the prompts that completed."""
+        return np.concatenate([self.r_gen[rows], np.asarray([len(s.output) for s in done_seqs], dtype=np.int64)])
 
     def worker_loop(self):
         """Non-zero TP ranks: replay rank 0's steps until it sends STOP."""

@@ -28,26 +28,64 @@ class SamplingParams:
         return self.temperature <= 0.0
 
 
-MAX_TOP_K = 1024  # candidates kept by the sampling kernel (top_k=0 with top_p<1 uses this many)
+MAX_TOP_K = 1024  # candidates of the top-k kernel; top_k = 0 or > MAX_TOP_K draws from the whole vocabulary
+
+
+def seeded_uniform(seed: int, index: int) -> float:
+    """The uniform of draw ``index`` (the token's position in the request's output) of a request
+    with ``SamplingParams.seed``: a splitmix64 hash of (seed, index), 24 bits, exact in fp32.
+    Independent of the batch the request rides in, of preemption and of other requests."""
+    z = (int(seed) * 0x9E3779B97F4A7C15 + (int(index) + 1) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    z ^= z >> 31
+    return (z >> 40) / float(1 << 24)
+
+
+def _sample_full_row(l: torch.Tensor, T: float, k: int, p: float, u: float) -> int:
+    """One row without a candidate bound (top_k = 0 or > MAX_TOP_K), fp64: members = the top-k
+    by value (ties at the k-th value all kept) or the whole vocabulary; nucleus = the smallest
+    prefix of the members sorted by value (ties by index) whose softmax mass reaches p of the
+    members' mass; the draw = inverse CDF over the nucleus in vocabulary order."""
+    V = l.numel()
+    l = l.double()
+    member = torch.ones(V, dtype=torch.bool)
+    if 0 < k < V:
+        member = l >= torch.topk(l, k).values[-1]
+    w = torch.exp((l - l.max()) / T) * member
+    nucleus = member
+    if p < 1.0:
+        order = torch.sort(-l, stable=True).indices  # descending value, ties by index
+        cum = torch.cumsum(w[order], 0)
+        keep = min(int((cum < p * float(cum[-1])).sum()) + 1, int(member.sum()))
+        nucleus = torch.zeros(V, dtype=torch.bool)
+        nucleus[order[:keep]] = True
+    c = torch.cumsum(w * nucleus, 0)
+    return int(min(int((c <= u * float(c[-1])).sum()), V - 1))
 
 
 def sample_reference(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor,
                      top_p: torch.Tensor, uniform: torch.Tensor) -> torch.Tensor:
-    """Plain-torch sampler with the kernel's semantics.
+    """Plain-torch sampler with the kernels' semantics (sampling.hip).
 
-    temps/top_k/top_p/uniform: [n]; rows with temp <= 0 are greedy.  Candidates:
-    the top min(top_k or MAX_TOP_K, V) logits; probabilities = softmax(l / T)
-    over them; top-p keeps the smallest prefix with mass >= p; the token is the
-    first candidate whose cumulative (renormalised) mass exceeds u."""
+    temps/top_k/top_p/uniform: [n]; rows with temp <= 0 are greedy (argmax, ties to the lowest
+    index).  0 < top_k <= MAX_TOP_K: candidates = the top-k logits; probabilities =
+    softmax(l / T) over them; top-p keeps the smallest prefix with mass >= p; the token is the
+    first candidate whose cumulative (renormalised) mass exceeds u.  top_k = 0 (or larger than
+    MAX_TOP_K): the softmax over the WHOLE vocabulary (``_sample_full_row``)."""
     n, V = logits.shape
     out = torch.empty(n, dtype=torch.int64, device=logits.device)
     kmax = min(MAX_TOP_K, V)
-    vals, idx = torch.topk(logits.float(), kmax, dim=-1)  # sorted desc
+    lf = logits.float()
+    vals, idx = torch.topk(lf, kmax, dim=-1)  # sorted desc
     for i in range(n):
         if float(temps[i]) <= 0.0:
-            out[i] = idx[i, 0]
+            out[i] = lf[i].argmax()
             continue
-        k = int(top_k[i]) if int(top_k[i]) > 0 else kmax
+        k = int(top_k[i])
+        if k <= 0 or k > MAX_TOP_K:
+            out[i] = _sample_full_row(lf[i].cpu(), float(temps[i]), k, float(top_p[i]), float(uniform[i]))
+            continue
         k = min(k, kmax)
         v = vals[i, :k] / float(temps[i])
         p = torch.softmax(v, dim=-1)
@@ -70,17 +108,26 @@ class Sampler:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
 
-    def __call__(self, logits: torch.Tensor, params: list[SamplingParams]) -> torch.Tensor:
+    def __call__(self, logits: torch.Tensor, params: list[SamplingParams], gen_index=None) -> torch.Tensor:
+        """``gen_index``: per row, the position of this draw in its request's output (array, or a
+        callable returning one; only consulted when a row has ``SamplingParams.seed``)."""
         n = logits.shape[0]
         if getattr(params, "all_greedy", False) or all(p.greedy for p in params[:n]):
             return ops.argmax(logits) if logits.is_cuda else logits.argmax(-1)
         dev = logits.device
         logits = logits.float()  # the top-k / top-p kernel works on fp32 rows
-        temps = torch.tensor([p.temperature for p in params[:n]], dtype=torch.float32)
-        ks = torch.tensor([p.top_k for p in params[:n]], dtype=torch.int32)
-        ps = torch.tensor([p.top_p for p in params[:n]], dtype=torch.float32)
+        rows = params[:n]
+        temps = torch.tensor([p.temperature for p in rows], dtype=torch.float32)
+        ks = torch.tensor([p.top_k for p in rows], dtype=torch.int32)
+        ps = torch.tensor([p.top_p for p in rows], dtype=torch.float32)
         u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float32)
+        seeded = [i for i, p in enumerate(rows) if p.seed is not None and not p.greedy]
+        if seeded:
+            gi = gen_index() if callable(gen_index) else gen_index
+            us = [seeded_uniform(rows[i].seed, int(gi[i]) if gi is not None else 0) for i in seeded]
+            u[torch.tensor(seeded, device=self.device)] = torch.tensor(us, dtype=torch.float32).to(self.device)
         if logits.is_cuda:
+            full = bool((((ks <= 0) | (ks > MAX_TOP_K)) & (temps > 0)).any())
             return ops.sample(logits, temps.to(dev, non_blocking=True), ks.to(dev, non_blocking=True),
-                              ps.to(dev, non_blocking=True), u)
+                              ps.to(dev, non_blocking=True), u, full=full)
         return sample_reference(logits, temps, ks, ps, u)

@@ -277,12 +277,14 @@ def test_argmax(gpu, n, V, dtype):
 @pytest.mark.parametrize("n,V", [(16, 32000), (4, 128256), (64, 32000), (8, 1000)])
 def test_sample_matches_reference(gpu, n, V):
     """n < 64: per-slice top-K pre-selection (16 workgroups per row) + the draw over the
-    candidates; n = 64: the single-stage kernel; same uniforms as the reference.
+    candidates; n = 64: the single-stage kernel; rows with top_k = 0: the full-vocabulary
+    kernel (softmax over the WHOLE row, top-p over the full mass); same uniforms as the reference.
 
-    Exact, tie-safe check of EVERY row: the drawn token must be the candidate whose interval
-    [c_{j-1}, c_j) of the fp64 reference CDF (top-k, temperature, top-p renormalised) holds u.
-    Only when u or the top-p cut lies within 1e-5 of an interval edge -- where fp32 summation
-    order legitimately decides -- is the neighbouring candidate accepted as well."""
+    Exact, tie-safe check of EVERY row: the drawn token must be the one whose interval
+    [c_{j-1}, c_j) of the fp64 reference CDF holds u (candidates in value order for top-k rows;
+    the nucleus in vocabulary order for full rows).  Only when u or the top-p cut lies within
+    1e-5 of an interval edge -- where fp32 summation order legitimately decides -- is the
+    neighbouring candidate accepted as well."""
     torch.manual_seed(1)
     x = 3 * torch.randn(n, V, device=gpu)
     temps = torch.tensor([0.0, 0.7, 1.0, 1.3] * (n // 4), device=gpu)
@@ -294,15 +296,35 @@ def test_sample_matches_reference(gpu, n, V):
 
     eps = 1e-5
     kmax = min(MAX_TOP_K, V)
-    vals, idx = torch.topk(x.cpu().double(), kmax, dim=-1)
+    xd = x.cpu().double()
+    vals, idx = torch.topk(xd, kmax, dim=-1)
     for i in range(n):
         if float(temps[i]) <= 0 or int(ks[i]) == 1:  # greedy rows: exact argmax
             assert int(got[i]) == int(idx[i, 0]), i
             continue
-        k = min(int(ks[i]) or kmax, kmax)
-        pr = torch.softmax(vals[i, :k] / float(temps[i]), dim=-1)
+        pp, ui, T = float(ps[i]), float(u[i]), float(temps[i])
+        if int(ks[i]) == 0:  # the whole vocabulary
+            w = torch.exp((xd[i] - xd[i].max()) / T)
+            order = torch.sort(-xd[i], stable=True).indices
+            cum = torch.cumsum(w[order], 0) / w.sum()
+            keep0 = int((cum < pp).sum()) + 1 if pp < 1 else V
+            keeps = {min(keep0, V)} | {kk for kk in (keep0 - 1, keep0 + 1)
+                                       if pp < 1 and 1 <= kk <= V and abs(float(cum[kk - 1]) - pp) < eps}
+            ok = False
+            for keep in keeps:
+                nuc = torch.zeros(V, dtype=torch.bool)
+                nuc[order[:keep]] = True
+                if not nuc[int(got[i])]:
+                    continue
+                c = torch.cumsum(w * nuc, 0) / (w * nuc).sum()
+                j = int(got[i])
+                lo = 0.0 if j == 0 else float(c[j - 1])
+                ok |= lo - eps <= ui <= float(c[j]) + eps
+            assert ok, (i, int(got[i]), ui)
+            continue
+        k = min(int(ks[i]), kmax)
+        pr = torch.softmax(vals[i, :k] / T, dim=-1)
         c = torch.cumsum(pr, dim=-1)
-        pp, ui = float(ps[i]), float(u[i])
         keeps = {k}
         if pp < 1.0:
             keep = min(int((c < pp).sum()) + 1, k)
@@ -318,6 +340,47 @@ def test_sample_matches_reference(gpu, n, V):
             hi = 1.0 if j == keep - 1 else float(cc[j])
             ok |= lo - eps <= ui <= hi + eps
         assert ok, (i, int(got[i]), ui)
+
+
+def test_sample_full_vocab_distribution(gpu):
+    """temperature > 0, top_k = 0, top_p = 1 samples the UNTRUNCATED softmax: over a 4096-token
+    vocabulary whose logits are flat up to a +-0.3 ramp, 3/4 of the mass lies outside the top
+    1024 logits (a 1024-candidate sampler would never draw there).  8192 draws; the empirical
+    frequencies of 8 equal-width index bands match the fp64 softmax within 4 sigma.  Also the
+    top_p = 0.5 nucleus: no draw outside the smallest prefix holding half the mass."""
+    V, n = 4096, 8192
+    torch.manual_seed(3)
+    row = torch.linspace(-0.3, 0.3, V, device=gpu)[torch.randperm(V, device=gpu)]
+    x = row.expand(n, V).contiguous()
+    temps = torch.ones(n, device=gpu)
+    ks = torch.zeros(n, dtype=torch.int32, device=gpu)
+    got = ops.sample(x, temps, ks, torch.ones(n, device=gpu), torch.rand(n, device=gpu)).cpu()
+    p = torch.softmax(row.double().cpu(), 0)
+    top1024 = set(torch.topk(row.cpu(), 1024).indices.tolist())
+    outside = sum(int(t) not in top1024 for t in got.tolist()) / n
+    p_out = 1 - float(p[list(top1024)].sum())
+    assert abs(outside - p_out) < 4 * (p_out * (1 - p_out) / n) ** 0.5 + 1e-3, (outside, p_out)
+    band = got // (V // 8)
+    for b in range(8):
+        pb = float(p[b * V // 8:(b + 1) * V // 8].sum())
+        fb = float((band == b).float().mean())
+        assert abs(fb - pb) < 4 * (pb * (1 - pb) / n) ** 0.5 + 1e-3, (b, fb, pb)
+    got = ops.sample(x, temps, ks, torch.full((n,), 0.5, device=gpu), torch.rand(n, device=gpu)).cpu()
+    order = torch.sort(-row.double().cpu(), stable=True).indices
+    keep = int((torch.cumsum(p[order], 0) < 0.5).sum()) + 1
+    assert set(got.tolist()) <= set(order[:keep + 1].tolist())
+
+
+def test_sampler_seed_reproducible(gpu):
+    """SamplingParams.seed: the same (seed, output position) draws the same uniform in any batch."""
+    from mlopamd.runtime.sampler import Sampler, SamplingParams
+
+    torch.manual_seed(4)
+    x = torch.randn(6, 32000, device=gpu)
+    mk = lambda s: SamplingParams(temperature=1.0, top_k=0, seed=s)  # noqa: E731
+    a = Sampler(gpu, seed=1)(x, [mk(7), mk(8), mk(None), mk(7), mk(9), mk(7)], gen_index=[3, 3, 0, 3, 0, 4])
+    b = Sampler(gpu, seed=2)(x[[3, 0, 1]], [mk(7), mk(7), mk(8)], gen_index=[3, 3, 3])
+    assert int(a[0]) == int(b[1]) and int(a[1]) == int(b[2]) and int(a[3]) == int(b[0])
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (7, 6144, 4096), (64, 4096, 14336),

@@ -129,3 +129,59 @@ def test_llama_forward_chain_on_off(gpu, w4, monkeypatch):
                 best = int(lg.argmax())
                 assert t == best or float(lg[best] - lg[t]) < 0.1 * float(lg.std()), (mode, len(toks), best, t)
                 toks.append(t)
+
+
+def test_gemm_res_ss_odd_group_count(gpu, w4):
+    """N = 3840 = 256 mod 512: the band ticket's row sum reads 30 groups of 128 columns (7
+    16-byte loads + one 8-byte tail).  A 4-wide-only loop would add the next row's first two
+    partials into every total."""
+    M, N, K = 2048, 3840, 4096
+    assert torch.ops.mlop.w4_chain_ok(M, N, K)
+    torch.manual_seed(7)
+    a = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    r = torch.randn(M, N, device=gpu, dtype=bf)
+    ss = ops.ss_buffer(M, N, gpu).fill_(float("nan"))
+    ops.gemm_res_ss(a, w, r, ss)
+    part, tot = ops.ss_parts(ss, M, N)
+    close(part, r.float().pow(2).view(M, N // 128, 128).sum(-1), atol=1e-3, rtol=1e-4)
+    close(tot, r.float().pow(2).sum(-1), atol=1e-2, rtol=1e-4)
+
+
+def test_checkpoint_norms_folded_chain_matches_hf(gpu, w4, tmp_path, monkeypatch):
+    """A checkpoint with trained (non-unit) RMSNorm weights: load_pretrained folds them into
+    QKV / gate_up, so the 2048-row prefill runs the norm chain, and its first tokens are the
+    fp32 transformers model's argmax (up to bf16 near-ties).  MLOP_FOLD_NORMS=0 keeps the norm
+    weights and the chain off."""
+    transformers = pytest.importorskip("transformers")
+    from mlopamd.models import loader
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    torch.manual_seed(5)
+    hf = transformers.LlamaForCausalLM(transformers.LlamaConfig(
+        vocab_size=1024, hidden_size=H, intermediate_size=I, num_hidden_layers=1, num_attention_heads=32,
+        num_key_value_heads=8, head_dim=128, max_position_embeddings=1024,
+        rope_parameters={"rope_theta": 500000.0, "rope_type": "default"})).eval()
+    with torch.no_grad():
+        for layer in hf.model.layers:
+            layer.input_layernorm.weight.uniform_(0.5, 1.5)
+            layer.post_attention_layernorm.weight.uniform_(0.5, 1.5)
+    hf.save_pretrained(tmp_path)
+    monkeypatch.setenv("MLOP_FOLD_NORMS", "0")
+    assert not loader.load_pretrained(tmp_path, device=gpu).unit_norms
+    monkeypatch.delenv("MLOP_FOLD_NORMS")
+    model = loader.load_pretrained(tmp_path, device=gpu)
+    assert model.unit_norms and model._chain_ok(2048)
+    eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=2048, max_model_len=512,
+                                     num_kv_blocks=8 * 32 + 1, use_graphs=False))
+    g = torch.Generator().manual_seed(11)
+    prompts = [torch.randint(3, 1000, (256,), generator=g).tolist() for _ in range(8)]
+    ops._GEMM_USED.clear()
+    outs = eng.generate(prompts, SamplingParams(max_tokens=1, ignore_eos=True))
+    assert ops.EPI_ADD_SS in set(k[3] for k in ops._GEMM_USED)
+    hf = hf.to(gpu)
+    with torch.no_grad():
+        lg = hf(torch.tensor(prompts, device=gpu)).logits[:, -1].float()
+    for row, o in zip(lg, outs):
+        assert row[o[0]] >= row.max() - 0.05 * row.abs().max(), (int(row.argmax()), o[0])
