@@ -96,7 +96,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     BUILD.mkdir(exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     kernels = sorted(CSRC.glob("*.hip"))
-    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__=1"]
+    # -Werror=return-type: a value-returning function that falls off its end is UB (a host crash)
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__=1", "-Werror=return-type"]
     jobs_list = []  # (cmd, obj, digest)
     for src in kernels:
         obj = BUILD / (src.stem + ".o")

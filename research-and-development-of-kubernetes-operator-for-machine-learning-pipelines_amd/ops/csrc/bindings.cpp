@@ -625,6 +625,47 @@ int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
 
+// ---- expert-parallel exchange over IPC peer memory (ep_exchange.hip) -------------
+int64_t ep_create(int64_t rank, int64_t world, int64_t E, int64_t k, int64_t H, int64_t tcap, int64_t device) {
+  return mlop::ep_create((int)rank, (int)world, (int)E, (int)k, (int)H, (int)tcap, (int)device);
+}
+Tensor ep_ipc_handle(int64_t h) {
+  Tensor t = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  mlop::ep_ipc_handle((long)h, t.data_ptr());
+  return t;
+}
+void ep_open(int64_t h, Tensor handles) {
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
+              handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
+  mlop::ep_open((long)h, handles.data_ptr());
+}
+// xp [rows, H] bf16 <- this rank's received rows grouped by local expert; offsets int32 [n_local + 1]
+void ep_dispatch(int64_t h, Tensor xp, Tensor offsets, Tensor x, Tensor topi) {
+  const long H = mlop::ep_hidden((long)h), k = mlop::ep_topk((long)h);
+  check_bf16(xp, "xp"); check_bf16(x, "x"); check_i32(topi, "topi"); check_i32(offsets, "offsets");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == H && xp.dim() == 2 && xp.size(1) == H, "ep_dispatch: [*, H] rows");
+  TORCH_CHECK(topi.dim() == 2 && topi.size(0) == x.size(0) && topi.size(1) == k, "ep_dispatch: topi [T, k]");
+  TORCH_CHECK(offsets.numel() == mlop::ep_local_experts((long)h) + 1, "ep_dispatch: offsets [n_local + 1]");
+  TORCH_CHECK(x.size(0) <= mlop::ep_tcap((long)h), "ep_dispatch: T exceeds the exchange's token capacity");
+  c10::DeviceGuard g(x.device());
+  mlop::ep_dispatch((long)h, xp.data_ptr(), (long)xp.size(0), offsets.data_ptr<int>(), x.data_ptr(),
+                    topi.data_ptr<int>(), (int)x.size(0), cur_stream());
+}
+// out [T, H] bf16 <- sum_j topw[t, j] * expert_j(x[t]) from the owners of the experts
+void ep_combine(int64_t h, Tensor out, Tensor y, Tensor topw, Tensor topi) {
+  const long H = mlop::ep_hidden((long)h), k = mlop::ep_topk((long)h);
+  check_bf16(out, "out"); check_bf16(y, "y"); check_i32(topi, "topi");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_cuda() && topw.is_contiguous(), "topw fp32");
+  TORCH_CHECK(out.dim() == 2 && out.size(1) == H && y.dim() == 2 && y.size(1) == H, "ep_combine: [*, H] rows");
+  TORCH_CHECK(topw.numel() == out.size(0) * k && topi.numel() == out.size(0) * k, "ep_combine: [T, k] routing");
+  c10::DeviceGuard g(out.device());
+  mlop::ep_combine((long)h, out.data_ptr(), y.data_ptr(), (long)y.size(0), topw.data_ptr<float>(),
+                   topi.data_ptr<int>(), (int)out.size(0), cur_stream());
+}
+int64_t ep_error(int64_t h) { return mlop::ep_error((long)h); }
+int64_t ep_mem_mode(int64_t h) { return mlop::ep_mem_mode((long)h); }
+void ep_destroy(int64_t h) { mlop::ep_destroy((long)h); }
+
 }  // namespace
 
 // sha256 of the sources this library was built from (ops/build.py writes srchash.cpp)
@@ -640,6 +681,14 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
+  m.def("ep_create(int rank, int world, int E, int k, int H, int tcap, int device) -> int", &ep_create);
+  m.def("ep_ipc_handle(int h) -> Tensor", &ep_ipc_handle);
+  m.def("ep_open(int h, Tensor handles) -> ()", &ep_open);
+  m.def("ep_dispatch(int h, Tensor(a!) xp, Tensor(b!) offsets, Tensor x, Tensor topi) -> ()");
+  m.def("ep_combine(int h, Tensor(a!) out, Tensor y, Tensor topw, Tensor topi) -> ()");
+  m.def("ep_error(int h) -> int", &ep_error);
+  m.def("ep_mem_mode(int h) -> int", &ep_mem_mode);
+  m.def("ep_destroy(int h) -> ()", &ep_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
@@ -725,4 +774,6 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
   m.impl("car_all_reduce", &car_all_reduce);
+  m.impl("ep_dispatch", &ep_dispatch);
+  m.impl("ep_combine", &ep_combine);
 }

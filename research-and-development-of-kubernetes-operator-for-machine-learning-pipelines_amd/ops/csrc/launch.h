@@ -166,4 +166,20 @@ int car_error(long h);
 int car_mem_mode(long h);
 void car_destroy(long h);
 
+// expert-parallel dispatch / combine over IPC peer memory (ep_exchange.hip)
+long ep_create(int rank, int world, int E, int k, int H, int tcap, int device);
+void ep_ipc_handle(long h, void* out64);
+void ep_open(long h, const void* handles);
+int ep_mem_mode(long h);
+int ep_world(long h);
+int ep_local_experts(long h);
+int ep_hidden(long h);
+int ep_topk(long h);
+int ep_tcap(long h);
+void ep_dispatch(long h, void* xp, long xp_rows, int* offsets, const void* x, const int* topi, int T, hipStream_t st);
+void ep_combine(long h, void* out, const void* y, long y_rows, const float* topw, const int* topi, int T,
+                hipStream_t st);
+int ep_error(long h);
+void ep_destroy(long h);
+
 }  // namespace mlop

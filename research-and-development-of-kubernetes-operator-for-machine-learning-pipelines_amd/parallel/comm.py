@@ -48,6 +48,7 @@ class Group:
     size: int = 1
     handle: object = None
     car: object = None  # CustomAllReduce (K15) for small bf16 messages on GPU
+    ex: object = None   # EPExchange (ep_ipc.py): the DP-attention + EP MoE exchange on GPU
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:

@@ -6,9 +6,11 @@ Two placements of the experts of one MoE layer over an EP group:
   rank runs its E/ep local experts on the rows routed to them and the partial
   outputs are summed by the layer's TP all-reduce (no all-to-all).
 * ``alltoall`` — tokens are sharded over the group (DP attention + EP MoE):
-  routed rows go to the rank owning their expert with an all-to-all (dispatch),
-  are computed there with the grouped GEMM, and come back with a second
-  all-to-all (combine), then the top-k weights are applied at the source.
+  routed rows go to the rank owning their expert (dispatch), are computed there
+  with the grouped GEMM, and come back (combine), then the top-k weights are
+  applied at the source.  On GPU the exchange is device-side over IPC peer
+  memory (``_ep_ipc``: exact, sync-free, graph-capturable); the padded RCCL /
+  gloo ``all_to_all_single`` pair (``_alltoall``) is the CPU reference.
 
 On GPU the routing, permutation, grouped GEMM and combine are HIP kernels
 (``ops.moe_*``); CPU tensors run the reference path.
@@ -73,7 +75,26 @@ def moe_forward(x, router_w, w13, w2, top_k: int, ep, e0: int, n_local: int, mod
     topw, topi = route(x, router_w, top_k)
     if ep.size == 1 or mode == "allreduce":
         return local_experts(x, topw, topi, w13, w2, e0, n_local)
+    ex = getattr(ep, "ex", None)
+    if x.is_cuda and ex is not None:
+        return _ep_ipc(x, topw, topi, w13, w2, ex, cap_tokens)
     return _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local, cap_tokens)
+
+
+def _ep_ipc(x, topw, topi, w13, w2, ex, cap_tokens: int | None = None):
+    """Expert-parallel MoE on GPU over IPC peer memory (parallel/ep_ipc.py, ep_exchange.hip):
+    routed rows land in their owner's buffer already grouped by expert (exact counts, no
+    padding rows on the fabric, no host sync), the owner runs its experts' grouped GEMM pair
+    (K13) on them with device offsets, and the outputs go back to the source slots for the
+    top-k weighted combine.  ``cap_tokens``: the group's agreed largest T this step (sizes the
+    received-row buffer and the grouped GEMM grid; rows past the received count are never
+    read)."""
+    T = x.shape[0]
+    xp, offsets = ex.dispatch(x, topi, cap_tokens or T)
+    avg = max(1, (T * ex.k) // max(1, ex.n_local))
+    a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg)
+    y = ops.grouped_gemm(a, w2, offsets, avg_rows=avg)
+    return ex.combine(y, topw, topi, T)
 
 
 def _alltoall(x, topw, topi, w13, w2, top_k, ep, n_local, cap_tokens: int | None = None):

@@ -302,6 +302,8 @@ class Engine:
         self._toks_flip = 0
         self._src_h = torch.zeros(R, dtype=torch.int64, pin_memory=cuda)
         self._src_d = torch.zeros(R, dtype=torch.int64, device=self.device)
+        if self.ep_sync is not None and self.device.type == "cuda":
+            self._setup_ep_exchange()
         self.stats["kv_alloc_ms"] = kv_alloc_ms
         self.stats.update(self.kv.timing_ms)
         self.tracer = StepTracer()
@@ -316,6 +318,20 @@ class Engine:
             self.capture_graphs()
         self.kv.start_background_fill()  # after capture: the rest of a lazy KV arena
         self.stats["kv_ready_blocks_at_start"] = self.alloc.available
+
+    def _setup_ep_exchange(self):
+        """DP-attention + EP on GPU: the device-side MoE exchange over IPC peer memory
+        (parallel/ep_ipc.py), sized for the largest forward this engine runs; collective over
+        the EP group (every rank builds its engine together).  MLOP_EP_IPC=0: RCCL all_to_all."""
+        import os
+
+        ep, mc = self.model.ps.ep, self.model.cfg
+        if os.environ.get("MLOP_EP_IPC", "1") == "0" or ep.ex is not None or not getattr(mc, "num_experts", 0):
+            return
+        from ..parallel.ep_ipc import EPExchange
+
+        ep.ex = EPExchange(ep.rank, ep.size, mc.num_experts, mc.top_k, mc.hidden_size, self.meta.max_tokens,
+                           self.device, group=ep.handle)
 
     # ----------------------------------------------------------- sizing --
     def _auto_blocks(self) -> int:
