@@ -87,6 +87,7 @@ class ParallelState:
     tp: Group
     ep: Group
     ep_cpu: object = None  # gloo group over the EP ranks: per-step control (engine.EPSync)
+    tp_cpu: object = None  # gloo group over the TP ranks: the step header (engine.StepSync)
 
     @property
     def tp_size(self) -> int:
@@ -134,6 +135,13 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
             h = dist.new_group(ranks, backend="gloo")
             if rank in ranks:
                 ep_cpu = h
+    tp_cpu = None
+    if tp_size > 1:  # the per-step header travels host to host, ahead of the device work
+        for start in range(0, world, tp_size):
+            ranks = list(range(start, start + tp_size))
+            h = dist.new_group(ranks, backend="gloo")
+            if rank in ranks:
+                tp_cpu = h
     car_env = os.environ.get("MLOP_CUSTOM_AR", "1")
     backend_ok = dist.get_backend(tp_handle) == "nccl" or car_env == "force"  # force: gloo + GPU tests
     if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() and backend_ok and car_env != "0":
@@ -141,4 +149,4 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
 
         tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
                                  group=tp_handle)
-    return ParallelState(tp=tp, ep=ep, ep_cpu=ep_cpu)
+    return ParallelState(tp=tp, ep=ep, ep_cpu=ep_cpu, tp_cpu=tp_cpu)

@@ -44,30 +44,47 @@ KIND_STOP, KIND_EAGER, KIND_GRAPH, KIND_BARRIER = 0, 1, 2, 3
 
 
 class StepSync:
-    """Lock-step execution across a tensor-parallel group.  Rank 0 writes
-    the step header [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket, num_flash_tiles,
-    greedy] into the head of the step's packed metadata buffer (attn_meta.MetaBuffers: header,
-    int32 metadata, ids and logits index in ONE device buffer, already uploaded by one H2D) and
-    broadcasts that buffer: ONE collective per step (RCCL on GPU, gloo on CPU); every rank then
-    runs the identical forward."""
+    """Lock-step execution across a tensor-parallel group.  Rank 0 alone
+    schedules.  Per step it sends two things:
+
+      * the step header [kind, T, num_tiles, n_logits, part_tokens, nparts, bucket,
+        num_flash_tiles, greedy] HOST to host, over the TP group's gloo (CPU) group: a worker
+        learns what step t+1 is while the device still runs step t, so it enqueues step t+1's
+        forward (and its graph replay) ahead, exactly as the leader does under one-step-ahead
+        scheduling, and no worker ever reads a device tensor back to decide what to run;
+      * the step's packed metadata buffer (attn_meta.MetaBuffers: int32 metadata, ids and
+        logits index in ONE device buffer, already uploaded by one H2D, decode ids gathered on
+        the device from the previous step's tokens) as ONE in-stream device broadcast (RCCL on
+        GPU, gloo on CPU), ordered after the previous forward on every rank's stream.
+    STOP / BARRIER steps carry the header only."""
 
     NHDR = 9
 
-    def __init__(self, group):
+    def __init__(self, group, cpu_group=None):
         self.g = group
+        self.cpu = cpu_group
         self.is_leader = group.rank == 0
+        self.hdr = torch.zeros(self.NHDR, dtype=torch.int64)
+
+    def _bcast_header(self):
+        import torch.distributed as dist
+
+        if self.cpu is None:  # no host group (single process): nothing to agree on
+            return
+        dist.broadcast(self.hdr, src=dist.get_global_rank(self.cpu, 0), group=self.cpu)
 
     def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
-        m = eng.meta
-        m.set_header([kind, T, nt, nl, part, nparts, bucket, npt, greedy])
-        if kind in (KIND_STOP, KIND_BARRIER):  # no step metadata: ship the header alone
-            m.dbuf[:m.HDR].copy_(m.hdr_h, non_blocking=True)
-        self.g.broadcast(m.dbuf, 0)
+        self.hdr[:] = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt, greedy], dtype=torch.int64)
+        self._bcast_header()
+        if kind not in (KIND_STOP, KIND_BARRIER):
+            self.g.broadcast(eng.meta.dbuf, 0)
 
     def recv(self, eng):
-        m = eng.meta
-        self.g.broadcast(m.dbuf, 0)
-        return tuple(m.dbuf[:self.NHDR].tolist())
+        self._bcast_header()
+        hdr = tuple(self.hdr.tolist())
+        if hdr[0] not in (KIND_STOP, KIND_BARRIER):
+            self.g.broadcast(eng.meta.dbuf, 0)
+        return hdr
 
 
 class _Tokens:
@@ -95,14 +112,17 @@ class EPSync:
     def __init__(self, group, cpu_group):
         self.g, self.cpu = group, cpu_group
         self.last_any = 1
+        self.last_busy = 1
 
-    def agree(self, has_work: int, eager: int, tokens: int, bucket: int):
+    def agree(self, has_work: int, eager: int, tokens: int, bucket: int, busy: int = 1):
+        """``busy``: this rank still holds requests (queued, running or in flight) even if it
+        launches nothing this step; the group is done only when no rank is busy."""
         import torch.distributed as dist
 
-        t = torch.tensor([has_work, eager, tokens, bucket], dtype=torch.int64)
+        t = torch.tensor([has_work, eager, tokens, bucket, busy], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.cpu)
-        any_work, any_eager, t_max, b_max = t.tolist()
-        self.last_any = any_work
+        any_work, any_eager, t_max, b_max, any_busy = t.tolist()
+        self.last_any, self.last_busy = any_work, any_busy
         return any_work, any_eager, t_max, b_max
 
 
@@ -233,7 +253,7 @@ class Engine:
         self.max_model_len = min(cfg.max_model_len, mc.max_position)
         nb = cfg.num_kv_blocks or self._auto_blocks()
         tp = model.ps.tp
-        self.step_sync = StepSync(tp) if tp.size > 1 else None
+        self.step_sync = StepSync(tp, model.ps.tp_cpu) if tp.size > 1 else None
         ep = model.ps.ep
         self.ep_sync = EPSync(ep, model.ps.ep_cpu) if (tp.size == 1 and ep.size > 1) else None
         if tp.size > 1:  # every rank must address the same page ids: agree on the minimum
@@ -290,9 +310,10 @@ class Engine:
         self.graph_pool = None
         self.stats = collections.Counter()
         # one-step-ahead (async) scheduling state: the in-flight step, its token read-back
-        # buffers (two pinned, alternating) and the event after its metadata upload
-        self._async = (cfg.async_scheduling and cfg.mixed_prefill and self.step_sync is None
-                       and self.ep_sync is None)
+        # buffers (two pinned, alternating) and the event after its metadata upload.  Under TP
+        # only the leader schedules (workers follow the host-side headers, StepSync); under EP
+        # every rank runs it, the per-step agreement happens at launch time (_ep_agree)
+        self._async = cfg.async_scheduling and cfg.mixed_prefill
         self._pending = None
         self._ids_gather = None
         self._meta_ev = None
@@ -350,13 +371,22 @@ class Engine:
         return int(min(nb, need))
 
     # -------------------------------------------------------- requests --
-    def add_request(self, prompt, params: SamplingParams | None = None, seq_id: int | None = None) -> Sequence:
-        params = params or SamplingParams()
-        prompt = list(prompt)
+    def check_request(self, prompt, params: SamplingParams | None = None) -> None:
+        """ValueError when this engine cannot serve the request (empty / too long prompt, token
+        ids outside the vocabulary, unusable sampling parameters)."""
         if not prompt:
             raise ValueError("empty prompt")
         if len(prompt) >= self.max_model_len:
             raise ValueError(f"prompt of {len(prompt)} tokens exceeds max_model_len {self.max_model_len}")
+        V = self.model.cfg.vocab_size
+        if min(prompt) < 0 or max(prompt) >= V:
+            raise ValueError(f"prompt token ids must be in [0, {V})")
+        (params or SamplingParams()).validate()
+
+    def add_request(self, prompt, params: SamplingParams | None = None, seq_id: int | None = None) -> Sequence:
+        params = params or SamplingParams()
+        prompt = list(prompt)
+        self.check_request(prompt, params)
         sid = next(self._ids) if seq_id is None else seq_id
         seq = Sequence(sid, prompt, params)
         self.seqs[sid] = seq
@@ -471,9 +501,10 @@ class Engine:
     def _ep_idle(self):
         """EP rank with nothing scheduled: agree, then run a padding-only forward (one row
         that attends nothing) eagerly, or replay the agreed decode graph on padding rows."""
-        any_work, eager, t_max, bucket = self.ep_sync.agree(0, 0, 0, 0)
+        any_work, eager, t_max, bucket = self.ep_sync.agree(0, 0, 0, 0, int(self.has_work()))
         if not any_work:
             return
+        self._wait_meta()  # async: the previous step's metadata H2D must have read the host buffer
         empty = np.zeros(0, dtype=np.int32)
         if eager or bucket not in self.graphs:
             self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=1)
@@ -484,6 +515,9 @@ class Engine:
             self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=bucket)
             self.meta.upload(bucket, bucket)
             self.graphs[bucket][0].replay()
+        if self._async and self.device.type == "cuda":
+            self._meta_ev = torch.cuda.Event()
+            self._meta_ev.record()
         self.stats["ep_idle_steps"] += 1
 
     def _step_local(self):
@@ -693,6 +727,22 @@ class Engine:
 
     def _async_step(self):
         prev, self._pending = self._pending, None
+        if not self.running:
+            # nothing decodes: finish the in-flight step (its finished rows free their slots),
+            # then this step's prompt work runs as a synchronous prefill step
+            out = self._async_post(prev) if prev is not None else StepBatch.from_list([])
+            if self._want_prefill():
+                p = self._prefill_step()
+                if p is not None and len(p):
+                    self._decode_since_prefill = 0
+                    reasons = dict(out.reasons)
+                    reasons.update(p.reasons)
+                    out = StepBatch(np.concatenate([out.seq_ids, p.seq_ids]), np.concatenate([out.tokens, p.tokens]),
+                                    np.concatenate([out.fin, p.fin]), reasons)
+                    return "prefill", out
+                if p is not None:
+                    return "prefill", out
+            return "idle", out
         kind, pend = "idle", None
         if self.running:
             self._wait_meta()
@@ -750,6 +800,7 @@ class Engine:
             bucket = next((b for b in self.buckets if b >= B), None)
             if bucket is not None and self.graphs.get(bucket) is not None:
                 self.meta.fill_decode(rows, ctx_d, last, pad_to=bucket)
+                self._repad = (rows, ctx_d, last, int(ctx_d.max()))  # EP: the group may re-pad it
                 launch = (KIND_GRAPH, bucket, bucket, bucket, 0, 0, bucket)
             else:
                 self.meta.fill_decode(rows, ctx_d, last, pad_to=B)
@@ -1040,23 +1091,21 @@ class Engine:
         npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
         if self.ep_sync is not None:
             kind, T, nt, nl, part, nparts, bucket = self._ep_agree(kind, T, nt, nl, part, nparts, bucket)
-        if self.step_sync is not None:
-            t0 = time.perf_counter()
-            self.meta.set_header([kind, T, nt, nl, part, nparts, bucket, npt, int(greedy)])
-            self.meta.upload(T, nl)
-            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt, int(greedy))
-            self.stats["tp_sync_us"] += int(1e6 * (time.perf_counter() - t0))
-            self.stats["tp_sync_calls"] += 1
-        else:
-            self.meta.upload(T, nl)
+        self.meta.upload(T, nl)
         g = self._ids_gather
         if g is not None:
             # async: decode rows' input ids = the previous (in-flight) step's sampled tokens,
-            # gathered on the device after the metadata H2D (which carried placeholders)
+            # gathered on the device after the metadata H2D (which carried placeholders) and
+            # before the TP broadcast of the buffer, so the workers receive the real ids
             self._ids_gather = None
             B, toks_d = g
             self._src_d[:B].copy_(self._src_h[:B], non_blocking=True)
             self.meta.ids_d[:B].copy_(toks_d.index_select(0, self._src_d[:B]))
+        if self.step_sync is not None:
+            t0 = time.perf_counter()
+            self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt, int(greedy))
+            self.stats["tp_sync_us"] += int(1e6 * (time.perf_counter() - t0))
+            self.stats["tp_sync_calls"] += 1
         if self._async and self.device.type == "cuda":
             self._meta_ev = torch.cuda.Event()
             self._meta_ev.record()
@@ -1188,7 +1237,7 @@ class Engine:
         if self.ep_sync is not None:
             while True:
                 self.step()
-                if self.ep_sync.last_any == 0 and all(s.status == Status.FINISHED for s in seqs):
+                if self.ep_sync.last_busy == 0 and all(s.status == Status.FINISHED for s in seqs):
                     return [s.output for s in seqs]
         while any(s.status != Status.FINISHED for s in seqs):
             self.step()

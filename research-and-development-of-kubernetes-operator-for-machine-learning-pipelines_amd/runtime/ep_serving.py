@@ -7,17 +7,24 @@ puts that group behind ONE predictor endpoint, the way the operator deploys it: 
 GPUs, ``python -m mlopamd.runtime.server --ep N`` (``server.launch_ranks`` starts one process
 per GPU; rank 0 serves HTTP).
 
-Per serving iteration, over the group's CPU (gloo) process group:
+Per serving iteration, over the group's CPU (gloo) process group, with fixed-layout int64
+tensors (no pickles: a peer's message can only ever be numbers):
 
-  1. rank 0 broadcasts ``{"stop", "new": [(rid, rank, prompt, params)]}`` -- the requests that
-     arrived over HTTP since the last iteration, each assigned to the least-loaded rank;
-  2. every rank admits its share and runs ONE ``engine.step()`` (the EP agreement inside lets a
-     rank with nothing scheduled join the step's all-to-alls with a padding-only forward);
-  3. ``all_gather_object`` of every rank's ``(rid, token, finished, reason)`` outputs and its
-     running count; rank 0 completes the HTTP futures / stream queues and keeps the load table.
+  1. rank 0 broadcasts a 3-int header [stop, n_new, payload_len] and, when requests arrived over
+     HTTP since the last iteration, one payload tensor of request records (``_pack``): request
+     id, assigned rank (the least-loaded), prompt, sampling parameters (floats as their bit
+     patterns).  Requests are validated on rank 0 BEFORE they are broadcast (``Engine.
+     check_request``): a bad one fails its own HTTP future and never reaches a rank;
+  2. every rank admits its share (an admission that still fails is reported back, below) and
+     runs ONE ``engine.step()`` (the EP agreement inside lets a rank with nothing scheduled join
+     the step's expert exchange with a padding-only forward);
+  3. every rank's outputs go to rank 0 as two all_gathers: [n_out, running, n_failed] counts,
+     then the rows [request id, token, finished, reason code] padded to the largest count; rank
+     0 completes the HTTP futures / stream queues, fails the requests a rank could not admit,
+     and keeps the load table.
 
 All ranks therefore call ``engine.step()`` the same number of times, in lock-step, which the
-EP all-to-alls require.  An idle group keeps a heartbeat (one empty iteration per second) so
+EP exchange requires.  An idle group keeps a heartbeat (one empty iteration per second) so
 the gloo collectives never sit past their timeout.  Reference contract: one predictor per
 model version behind the SeldonDeployment's endpoint (mlflow_operator.py:194-238).
 """
@@ -28,8 +35,15 @@ import os
 import threading
 import time
 
-from .backends import LLMBackend
+import numpy as np
+import torch
+
+from .backends import LLMBackend, _set_exc
 from .sampler import SamplingParams
+
+REASONS = {None: 0, "stop": 1, "length": 2, "abort": 3}
+REASON_NAMES = {v: k for k, v in REASONS.items()}
+FAILED = -1  # reason code of a request a rank could not admit
 
 
 class _Out:
@@ -39,8 +53,40 @@ class _Out:
         self.seq_id, self.token, self.finished, self.finish_reason = rid, token, finished, reason
 
 
-def _params_dict(p: SamplingParams) -> dict:
-    return {k: getattr(p, k) for k in p.__dataclass_fields__}
+def _f2i(x: float) -> int:
+    return int(np.array([x], dtype=np.float64).view(np.int64)[0])
+
+
+def _i2f(i: int) -> float:
+    return float(np.array([i], dtype=np.int64).view(np.float64)[0])
+
+
+def _pack(new) -> torch.Tensor:
+    """[(rid, rank, prompt, SamplingParams)] -> one int64 tensor of records:
+    rid, rank, len(prompt), max_tokens, top_k, ignore_eos, len(stop), has_seed, seed,
+    temperature bits, top_p bits, *stop_token_ids, *prompt."""
+    out = []
+    for rid, r, prompt, p in new:
+        stop = list(p.stop_token_ids)
+        out += [rid, r, len(prompt), int(p.max_tokens), int(p.top_k), int(bool(p.ignore_eos)), len(stop),
+                int(p.seed is not None), int(p.seed or 0), _f2i(p.temperature), _f2i(p.top_p), *stop, *prompt]
+    return torch.tensor(out, dtype=torch.int64)
+
+
+def _unpack(buf: torch.Tensor, n: int):
+    v = buf.tolist()
+    i, out = 0, []
+    for _ in range(n):
+        rid, r, plen, mt, tk, ign, nstop, hs, seed, tb, pb = v[i:i + 11]
+        i += 11
+        stop = v[i:i + nstop]
+        i += nstop
+        prompt = v[i:i + plen]
+        i += plen
+        out.append((rid, r, prompt, SamplingParams(max_tokens=mt, temperature=_i2f(tb), top_k=tk, top_p=_i2f(pb),
+                                                   ignore_eos=bool(ign), stop_token_ids=stop,
+                                                   seed=seed if hs else None)))
+    return out
 
 
 class EPGroupLoop:
@@ -52,38 +98,69 @@ class EPGroupLoop:
         self.rank, self.world = ps.ep.rank, ps.ep.size
         self.local: dict[int, int] = {}  # local seq_id -> global request id
         self.iterations = 0
+        self.hdr = torch.zeros(3, dtype=torch.int64)
 
-    def iterate(self, msg: dict | None) -> tuple[dict, list]:
-        """One lock-step iteration.  ``msg`` is rank 0's broadcast (None elsewhere).  Returns
-        (the broadcast message, every rank's [(outputs, running)])."""
+    def _src(self):
         import torch.distributed as dist
 
-        box = [msg]
-        dist.broadcast_object_list(box, src=dist.get_global_rank(self.group, 0), group=self.group)
-        msg = box[0]
-        for rid, r, prompt, pd in msg["new"]:
-            if r == self.rank:
-                seq = self.engine.add_request(prompt, SamplingParams(**pd))
+        return dist.get_global_rank(self.group, 0)
+
+    def iterate(self, stop: bool = False, new=()) -> tuple[bool, list]:
+        """One lock-step iteration.  ``stop`` / ``new`` [(rid, rank, prompt, params)]: rank 0's
+        (ignored elsewhere).  Returns (stop, every rank's (outputs [n, 4] int64, running))."""
+        import torch.distributed as dist
+
+        if self.rank == 0:
+            payload = _pack(new) if new else None
+            self.hdr.copy_(torch.tensor([int(stop), len(new), 0 if payload is None else payload.numel()]))
+        dist.broadcast(self.hdr, src=self._src(), group=self.group)
+        stop, n_new, plen = (int(x) for x in self.hdr.tolist())
+        if n_new:
+            if self.rank != 0:
+                payload = torch.empty(plen, dtype=torch.int64)
+            dist.broadcast(payload, src=self._src(), group=self.group)
+            new = _unpack(payload, n_new)
+        rows, failed = [], []
+        for rid, r, prompt, params in (new if n_new else ()):
+            if r != self.rank:
+                continue
+            try:
+                seq = self.engine.add_request(prompt, params)
                 self.local[seq.seq_id] = rid
-        outs = []
-        if not msg["stop"]:
+            except Exception:  # noqa: BLE001 - reported to rank 0, which fails that request only
+                failed.append(rid)
+        if not stop:
             for o in self.engine.step():
                 rid = self.local.get(o.seq_id)
                 if rid is None:
                     continue
-                outs.append((rid, int(o.token), bool(o.finished), o.finish_reason))
+                rows.append((rid, int(o.token), int(bool(o.finished)), REASONS.get(o.finish_reason, 0)))
                 if o.finished:
                     self.local.pop(o.seq_id, None)
-        gathered = [None] * self.world
-        dist.all_gather_object(gathered, (outs, self.engine.num_running + len(self.engine.waiting)), group=self.group)
+        rows += [(rid, 0, 1, FAILED) for rid in failed]
+        running = self.engine.num_running + len(self.engine.waiting)
+        cnt = torch.tensor([len(rows), running], dtype=torch.int64)
+        cnts = [torch.zeros(2, dtype=torch.int64) for _ in range(self.world)]
+        dist.all_gather(cnts, cnt, group=self.group)
+        m = max(int(c[0]) for c in cnts)
+        gathered = []
+        if m:
+            mine = torch.zeros(m, 4, dtype=torch.int64)
+            if rows:
+                mine[:len(rows)] = torch.tensor(rows, dtype=torch.int64)
+            allr = [torch.zeros(m, 4, dtype=torch.int64) for _ in range(self.world)]
+            dist.all_gather(allr, mine, group=self.group)
+            gathered = [(allr[r][:int(cnts[r][0])], int(cnts[r][1])) for r in range(self.world)]
+        else:
+            gathered = [(torch.zeros(0, 4, dtype=torch.int64), int(cnts[r][1])) for r in range(self.world)]
         self.iterations += 1
-        return msg, gathered
+        return bool(stop), gathered
 
     def worker(self):
         """Ranks > 0: follow rank 0's iterations until it broadcasts stop."""
         while True:
-            msg, _ = self.iterate(None)
-            if msg["stop"]:
+            stop, _ = self.iterate()
+            if stop:
                 return
 
 
@@ -123,12 +200,17 @@ class EPBackend(LLMBackend):
                 stop = self._stop
             new = []
             for r in pend:
+                try:  # validated HERE, before any rank sees it: a bad request fails alone
+                    self.engine.check_request(list(r.prompt), r.params)
+                except Exception as e:  # noqa: BLE001
+                    r.loop.call_soon_threadsafe(_set_exc, r.future, e)
+                    continue
                 rid = next(self._rid)
                 self._by_rid[rid] = r
-                new.append((rid, self._assign(), list(r.prompt), _params_dict(r.params)))
-            msg, gathered = self.group_loop.iterate({"stop": stop, "new": new})
+                new.append((rid, self._assign(), list(r.prompt), r.params))
+            stop_now, gathered = self.group_loop.iterate(stop, new)
             last = time.perf_counter()
-            if stop:
+            if stop_now:
                 break
             self.steps += 1
             now = time.perf_counter()
@@ -137,9 +219,12 @@ class EPBackend(LLMBackend):
             for rank, (outs, running) in enumerate(gathered):
                 self.load[rank] = running
                 busy = busy or running > 0
-                for rid, tok, fin, reason in outs:
+                for rid, tok, fin, code in outs.tolist():
+                    if code == FAILED:
+                        self._fail(rid, RuntimeError(f"request {rid} could not be admitted on rank {rank}"))
+                        continue
                     n_tok += 1
-                    self._deliver(_Out(rid, tok, fin, reason), now)
+                    self._deliver(_Out(rid, tok, bool(fin), REASON_NAMES.get(code)), now)
             if self.metrics:
                 self.metrics.engine_steps.labels(**self.metrics.labels).inc()
                 if n_tok:
@@ -147,6 +232,13 @@ class EPBackend(LLMBackend):
                 m = self.metrics
                 m.running.labels(**m.labels).set(sum(self.load))
         self.stopped.set()
+
+    def _fail(self, rid, exc):
+        r = self._by_rid.pop(rid, None)
+        if r is not None:
+            if r.queue is not None:
+                r.loop.call_soon_threadsafe(r.queue.put_nowait, None)
+            r.loop.call_soon_threadsafe(_set_exc, r.future, exc)
 
     def _deliver(self, o, now):
         r = self._by_rid.get(o.seq_id)

@@ -27,6 +27,24 @@ class SamplingParams:
     def greedy(self) -> bool:
         return self.temperature <= 0.0
 
+    def validate(self) -> "SamplingParams":
+        """Raise ValueError for parameters no sampler can honour (a bad request fails alone)."""
+        import math
+
+        if int(self.max_tokens) < 1:
+            raise ValueError(f"max_tokens must be >= 1, got {self.max_tokens}")
+        if not math.isfinite(float(self.temperature)) or self.temperature < 0:
+            raise ValueError(f"temperature must be finite and >= 0, got {self.temperature}")
+        if int(self.top_k) < 0:
+            raise ValueError(f"top_k must be >= 0, got {self.top_k}")
+        if not (0.0 < float(self.top_p) <= 1.0):
+            raise ValueError(f"top_p must be in (0, 1], got {self.top_p}")
+        if any(not isinstance(t, int) or t < 0 for t in self.stop_token_ids):
+            raise ValueError("stop_token_ids must be non-negative ints")
+        if self.seed is not None and not isinstance(self.seed, int):
+            raise ValueError("seed must be an int")
+        return self
+
 
 MAX_TOP_K = 1024  # candidates of the top-k kernel; top_k = 0 or > MAX_TOP_K draws from the whole vocabulary
 

@@ -42,7 +42,8 @@ def _params(p: dict) -> SamplingParams:
     return SamplingParams(max_tokens=int(p.get("max_tokens", 64)), temperature=float(p.get("temperature", 0.0)),
                           top_k=int(p.get("top_k", 0)), top_p=float(p.get("top_p", 1.0)),
                           ignore_eos=bool(p.get("ignore_eos", False)),
-                          stop_token_ids=list(p.get("stop_token_ids", [])))
+                          stop_token_ids=list(p.get("stop_token_ids", [])),
+                          seed=None if p.get("seed") is None else int(p["seed"]))
 
 
 def make_app(backend, metrics, version: str = "1", inject_latency_s: float | None = None,
@@ -65,7 +66,10 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
                     await asyncio.sleep(lat)
                 if err_rate and random.random() < err_rate:
                     raise web.HTTPInternalServerError(text="injected failure")
-            resp = await handler(request)
+            try:
+                resp = await handler(request)
+            except ValueError as e:  # a request the engine refuses (engine.check_request): the client's error
+                raise web.HTTPBadRequest(text=str(e)) from None
             code = resp.status
             return resp
         except web.HTTPException as e:
@@ -126,7 +130,7 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
             raise web.HTTPBadRequest(text="generate is only served by LLM predictors")
         body = await req.json()
         params = _params(body.get("parameters", body))
-        ids = body.get("input_ids") or backend.tokenizer.encode(body.get("text_input", ""))
+        ids = body["input_ids"] if "input_ids" in body else backend.tokenizer.encode(body.get("text_input", ""))
         res = await backend.generate(ids, params)
         return web.json_response({"model_name": backend.name, "model_version": version,
                                   "text_output": backend.tokenizer.decode(res["output_ids"]),
@@ -140,7 +144,7 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
             raise web.HTTPBadRequest(text="generate_stream is only served by LLM predictors")
         body = await req.json()
         params = _params(body.get("parameters", body))
-        ids = body.get("input_ids") or backend.tokenizer.encode(body.get("text_input", ""))
+        ids = body["input_ids"] if "input_ids" in body else backend.tokenizer.encode(body.get("text_input", ""))
         r = backend.submit(ids, params, stream=True)
         resp = web.StreamResponse(headers={"Content-Type": "text/event-stream"})
         await resp.prepare(req)

@@ -72,6 +72,18 @@ def test_operator_deploys_ep2_predictor_matching_ep1(tmp_path):
                     out[name] = [await gen(name, ids) for ids in prompts]
                 # concurrent: the EP front spreads them over both ranks' engines
                 out["ep2_conc"] = list(await asyncio.gather(*(gen("ep2", ids) for ids in prompts)))
+                # bad requests fail alone (400, validated on rank 0 before any rank sees them) and
+                # the group keeps serving: empty, longer than max_model_len, out-of-vocab, bad params
+                bad = [({"input_ids": [], "parameters": {"max_tokens": 2}}),
+                       ({"input_ids": [5] * 300, "parameters": {"max_tokens": 2}}),
+                       ({"input_ids": [10 ** 9], "parameters": {"max_tokens": 2}}),
+                       ({"input_ids": [5, 6], "parameters": {"max_tokens": 2, "top_p": 0}})]
+                codes = []
+                for body in bad:
+                    async with s.post(pods["ep2"].endpoint + "/v2/models/moe/generate", json=body) as r:
+                        codes.append(r.status)
+                out["bad_codes"] = codes
+                out["after_bad"] = [await gen("ep2", ids) for ids in prompts[:2]]
                 async with s.get(pods["ep2"].endpoint + "/metrics") as r:
                     txt = await r.text()
             return out, txt
@@ -82,5 +94,7 @@ def test_operator_deploys_ep2_predictor_matching_ep1(tmp_path):
     out, txt = asyncio.run(asyncio.wait_for(go(), 300))
     assert out["ep2"] == out["ep1"]
     assert out["ep2_conc"] == out["ep1"]
+    assert out["bad_codes"] == [400, 400, 400, 400], out["bad_codes"]
+    assert out["after_bad"] == out["ep1"][:2]
     assert all(len(o) == 6 for o in out["ep1"])
     assert "mlop_engine_steps_total{" in txt
