@@ -18,6 +18,7 @@ import torch
 
 from .. import ops
 from ..parallel.comm import ParallelState, single
+from ..parallel.overlap import row_parallel_add_norm
 from .config import ModelConfig
 from .layers import init_norm, init_weight, linear, rope_table
 
@@ -213,13 +214,17 @@ class LlamaModel:
             if tp.size == 1:
                 x = self.attn_out_mlp(i, a.view(a.shape[0], -1), residual, nxt, eps)
                 continue
-            o = linear(a.view(a.shape[0], -1), L["o"])
-            tp.all_reduce(o)
-            x = ops.add_rmsnorm(o, residual, L["post_norm"], eps)
-            m = self.mlp(i, x)
-            tp.all_reduce(m)
-            x = ops.add_rmsnorm(m, residual, nxt, eps)
+            # row-parallel O / down: the all-reduce + add + RMSNorm of row chunk i run on the
+            # communication stream under the GEMM of chunk i+1 (parallel/overlap.py)
+            x = row_parallel_add_norm(a.view(a.shape[0], -1), L["o"], tp, residual, L["post_norm"], eps)
+            x = self.mlp_row_parallel(i, x, residual, nxt, eps)
         return x
+
+    def mlp_row_parallel(self, i, x, residual, next_norm, eps):
+        """TP > 1: gate_up (column-parallel, SiLU-mul fused), then the row-parallel down
+        projection with its all-reduce overlapped, + the next residual add / norm."""
+        act = ops.gemm(x, self.layers[i]["gate_up"], epi=ops.EPI_SILU_MUL)
+        return row_parallel_add_norm(act, self.layers[i]["down"], self.ps.tp, residual, next_norm, eps)
 
     # --------------------------------------------------------- norm chain --
     def _chain_ok(self, M: int) -> bool:

@@ -57,6 +57,13 @@ class MixtralModel(LlamaModel):
                            self.expert_start, self.n_local_experts, mode=mode,
                            cap_tokens=max(cap or 0, x.shape[0]))
 
+    def mlp_row_parallel(self, i, x, residual, next_norm, eps):
+        """TP > 1 (experts sharded over the TP ranks): each rank's partial MoE output, summed by
+        the TP all-reduce, then the next residual add / norm."""
+        m = self.mlp(i, x)
+        self.ps.tp.all_reduce(m)
+        return ops.add_rmsnorm(m, residual, next_norm, eps)
+
     def post_attention(self, i, o, residual, eps):
         """MoE block in the decode forward: the router / grouped GEMM take a normed x."""
         x = ops.add_rmsnorm(o, residual, self.layers[i]["post_norm"], eps)

@@ -99,6 +99,9 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     if not x.is_cuda:
         y, r = ref.add_rmsnorm(x, residual, w, eps)
         residual.copy_(r)
+        if out is not None:
+            out.copy_(y)
+            return out
         return y
     _need_gpu()
     out = torch.empty_like(x) if out is None else out

@@ -51,7 +51,8 @@ constexpr int kMaxRanks = 8;
 constexpr int kBlocks = 64;
 constexpr int kThreads = 512;
 constexpr int kFlagStride = 16;  // u32 per flag slot: one 64-B line per (source rank, block)
-constexpr size_t kFlagsBytes = (size_t)kMaxRanks * kBlocks * kFlagStride * 4;
+constexpr size_t kFlagBank = (size_t)kMaxRanks * kBlocks * kFlagStride * 4;
+constexpr size_t kFlagsBytes = 2 * kFlagBank;  // bank 0: one-shot + two-shot phase 1; bank 1: two-shot phase 2
 constexpr long kMaxSpins = 1L << 26;
 
 struct Peers {
@@ -153,6 +154,124 @@ __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restr
   if (tid == 0) epochs[b] = e;
 }
 
+// Two-shot form for large messages (tensor-parallel prefill chunks; one-shot would read (N-1) x
+// the message over the fabric per rank): reduce-scatter then all-gather, each ONE hop over the
+// full xGMI mesh, so a rank moves 2 (N-1) / N x the message -- the ring's volume -- but over all
+// N-1 links at once and in 2 steps instead of 2 (N-1).
+//   data[parity] = | input copy (n16 x 16 B) | reduced (n16 x 16 B, only this rank's slice) |
+//   phase 1: block b publishes its piece of the input copy (all slices), flag (rank, b, phase 1)
+//            at every peer; then for THIS rank's slice piece b: wait for every peer's phase-1
+//            flag b, sum the N copies in rank order (fp32), store bf16 into reduced (own buffer)
+//            AND into out; flag (rank, b, phase 2) at every peer;
+//   phase 2: for every other slice p: wait for peer p's phase-2 flag b, copy its reduced piece b
+//            into out.
+// Every rank's result is bitwise the same (the sum of slice p is computed by rank p only).
+// In place (out == in) is safe: block b reads every input element it owns (1a, 1b) before it
+// writes that element (1b: the same thread, same index; 2: after the phase-1 barriers).
+// Phase-2 flags live in the second flag bank (the first is shared with the one-shot kernel: both
+// advance the same per-block epochs, so a slot always holds the latest epoch it was raised at).
+template <int NR>
+__global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restrict__ out,
+                                                               const uint16_t* __restrict__ in, long n16,
+                                                               Peers peers, int rank, uint32_t* epochs, int* err,
+                                                               size_t max_bytes) {
+  __shared__ uint32_t s_e;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) s_e = epochs[b] + 1;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t half = max_bytes / 2;  // input copy | reduced, per parity
+  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* o = reinterpret_cast<uint4*>(out);
+  // slices: rank p owns [p * sl, min(n16, (p + 1) * sl)); block b its piece of every slice
+  const long sl = (n16 + NR - 1) / NR;
+  const long per = (sl + kBlocks - 1) / kBlocks;
+  auto piece = [&](int p, long& lo, long& hi) {
+    const long s0 = min(n16, (long)p * sl), s1 = min(n16, s0 + sl);
+    lo = min(s1, s0 + (long)b * per);
+    hi = min(s1, lo + per);
+  };
+  auto flag = [&](int owner, int src_rank, int phase) {
+    return reinterpret_cast<uint32_t*>(peers.base[owner]) + (size_t)phase * (kFlagBank / 4) +
+           (size_t)(src_rank * kBlocks + b) * kFlagStride;
+  };
+  auto wait = [&](int p, int phase) {
+    const uint32_t* f = flag(rank, p, phase);
+    long spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++spins > kMaxSpins) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  };
+  auto signal = [&](int phase) {  // after this block's stores: release, then flag at every peer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < NR; ++p) __hip_atomic_store(flag(p, rank, phase), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+  // 1a. publish piece b of every slice of the input
+  uint4* mine_in = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    long lo, hi;
+    piece(p, lo, hi);
+    for (long i = lo + tid; i < hi; i += kThreads) mine_in[i] = src[i];
+  }
+  signal(0);
+  // 1b. reduce my slice's piece b over the N copies, in rank order
+  if (tid < 64) {
+    if (tid < NR) wait(tid, 0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  {
+    long lo, hi;
+    piece(rank, lo, hi);
+    uint4* red = reinterpret_cast<uint4*>(peers.base[rank] + doff + half);
+    for (long i = lo + tid; i < hi; i += kThreads) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < NR; ++p) {
+        const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.base[p] + doff)[i];
+        add_bf16x8(acc, v);
+      }
+      uint4 r;
+      r.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
+      r.y = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
+      r.z = (uint32_t)f2bf(acc[4]) | ((uint32_t)f2bf(acc[5]) << 16);
+      r.w = (uint32_t)f2bf(acc[6]) | ((uint32_t)f2bf(acc[7]) << 16);
+      red[i] = r;
+      o[i] = r;
+    }
+  }
+  signal(1);
+  // 2. gather the other ranks' reduced pieces b
+  if (tid < 64) {
+    if (tid < NR && tid != rank) wait(tid, 1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    if (p == rank) continue;
+    long lo, hi;
+    piece(p, lo, hi);
+    const uint4* red = reinterpret_cast<const uint4*>(peers.base[p] + doff + half);
+    for (long i = lo + tid; i < hi; i += kThreads) o[i] = red[i];
+  }
+  if (tid == 0) epochs[b] = e;
+}
+
 CarState* get(long h) {
   if (h == 0) throw std::runtime_error("custom all-reduce: null handle");
   return reinterpret_cast<CarState*>(h);
@@ -212,16 +331,28 @@ long car_max_bytes(long h) { return (long)get(h)->max_bytes; }
 
 int car_mem_mode(long h) { return get(h)->uncached; }
 
-void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st) {
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot) {
   CarState* s = get(h);
   if (numel % 8) throw std::runtime_error("custom all-reduce: numel must be a multiple of 8");
-  if ((size_t)numel * 2 > s->max_bytes) throw std::runtime_error("custom all-reduce: message too large");
+  if ((size_t)numel * 2 * (two_shot ? 2 : 1) > s->max_bytes)
+    throw std::runtime_error("custom all-reduce: message too large");
   for (int p = 0; p < s->world; ++p)
     if (!s->peers.base[p]) throw std::runtime_error("custom all-reduce: peers not opened");
   const long n16 = numel / 8;
   dim3 g(kBlocks), blk(kThreads);
   auto* o = static_cast<uint16_t*>(out);
   auto* i = static_cast<const uint16_t*>(in);
+  if (two_shot) {
+    switch (s->world) {
+      case 1: car_twoshot_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+      case 2: car_twoshot_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+      case 4: car_twoshot_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+      case 8: car_twoshot_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+      default: throw std::runtime_error("custom all-reduce: world must be 1, 2, 4 or 8");
+    }
+    CAR_CHECK(hipGetLastError());
+    return;
+  }
   switch (s->world) {
     case 1: car_oneshot_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
     case 2: car_oneshot_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;

@@ -613,13 +613,14 @@ void car_open(int64_t h, Tensor handles) {
               handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
   mlop::car_open((long)h, handles.data_ptr());
 }
-void car_all_reduce(int64_t h, Tensor out, Tensor inp) {
+void car_all_reduce(int64_t h, Tensor out, Tensor inp, bool two_shot) {
   check_bf16(out, "out"); check_bf16(inp, "inp");
   TORCH_CHECK(out.numel() == inp.numel(), "all_reduce: out/inp size mismatch");
   TORCH_CHECK(inp.numel() % 8 == 0, "all_reduce: numel must be a multiple of 8");
-  TORCH_CHECK(inp.numel() * 2 <= mlop::car_max_bytes((long)h), "all_reduce: message exceeds the registered buffer");
+  TORCH_CHECK(inp.numel() * 2 * (two_shot ? 2 : 1) <= mlop::car_max_bytes((long)h),
+              "all_reduce: message exceeds the registered buffer");
   c10::DeviceGuard g(inp.device());
-  mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream());
+  mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream(), two_shot);
 }
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
@@ -677,7 +678,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_create(int rank, int world, int max_bytes, int device) -> int", &car_create);
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);
-  m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp) -> ()");
+  m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp, bool two_shot=False) -> ()");
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);

@@ -161,7 +161,7 @@ long car_create(int rank, int world, long max_bytes, int device);
 void car_ipc_handle(long h, void* out64);
 void car_open(long h, const void* handles);
 long car_max_bytes(long h);
-void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st);
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot = false);
 int car_error(long h);
 int car_mem_mode(long h);
 void car_destroy(long h);

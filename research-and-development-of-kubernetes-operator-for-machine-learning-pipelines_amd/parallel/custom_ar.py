@@ -20,7 +20,12 @@ import os
 import torch
 import torch.distributed as dist
 
-DEFAULT_MAX_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_MAX_BYTES", 4 << 20))
+# registered buffer per parity: one-shot messages up to this size, two-shot ones up to half of it
+# (tensor-parallel prefill chunks: 8192 x 4096 bf16 = 64 MiB at Llama-3-70B TP 8, chunked below)
+DEFAULT_MAX_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_MAX_BYTES", 64 << 20))
+# above this message size the two-shot kernel (reduce-scatter + all-gather, each one hop over the
+# full mesh: 2 (N-1)/N x the message per rank instead of the one-shot's N-1 x)
+TWO_SHOT_MIN_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_TWO_SHOT_MIN", 512 << 10))
 
 
 class CustomAllReduce:
@@ -44,13 +49,19 @@ class CustomAllReduce:
             dist.barrier(group=group)
 
     def eligible(self, x: torch.Tensor) -> bool:
-        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
-                and x.numel() % 8 == 0 and 2 * x.numel() <= self.max_bytes)
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0):
+            return False
+        n = 2 * x.numel()
+        return n <= self.max_bytes if n < TWO_SHOT_MIN_BYTES else 2 * n <= self.max_bytes
 
-    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Sum over ranks (rank order, fp32 accumulation: identical on every rank)."""
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None, two_shot: bool | None = None) -> torch.Tensor:
+        """Sum over ranks (rank order, fp32 accumulation: identical on every rank).  One-shot
+        below TWO_SHOT_MIN_BYTES, two-shot above (``two_shot`` forces either); in place when
+        ``out`` is None."""
         out = x if out is None else out
-        torch.ops.mlop.car_all_reduce(self.h, out, x)
+        if two_shot is None:
+            two_shot = 2 * x.numel() >= TWO_SHOT_MIN_BYTES
+        torch.ops.mlop.car_all_reduce(self.h, out, x, bool(two_shot))
         return out
 
     @property

@@ -5,6 +5,5 @@
 source scripts/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for spec in "$@"; do
-  # shellcheck disable=SC2086
-  step $spec
+  eval "step $spec"  # eval: quotes inside a spec group words ("-c 'import x; x.f()'")
 done

@@ -2,7 +2,9 @@
 share cuda:0 and map each other's buffers through HIP IPC, so the epoch-flag
 handshake, the parity double-buffering, in-place use and hipGraph capture are
 exercised exactly as across xGMI peers (the fabric path itself needs a
-multi-GPU node).  Oracle: fp32 sum in rank order of the known per-rank inputs,
+multi-GPU node).  Messages of 512 KiB and more take the two-shot kernel
+(reduce-scatter + all-gather over peer memory); small ones are also forced
+through it.  Oracle: fp32 sum in rank order of the known per-rank inputs,
 rounded once to bf16 — the kernel must match it bit for bit on every rank."""
 import os
 import socket
@@ -15,7 +17,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [8, 4096, 3 * 4096, 64 * 1024, 8000, 4096, 200 * 1024]
+SIZES = [8, 4096, 3 * 4096, 64 * 1024, 8000, 4096, 200 * 1024, 300 * 1024, 1 << 20, 1000 * 1024 + 8]
 
 
 def _free_port():
@@ -44,8 +46,8 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     from mlopamd.parallel.custom_ar import CustomAllReduce
 
-    car = CustomAllReduce(rank, world, torch.device("cuda", 0), group=None, max_bytes=1 << 20)
-    res = {"eager": [], "inplace": [], "graph": []}
+    car = CustomAllReduce(rank, world, torch.device("cuda", 0), group=None, max_bytes=8 << 20)
+    res = {"eager": [], "inplace": [], "graph": [], "two_shot": []}
     try:
         for it, n in enumerate(SIZES):
             xs = _inputs(it, n, world)
@@ -56,6 +58,17 @@ def _worker(rank, world, port, out_dir):
             car.all_reduce(x, out)
             torch.cuda.synchronize()
             res["eager"].append(torch.equal(out.cpu(), _oracle(xs)))
+        # two-shot forced at small / odd sizes (fewer 16-B units than ranks x blocks), in place
+        # and out of place, interleaved with one-shot calls (shared per-block epochs)
+        for it, n in enumerate([8, 24, 4096, 8000, 12288, 64 * 1024 + 8]):
+            xs = _inputs(200 + it, n, world)
+            x = xs[rank].cuda()
+            out = torch.empty_like(x)
+            car.all_reduce(x, out, two_shot=True)
+            y = xs[rank].cuda()
+            car.all_reduce(y, two_shot=it % 2 == 0)
+            torch.cuda.synchronize()
+            res["two_shot"].append(torch.equal(out.cpu(), _oracle(xs)) and torch.equal(y.cpu(), _oracle(xs)))
         # in place, back to back (parity reuse every second call)
         for it in range(6):
             xs = _inputs(50 + it, 4096, world)
@@ -72,7 +85,7 @@ def _worker(rank, world, port, out_dir):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
             car.all_reduce(static[0], outs[0])
-            car.all_reduce(static[1], outs[1])
+            car.all_reduce(static[1], outs[1], two_shot=True)
         dist.barrier()
         for it in range(4):
             xs0, xs1 = _inputs(80 + it, 8192, world), _inputs(90 + it, 8192, world)
@@ -107,3 +120,4 @@ def test_custom_all_reduce_two_processes_one_gpu():
         assert all(res["eager"]), (r, res["eager"])
         assert all(res["inplace"]), (r, res["inplace"])
         assert all(res["graph"]), (r, res["graph"])
+        assert all(res["two_shot"]), (r, res["two_shot"])

@@ -216,3 +216,43 @@ def test_ep_engine_matches_single_rank(fn, world):
     for r in res:
         assert r["ep"] == r["ref"]
     assert res[-1]["idle_steps"] > 0  # the idle rank joined every step's all-to-alls
+
+
+def _overlap_rowpar(rank, world):
+    """parallel/overlap.py: the chunked row-parallel projection (GEMM of chunk i+1 under the
+    all-reduce + add + RMSNorm of chunk i on GPU) == the unchunked GEMM -> all-reduce -> norm,
+    including a ragged last chunk, residual updated in place the same way (bit for bit at 2
+    ranks; at 4 gloo's ring segments by message size, so the fp32 sum order may differ)."""
+    from mlopamd import ops
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.parallel.overlap import chunks_of, row_parallel_add_norm
+
+    ps = make_parallel_state(tp_size=world)
+    g = torch.Generator().manual_seed(rank)
+    M, K, N = 700, 48, 64
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=torch.Generator().manual_seed(100 + rank))
+    res0 = torch.randn(M, N, generator=torch.Generator().manual_seed(7))  # same on every rank
+    nw = torch.rand(N, generator=torch.Generator().manual_seed(8)) + 0.5
+    r1, r2 = res0.clone(), res0.clone()
+    assert len(chunks_of(M, 256)) == 3
+    x1 = row_parallel_add_norm(a, w, ps.tp, r1, nw, 1e-5, chunk=256, min_rows=512)
+    o = ops.gemm(a, w)
+    ps.tp.all_reduce(o)
+    x2 = ops.add_rmsnorm(o, r2, nw, 1e-5)
+    return {"x": float((x1 - x2).abs().max()), "r": float((r1 - r2).abs().max())}
+
+
+def overlap2(rank, world):
+    return _overlap_rowpar(rank, world)
+
+
+def overlap4(rank, world):
+    return _overlap_rowpar(rank, world)
+
+
+@pytest.mark.parametrize("fn,world", [("overlap2", 2), ("overlap4", 4)])
+def test_chunked_row_parallel_matches_unchunked(fn, world):
+    for r in run_ranks(fn, world):
+        tol = 0.0 if world == 2 else 1e-4
+        assert r["x"] <= tol and r["r"] <= tol, r

@@ -66,6 +66,56 @@ def _worker(rank, world, port, out_dir, cfg_name):
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
 
 
+def _overlap_worker(rank, world, port, out_dir):
+    """parallel/overlap.py on the GPU path: chunked row-parallel GEMM with the K15 two-shot
+    all-reduce + add + RMSNorm of each chunk on the communication stream == the unchunked order,
+    bit for bit (both sum in rank order)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MLOP_CUSTOM_AR="force")
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mlopamd import ops
+    from mlopamd.parallel.comm import make_parallel_state
+    from mlopamd.parallel.overlap import row_parallel_add_norm
+
+    ps = make_parallel_state(tp_size=2)
+    dev = torch.device("cuda", 0)
+    res = {}
+    try:
+        M, K, N = 2600, 1024, 2048
+        g = torch.Generator(device=dev).manual_seed(rank)
+        a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        w = (0.05 * torch.randn(N, K, device=dev, generator=g)).to(torch.bfloat16)
+        gr = torch.Generator(device=dev).manual_seed(9)
+        res0 = torch.randn(M, N, device=dev, generator=gr).to(torch.bfloat16)
+        nw = (torch.rand(N, device=dev, generator=gr) + 0.5).to(torch.bfloat16)
+        r1, r2 = res0.clone(), res0.clone()
+        x1 = row_parallel_add_norm(a, w, ps.tp, r1, nw, 1e-5)  # 3 chunks, comm stream
+        o = ops.gemm(a, w)
+        ps.tp.all_reduce(o)
+        x2 = ops.add_rmsnorm(o, r2, nw, 1e-5)
+        torch.cuda.synchronize()
+        res["equal"] = bool(torch.equal(x1, x2) and torch.equal(r1, r2))
+        res["car_error"] = ps.tp.car.error()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        ps.tp.car.close()
+        dist.destroy_process_group()
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+
+
+def test_tp2_chunked_row_parallel_overlap_on_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = tempfile.mkdtemp()
+    mp.start_processes(_overlap_worker, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
+        assert res["car_error"] == 0 and res["equal"], (r, res)
+
+
 @pytest.mark.parametrize("cfg_name", ["tiny-llama"])
 def test_tp2_engine_on_gpu_with_custom_all_reduce(cfg_name):
     if not torch.cuda.is_available():
