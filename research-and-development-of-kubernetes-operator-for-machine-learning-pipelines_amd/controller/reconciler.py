@@ -125,24 +125,57 @@ class MlflowModelReconciler:
             cands.append({"node": n["metadata"]["name"], "gpus": int(alloc), "hbm_gb": hbm})
         if not cands:
             return {}
-        used = 0
-        try:
-            sds = await self.kube.list(SELDON_GROUP, SELDON_VERSION, None, SELDON_PLURAL)
-        except Exception:  # noqa: BLE001
-            sds = []
-        for sd in sds:
-            md = sd.get("metadata") or {}
-            if exclude and (md.get("namespace"), md.get("name")) == exclude:
-                continue
-            for p in (sd.get("spec") or {}).get("predictors", []):
-                used += int(p.get("replicas", 1)) * seldon.gpus_of(p, res)
-        # one node's view: the free GPUs are taken from the roomiest node (used GPUs are
-        # charged to it, a conservative single-node model of the scheduler)
-        best = max(cands, key=lambda c: c["gpus"])
-        out = {"node": best["node"], "gpus": best["gpus"], "free_gpus": max(0, best["gpus"] - used)}
+        # per-node accounting from the pods bound to each node (GPU limits of pods that still
+        # hold their devices); without pod access, the SeldonDeployments' total is charged to
+        # the cluster and the roomiest node reports min(its GPUs, the cluster's free GPUs)
+        per_node = await self._gpus_used_per_node(res)
+        if per_node is not None:
+            for c in cands:
+                c["free"] = max(0, c["gpus"] - per_node.get(c["node"], 0))
+            best = max(cands, key=lambda c: (c["free"], c["gpus"]))
+            out = {"node": best["node"], "gpus": best["gpus"], "free_gpus": best["free"], "accounting": "per-node"}
+        else:
+            used = 0
+            try:
+                sds = await self.kube.list(SELDON_GROUP, SELDON_VERSION, None, SELDON_PLURAL)
+            except Exception:  # noqa: BLE001
+                sds = []
+            for sd in sds:
+                md = sd.get("metadata") or {}
+                if exclude and (md.get("namespace"), md.get("name")) == exclude:
+                    continue
+                for p in (sd.get("spec") or {}).get("predictors", []):
+                    used += int(p.get("replicas", 1)) * seldon.gpus_of(p, res)
+            best = max(cands, key=lambda c: c["gpus"])
+            cluster_free = max(0, sum(c["gpus"] for c in cands) - used)
+            out = {"node": best["node"], "gpus": best["gpus"], "free_gpus": min(best["gpus"], cluster_free),
+                   "accounting": "cluster (pods not listable: requests charged cluster-wide)"}
         if best["hbm_gb"]:
             out["hbm_gb"] = best["hbm_gb"]
         return out
+
+    async def _gpus_used_per_node(self, res: str) -> dict | None:
+        """{node: GPUs requested by the pods bound to it and not finished}, or None when pods
+        cannot be listed (no RBAC / no pod API in this cluster emulation)."""
+        try:
+            pods = await self.kube.list("", "v1", None, "pods")
+        except Exception:  # noqa: BLE001
+            return None
+        if not pods:
+            return None
+        used: dict = {}
+        for pod in pods:
+            spec, st = pod.get("spec") or {}, pod.get("status") or {}
+            node = spec.get("nodeName")
+            if not node or st.get("phase") in ("Succeeded", "Failed"):
+                continue
+            n = 0
+            for c in spec.get("containers") or []:
+                lim = ((c.get("resources") or {}).get("limits") or {}).get(res)
+                if lim:
+                    n += int(lim)
+            used[node] = used.get(node, 0) + n
+        return used
 
     # --------------------------------------------------------- desired --
     async def _uri(self, spec: ModelSpec, version) -> tuple[str, object]:
@@ -185,7 +218,8 @@ class MlflowModelReconciler:
                              "gpus": p.gpus, "weightGBPerGPU": p.weightGBPerGPU,
                              "kvTokenCapacity": p.kvTokenCapacity, "fits": p.fits}
                 if not p.fits:
-                    placement["reason"] = p.reason
+                    placement["reason"] = p.reason + (f" [GPU accounting: {node['accounting']}]"
+                                                      if node.get("accounting") else "")
                 if node.get("node"):
                     placement["node"] = node["node"]
                 if node.get("free_gpus") is not None:  # the canary's second predictor needs its own

@@ -155,10 +155,16 @@ def shares_from_events(events) -> dict:
 
 
 class KernelTimeSampler:
-    """In-process kernel-time shares: every ``period_s`` the serving loop wraps ONE engine step
-    in ``torch.profiler`` (HIP activity) and publishes the per-class device-time shares.  One
-    profiled step per period keeps the overhead to that step; the shares of a mixed / decode
-    step are what a rocprof window of the pod would show."""
+    """In-process kernel-time shares: every ``period_s`` the serving loop opens a ``torch.profiler``
+    window (HIP activity) at one engine step and publishes the per-class device-time shares; the
+    shares of a mixed / decode step are what a rocprof window of the pod would show (SURVEY.md
+    §2.5 G3).
+
+    Off the critical path: nothing ever waits for the device.  The profiled step gets an event
+    after its launch; the window closes at the first later step boundary where that event has
+    completed (``Event.query()``, non-blocking).  Under one-step-ahead scheduling that is the
+    next step (the engine has read its tokens), so the window covers the profiled step plus at
+    most the step queued behind it -- shares, not absolute times, are published."""
 
     def __init__(self, period_s: float | None = None, on_shares=None):
         self.period_s = float(os.environ.get("MLOP_KERNEL_SAMPLE_S", 30.0) if period_s is None else period_s)
@@ -166,6 +172,8 @@ class KernelTimeSampler:
         self.last: dict = {}
         self._next = 0.0
         self._prof = None
+        self._done_ev = None
+        self.windows = 0
 
     def before_step(self, now: float) -> None:
         if self.period_s <= 0 or now < self._next or self._prof is not None:
@@ -182,12 +190,18 @@ class KernelTimeSampler:
             return None
         import torch
 
-        torch.cuda.synchronize()
+        if self._done_ev is None:  # the profiled step was just launched: mark its end
+            self._done_ev = torch.cuda.Event()
+            self._done_ev.record()
+            return None
+        if not self._done_ev.query():  # still running: look again after the next step
+            return None
         self._prof.__exit__(None, None, None)
         ev = [(e.key, float(getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)))
               for e in self._prof.key_averages()]
-        self._prof = None
+        self._prof, self._done_ev = None, None
         self._next = now + self.period_s
+        self.windows += 1
         shares = shares_from_events(ev)
         if shares:
             self.last = shares

@@ -494,6 +494,37 @@ def test_placement_reads_node_capacity():
     run(go())
 
 
+def _gpu_pod(name, node, gpus, phase="Running"):
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name, "namespace": "team"},
+            "spec": {"nodeName": node, "containers": [{"name": "c", "resources": {"limits": {"amd.com/gpu": str(gpus)}}}]},
+            "status": {"phase": phase}}
+
+
+def test_placement_charges_gpus_per_node():
+    """Two 8-GPU nodes: pods bound to node A hold 6 of its GPUs, node B has a finished pod only.
+    Per-node accounting (pods' nodeName) picks node B with 8 free, so a TP=8 70B predictor fits;
+    the old single-node model charged every request to one node."""
+    async def go():
+        env = Env()
+        await env.kube.create("", "v1", None, "nodes", _gpu_node("node-a", 8))
+        await env.kube.create("", "v1", None, "nodes", _gpu_node("node-b", 8))
+        await env.kube.create("", "v1", "team", "pods", _gpu_pod("p1", "node-a", 4))
+        await env.kube.create("", "v1", "team", "pods", _gpu_pod("p2", "node-a", 2))
+        await env.kube.create("", "v1", "team", "pods", _gpu_pod("p3", "node-b", 8, phase="Succeeded"))
+        v = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v)
+        await env.start()
+        cap = await env.rec.node_capacity()
+        assert cap["node"] == "node-b" and cap["free_gpus"] == 8 and cap["accounting"] == "per-node", cap
+        await env.create_cr(tensorParallel=8, maxModelLen=8192, maxNumSeqs=128)
+        assert await env.run_until(lambda: _ready(env))
+        (p,) = (await env.sd())["spec"]["predictors"]
+        ann = p["annotations"]
+        assert ann["mlop.amd.com/fits"] == "True" and ann["mlop.amd.com/node"] == "node-b", ann
+        await env.stop()
+    run(go())
+
+
 def test_placement_uses_node_vram_label():
     from mlopamd.controller import placement
 

@@ -128,7 +128,14 @@ def test_kernel_time_sampler_on_engine_steps(gpu, graphs):
     s = KernelTimeSampler(period_s=1e-6, on_shares=got.append)
     s.before_step(0.0)
     eng.step()
-    sh = s.after_step(1.0)
-    assert got and sh == got[0], sh
+    assert s.after_step(1.0) is None  # never waits for the device: the window stays open
+    sh = None
+    for k in range(50):  # closes at the first step boundary after the profiled step completed
+        s.before_step(2.0 + k)
+        eng.step()
+        sh = s.after_step(2.0 + k)
+        if sh is not None:
+            break
+    assert got and sh == got[0] and s.windows == 1, sh
     assert abs(sum(sh.values()) - 1.0) < 1e-6
     assert sh.get("gemm", 0) > 0 and sh.get("attention", 0) > 0, sh
