@@ -78,6 +78,15 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree per replica (config 4: --model llama3-70b --tp 8); "
                          "replicas = world / tp, each TP group's rank 0 schedules")
+    ap.add_argument("--ep", type=int, default=1,
+                    help="expert-parallel degree (config 5: --model mixtral-8x7b --ep N): N data-parallel "
+                         "attention engines, each rank serving its own --batch requests, every MoE layer an "
+                         "expert exchange over IPC peer memory (parallel/ep_ipc.py); replicas = world / ep")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on cuda:0 (gloo process group; RCCL cannot put two ranks on one GPU): "
+                         "rehearses the multi-rank paths (EP exchange, TP K15 all-reduce) on a one-GPU box")
+    ap.add_argument("--kv-gb", type=float, default=None,
+                    help="KV-cache pool per rank in GB (default: sized from free HBM; set it with --share-gpu)")
     ap.add_argument("--http", action="store_true",
                     help="drive the load through the deployed stack instead: operator + ProcessLauncher "
                          "(a fresh predictor process: CR->ready includes its start-up) + V2 HTTP + Router "
@@ -129,7 +138,7 @@ def launch(a, argv) -> int:
 
     n = a.gpus
     ngpu = _gpu_count()
-    if ngpu and ngpu < n:
+    if ngpu and ngpu < n and not a.share_gpu:
         raise SystemExit(f"--gpus {n}: only {ngpu} GPUs visible")
     extra = {}
     if a.cr_ready_samples > 0 and not a.no_operator:
@@ -193,8 +202,8 @@ def main(argv=None):
         else:  # before this process makes its first HIP call (the probe's predictor uses this GPU)
             proc_ready = _process_ready(a, local_rank if _gpu_count() else None)
     if world > 1:
-        init_distributed()
-    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+        init_distributed(backend="gloo" if a.share_gpu else None)
+    dev = torch.device("cuda", 0 if a.share_gpu else local_rank) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
 
@@ -205,9 +214,26 @@ def main(argv=None):
                prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
                mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk,
                enable_prefix_caching=not a.no_prefix_cache, async_scheduling=not a.no_async)
+    if a.kv_gb:
+        ekw["kv_cache_bytes"] = int(a.kv_gb * 2**30)
+    if a.share_gpu:
+        os.environ.setdefault("MLOP_CUSTOM_AR", "force")  # K15 over the gloo group (same-GPU IPC)
     t0 = time.perf_counter()
     leader = True
-    if a.tp > 1:
+    if a.ep > 1:
+        assert a.tp == 1, "--ep with --tp: TP shards the experts itself"
+        assert world % a.ep == 0, f"world {world} not divisible by --ep {a.ep}"
+        from mlopamd.runtime.tp_worker import build_tp_engine
+
+        engine, ps = build_tp_engine(a.model, 1, device=dev, seed=a.seed, engine_kwargs=ekw, ep=a.ep)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        ready_s = time.perf_counter() - t0
+        deploy_info = {"path": "direct-ep", "ep": a.ep, "replicas": world // a.ep,
+                       "weight_gb_per_gpu": round(engine.model.weight_bytes() / 1e9, 2),
+                       "kv_blocks": engine.kv.num_blocks,
+                       "exchange": "ipc" if getattr(ps.ep, "ex", None) is not None else "all_to_all"}
+    elif a.tp > 1:
         assert world % a.tp == 0, f"world {world} not divisible by --tp {a.tp}"
         os.environ.setdefault("MLOP_TP_GRAPHS", "1")  # the one-shot all-reduce is graph-capturable
         from mlopamd.runtime.tp_worker import build_tp_engine
@@ -268,8 +294,15 @@ def main(argv=None):
     ramp_cap = 4 * (a.batch * P) // max(1, a.max_batched_tokens) + 64
     ramp = 0
     backlog = max(a.prefill_min_batch, 2 * a.batch // max(1, O))  # ~2 steps of arrivals
-    while a.ramp and ramp < ramp_cap and (engine.stats["prefill_tokens"] < a.batch * P
-                                          or len(engine.waiting) > backlog):
+    def ramp_more() -> bool:
+        more = ramp < ramp_cap and (engine.stats["prefill_tokens"] < a.batch * P or len(engine.waiting) > backlog)
+        if a.ep > 1:  # EP ranks step in lock-step: continue while ANY rank still ramps
+            t = torch.tensor([int(more)], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=engine.model.ps.ep_cpu)
+            more = bool(t.item())
+        return more
+
+    while a.ramp and ramp_more():
         run_steps(1)
         ramp += 1
     deploy_info["ramp_steps"] = ramp
@@ -343,7 +376,9 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
             "config": {"model": "Llama-3-8B" if a.model == "llama3-8b" else a.model,
                        "global_batch": a.batch * (world // a.tp), "seq_len": a.prompt_len + a.output_len,
                        "prompt_len": a.prompt_len, "output_len": a.output_len,
-                       "parallelism": f"dp{world // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else ""),
+                       "parallelism": (f"dp{world // a.tp}" + (f"-tp{a.tp}" if a.tp > 1 else "")
+                                       + (f"-ep{a.ep}" if a.ep > 1 else "")),
+                       "shared_gpu": a.share_gpu,
                        "graphs": not a.no_graphs, "mixed_prefill": not a.no_mixed,
                        "async_scheduling": not a.no_async,
                        "prefill_min_batch": a.prefill_min_batch, "max_decode_gap": a.max_decode_gap,

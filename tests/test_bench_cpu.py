@@ -73,6 +73,16 @@ def test_bench_self_launches_tp_group():
     assert d["dist"]["world_size"] == 2 and d["dist"]["launcher"] == "bench.py"
 
 
+def test_bench_expert_parallel_mode():
+    """``bench.py --gpus 2 --ep 2 --model tiny-mixtral`` (config 5): two DP-attention engines in
+    lock-step, every MoE layer an expert exchange (gloo all_to_all on CPU, the IPC exchange on
+    GPU); both ranks' tokens counted."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--ep", "2", "--model", "tiny-mixtral",
+              "--steps", "4", "--warmup", "2", "--batch", "8", "--cr-ready-samples", "0"])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2-ep2" and d["deploy"]["ep"] == 2
+    assert d["deploy"]["exchange"] == "all_to_all" and min(d["per_rank_tokens_per_sec"]) > 0
+
+
 def test_deploy_fails_fast_when_predictor_cannot_start():
     """A predictor whose start-up raises (here: a 1-page KV cache) fails the bench's
     operator deploy at once, not after the 900 s readiness timeout."""
