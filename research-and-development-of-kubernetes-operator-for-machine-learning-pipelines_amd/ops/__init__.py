@@ -377,7 +377,10 @@ def gemm_add_rmsnorm(x, w, residual, norm_w, eps: float):
         x2 = x2.contiguous()
     M, K = x2.shape
     N = w.shape[0]
-    nws = torch.ops.mlop.gemm_workspace(M, N, K, 0) if (K % 64 == 0 and N % 8 == 0) else 0
+    _sk_reserve(x.device)  # the GEMV epilogue form's grid ticket lives in the stream-K scratch
+    # decode sizes (M <= 4): the GEMV with the add + RMSNorm as its epilogue (grid ticket, one
+    # launch); larger M: the split-K reduce pass does them
+    nws = torch.ops.mlop.gemm_workspace(M, N, K, EPI_ADD_RMSNORM) if (K % 8 == 0 and N % 8 == 0) else 0
 
     def fused(res):
         ws = torch.empty(nws, dtype=torch.float32, device=x.device)

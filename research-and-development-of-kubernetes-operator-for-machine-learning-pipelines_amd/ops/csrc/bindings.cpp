@@ -222,6 +222,11 @@ bool gemm_sk_reserve() { return mlop::gemm_sk_reserve(); }
 int64_t gemm_sk_workgroups(int64_t M, int64_t N, int64_t K) { return mlop::gemm_sk_workgroups((int)M, (int)N, (int)K); }
 
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  if (epi == 2) {  // GEMM + residual add + RMSNorm: the GEMV epilogue form's partials, else split-K slabs
+    const long g = mlop::gemv_addnorm_ws_floats((int)M, (int)N, (int)K);
+    if (g > 0) return g;
+    return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, 0);
+  }
   return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, (int)epi);
 }
 

@@ -1230,7 +1230,8 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              const void* w, float eps, float* ws, long ws_floats, int M, int N,
                              int K, hipStream_t st) {
   if (M == 0) return true;
-  if (gemv_takes(M, N, K, EPI_NONE)) return false;  // GEMV + add_rmsnorm
+  if (gemv_takes(M, N, K, EPI_NONE))  // decode sizes: the GEMV's epilogue form (or false: GEMV + add_rmsnorm)
+    return launch_gemv_addnorm(A, lda, B, out, residual, w, eps, ws, ws_floats, M, N, K, st);
   int splits;
   const Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;

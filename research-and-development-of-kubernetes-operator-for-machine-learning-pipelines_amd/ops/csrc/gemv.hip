@@ -45,7 +45,7 @@ namespace mlop {
 
 namespace {
 
-enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3 };
+enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3, EPI_ADDNORM = 4 };
 constexpr int kHeadD = 128;
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
@@ -60,6 +60,18 @@ __device__ __forceinline__ float dot8(const u32x4& w, const u32x4& x, float c) {
   c = dot2(w.y, x.y, c);
   c = dot2(w.z, x.z, c);
   return dot2(w.w, x.w, c);
+}
+
+// acc[r][m] with runtime (r, m) and every index static (the array stays in registers)
+template <int R, int M>
+__device__ __forceinline__ float acc_pick(const float (&acc)[R][M], int r, int m) {
+  float v = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+    for (int mm = 0; mm < M; ++mm)
+      if (rr == r && mm == m) v = acc[rr][mm];
+  return v;
 }
 
 // grouped mode (MoE decode, K13 at <= 8 routed rows): rows of A sorted by expert, offsets[E+1]
@@ -206,7 +218,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       }
     }
     __syncthreads();
-    if (wv != 0) return;
+    if (EPI != EPI_ADDNORM && wv != 0) return;  // ADDNORM: every wave joins the grid ticket below
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       float t = 0.f;
@@ -261,6 +273,58 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         uint16_t* dst = re.v_cache + (((size_t)blk * re.Hkv + kh) * kHeadD + dd) * re.BS + off;
         dst[0] = f2bf(acc[0][m]);
         dst[re.BS] = f2bf(acc[1][m]);
+      }
+    }
+  } else if constexpr (EPI == EPI_ADDNORM) {
+    // Epilogue form of the decoder's residual add + RMSNorm (the norm AFTER this projection,
+    // fused into its launch): lane m*R + r owns output (m, set*R + r):
+    //   residual = bf16(residual + bf16(y)) in place; its square -> the set's row partial;
+    // every workgroup then takes a grid ticket, and the last one (its acquire after every other
+    // workgroup's release) sums the partials per row in a FIXED order (deterministic) and
+    // writes out = bf16(bf16(residual * rsqrt(mean + eps)) * w) for all M rows: norm.hip's
+    // rounding, one launch instead of two.  Writer waves: every wave (KW == 1: 4 sets per
+    // workgroup) or wave 0 (KW > 1: one set).
+    __shared__ float s_red[16];
+    __shared__ int s_last;
+    const bool wwave = KW == 1 || wv == 0;
+    const int nsets = N / R;
+    if (wwave) {
+      float sq = 0.f;
+      const int m = lane / R, r = lane % R;
+      if (lane < M * R) {
+        uint16_t* rp = np.res_out + (size_t)m * ldc + set * R + r;
+        const float rn = bf2f(f2bf(bf2f(*rp) + bf2f(f2bf(acc_pick(acc, r, m)))));
+        *rp = f2bf(rn);
+        sq = rn * rn;
+      }
+      // row partial of this set: lanes m*R .. m*R+R-1 (R <= 4, adjacent lanes)
+#pragma unroll
+      for (int o = 1; o < R; o <<= 1) sq += __shfl_xor(sq, o, 64);
+      if (lane < M * R && lane % R == 0) np.part[(size_t)set * M + lane / R] = sq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();  // agent-scope release of this workgroup's residual + partial stores
+      const int tk = atomicAdd(np.cnt, 1);
+      s_last = tk == (int)gridDim.x - 1;
+      if (s_last) atomicExch(np.cnt, 0);  // re-armed for the next launch (stream-ordered)
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: every workgroup's stores are visible
+    for (int m = 0; m < M; ++m) {
+      float t = 0.f;
+      for (int sidx = threadIdx.x; sidx < nsets; sidx += blockDim.x) t += __builtin_nontemporal_load(np.part + (size_t)sidx * M + m);
+      t = block_sum(t, s_red);
+      const float inv = rsqrtf(t / (float)N + np.eps);
+      for (int c = threadIdx.x * 8; c < N; c += blockDim.x * 8) {
+        const u32x4 rv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(np.res_out + (size_t)m * ldc + c));
+        const u32x4 wv8 = *reinterpret_cast<const u32x4*>(np.w + c);
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = pack2(bf2f(f2bf(lo_bf(rv[q]) * inv)) * lo_bf(wv8[q]), bf2f(f2bf(hi_bf(rv[q]) * inv)) * hi_bf(wv8[q]));
+        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + c) = o;
       }
     }
   } else {
@@ -420,6 +484,37 @@ void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offse
     default: break;
   }
 #undef MLOP_GG
+}
+
+// The epilogue form: residual add + RMSNorm fused into the projection that PRODUCES the
+// residual update (O, down), so the batch-1..4 decode step loses its 64 separate add_rmsnorm
+// launches (~4.7 us each, profiles/r01_decode_small_batch.md) for one small tail per launch.
+long gemv_addnorm_ws_floats(int M, int N, int K) {
+  // whole row sets in every wave of every workgroup (the grid ticket needs no early exits)
+  static const int on = env_int("MLOP_GEMV_ADDNORM", 1);
+  if (!on || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
+  return (long)(N / 2) * M;  // >= sets x M for either row-set size (R = 2 or 4)
+}
+
+bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
+                         float* ws, long ws_floats, int M, int N, int K, hipStream_t st) {
+  if (gemv_addnorm_ws_floats(M, N, K) == 0 || ws_floats < gemv_addnorm_ws_floats(M, N, K)) return false;
+  float* wsk = nullptr;
+  int* cnt = nullptr;
+  int cus = 0;
+  if (!gemm_sk_scratch(&wsk, &cnt, &cus)) return false;  // the ticket counter lives there
+  NormPro np{nullptr, nullptr, (uint16_t*)residual, (const uint16_t*)w, eps, ws, cnt};
+  const RopeEpi none{};
+  auto* a = (const uint16_t*)A;
+  auto* b = (const uint16_t*)B;
+  auto* o = (uint16_t*)out;
+  switch (M) {
+    case 1: run_gemv_m<1, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    case 2: run_gemv_m<2, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    case 3: run_gemv_m<3, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    default: run_gemv_m<4, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
+  }
+  return true;
 }
 
 // residual add + RMSNorm fused into the projection that consumes it (prologue NORM):

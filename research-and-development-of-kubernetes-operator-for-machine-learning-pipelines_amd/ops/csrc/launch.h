@@ -102,7 +102,15 @@ struct NormPro {
   uint16_t* res_out;
   const uint16_t* w;
   float eps;
+  float* part = nullptr;  // epilogue form (launch_gemv_addnorm): per-(set, row) partial sums of squares
+  int* cnt = nullptr;     // epilogue form: the grid ticket
 };
+// decode projection with the residual add + RMSNorm AFTER it in the same launch (gemv.hip
+// epilogue form, M <= 4): residual <- bf16(residual + bf16(A.B^T)); out <- rmsnorm(residual) * w.
+// ws: gemv_addnorm_ws_floats(M, N, K) floats; false = shape not on this path.
+long gemv_addnorm_ws_floats(int M, int N, int K);
+bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
+                         float* ws, long ws_floats, int M, int N, int K, hipStream_t st);
 bool gemv_norm_takes(int M, int N, int K, int epi);
 bool gemv_grouped_takes(int M, int N, int K, int epi);
 void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,

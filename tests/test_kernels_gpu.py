@@ -877,3 +877,42 @@ def test_norm_qkv_rope_fused(gpu, M, Hq, Hkv):
     close(q, q_ref, atol=3e-2, rtol=3e-2)
     close(kc, kr, atol=3e-2, rtol=3e-2)
     close(vc, vr, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (2, 4096, 14336), (3, 4096, 4096), (4, 8192, 1024),
+                                   (1, 1024, 4096)])
+def test_gemv_add_rmsnorm_epilogue(gpu, M, N, K):
+    """Decode sizes: residual add + RMSNorm as the GEMV's epilogue (grid ticket, the last
+    workgroup normalises): residual bit-equal to GEMV -> add_rmsnorm (same roundings), the normed
+    output vs the fp32 oracle, relaunch bit-identical (partials summed in a fixed order; the
+    ticket re-arms), and inside a captured graph."""
+    torch.manual_seed(M * N + K)
+    assert torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) > 0
+    x = torch.randn(M, K, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
+    res = torch.randn(M, N, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
+    y = ops.gemm(x, w)
+    r_ref = res.clone()
+    out_ref = ops.add_rmsnorm(y, r_ref, nw, 1e-5)
+    exp_out, _ = ref.add_rmsnorm((x.float() @ w.float().t()).to(bf), res, nw, 1e-5)
+    ops.GEMM_BACKEND = "mlop"
+    try:
+        r1, r2 = res.clone(), res.clone()
+        o1 = ops.gemm_add_rmsnorm(x, w, r1, nw, 1e-5)
+        o2 = ops.gemm_add_rmsnorm(x, w, r2, nw, 1e-5)
+        rg = res.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            og = ops.gemm_add_rmsnorm(x, w, rg, nw, 1e-5)
+        rg.copy_(res)
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
+    assert torch.equal(r1, r_ref) and torch.equal(r1, r2) and torch.equal(o1, o2)
+    assert torch.equal(rg, r1) and torch.equal(og, o1)
+    close(o1, out_ref, atol=1.6e-2, rtol=1e-2)  # the sum of squares' order differs from norm.hip's
+    close(o1, exp_out, atol=5e-2, rtol=3e-2)
