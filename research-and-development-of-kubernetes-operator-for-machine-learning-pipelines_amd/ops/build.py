@@ -53,7 +53,7 @@ def _torch_dirs():
 
 
 def _sources() -> list[Path]:
-    return sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.h"), *CSRC.glob("*.cpp")])
+    return sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.h"), *CSRC.glob("*.cpp"), *CSRC.glob("*.cc")])
 
 
 def source_hash() -> str:
@@ -106,6 +106,14 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
         stale, digest = _stale(obj, src, headers, cmd)
         if force or stale:
             jobs_list.append((cmd, obj, digest))
+    # host-only runtime sources (C++, no device code): csrc/*.cc
+    hosts = sorted(CSRC.glob("*.cc"))
+    for src in hosts:
+        obj = BUILD / (src.stem + ".o")
+        cmd = [hipcc, *common, "-x", "c++", "-c", str(src), "-o", str(obj)]
+        stale, digest = _stale(obj, src, headers, cmd)
+        if force or stale:
+            jobs_list.append((cmd, obj, digest))
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "bindings.o"
     py_inc = sysconfig.get_paths()["include"]
@@ -137,7 +145,7 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             for r in ex.map(run, jobs_list):
                 if verbose and (r.stdout or r.stderr):
                     print(r.stdout, r.stderr, file=sys.stderr)
-    objs = [BUILD / (s.stem + ".o") for s in kernels] + [bobj, hobj]
+    objs = [BUILD / (s.stem + ".o") for s in kernels] + [BUILD / (s.stem + ".o") for s in hosts] + [bobj, hobj]
     if force or jobs_list or not OUT.exists():
         tlib = troot / "lib"
         tmp = OUT.with_suffix(".so.tmp")

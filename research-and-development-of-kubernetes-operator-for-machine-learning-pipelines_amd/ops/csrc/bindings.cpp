@@ -631,6 +631,22 @@ int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
 
+// ---- TP step-header channel over POSIX shared memory (shm_channel.cc) -------------
+int64_t chan_create(std::string name, int64_t slots, int64_t consumers) {
+  return mlop::chan_create(name, (int)slots, (int)consumers);
+}
+int64_t chan_open(std::string name) { return mlop::chan_open(name); }
+bool chan_send(int64_t h, Tensor vals, int64_t timeout_us) {
+  TORCH_CHECK(!vals.is_cuda() && vals.scalar_type() == at::kLong && vals.is_contiguous(), "vals: CPU int64");
+  return mlop::chan_send((long)h, vals.data_ptr<int64_t>(), (int)vals.numel(), (long)timeout_us);
+}
+bool chan_recv(int64_t h, int64_t consumer, Tensor out, int64_t timeout_us) {
+  TORCH_CHECK(!out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous(), "out: CPU int64");
+  return mlop::chan_recv((long)h, (int)consumer, out.data_ptr<int64_t>(), (int)out.numel(), (long)timeout_us);
+}
+void chan_unlink(std::string name) { mlop::chan_unlink(name); }
+void chan_close(int64_t h, bool unlink) { mlop::chan_close((long)h, unlink); }
+
 // ---- expert-parallel exchange over IPC peer memory (ep_exchange.hip) -------------
 int64_t ep_create(int64_t rank, int64_t world, int64_t E, int64_t k, int64_t H, int64_t tcap, int64_t device) {
   return mlop::ep_create((int)rank, (int)world, (int)E, (int)k, (int)H, (int)tcap, (int)device);
@@ -687,6 +703,12 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
+  m.def("chan_create(str name, int slots, int consumers) -> int", &chan_create);
+  m.def("chan_open(str name) -> int", &chan_open);
+  m.def("chan_send(int h, Tensor vals, int timeout_us) -> bool", &chan_send);
+  m.def("chan_recv(int h, int consumer, Tensor(a!) out, int timeout_us) -> bool", &chan_recv);
+  m.def("chan_unlink(str name) -> ()", &chan_unlink);
+  m.def("chan_close(int h, bool unlink) -> ()", &chan_close);
   m.def("ep_create(int rank, int world, int E, int k, int H, int tcap, int device) -> int", &ep_create);
   m.def("ep_ipc_handle(int h) -> Tensor", &ep_ipc_handle);
   m.def("ep_open(int h, Tensor handles) -> ()", &ep_open);

@@ -1,6 +1,8 @@
 // Host-side launchers of the gfx950 kernels (raw pointers + stream; no torch
 // headers here so the .hip files compile quickly).  Bound to torch in bindings.cpp.
 #pragma once
+
+#include <string>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
@@ -173,6 +175,14 @@ void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t s
 int car_error(long h);
 int car_mem_mode(long h);
 void car_destroy(long h);
+
+// host-to-host step-header channel over POSIX shared memory (shm_channel.cc, host code)
+long chan_create(const std::string& name, int nslots, int nconsumers);
+long chan_open(const std::string& name);
+bool chan_send(long h, const int64_t* w, int n, long timeout_us);
+bool chan_recv(long h, int consumer, int64_t* w, int n, long timeout_us);
+void chan_unlink(const std::string& name);
+void chan_close(long h, bool unlink);
 
 // expert-parallel dispatch / combine over IPC peer memory (ep_exchange.hip)
 long ep_create(int rank, int world, int E, int k, int H, int tcap, int device);

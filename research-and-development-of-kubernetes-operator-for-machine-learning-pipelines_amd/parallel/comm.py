@@ -150,3 +150,58 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
         tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
                                  group=tp_handle)
     return ParallelState(tp=tp, ep=ep, ep_cpu=ep_cpu, tp_cpu=tp_cpu)
+
+
+class HostChannel:
+    """One-producer / N-consumer broadcast of small int64 messages between the processes of a
+    group on ONE node, over POSIX shared memory (``ops/csrc/shm_channel.cc``): the TP leader's
+    step header reaches the workers in about a microsecond instead of a gloo TCP broadcast.
+    Collective construction over ``cpu_group`` (the segment's name travels once); the name is
+    unlinked as soon as every rank mapped it, so a crash leaves nothing in /dev/shm."""
+
+    SLOTS = 64
+
+    def __init__(self, cpu_group, words: int = 16):
+        import uuid
+
+        from .. import ops
+
+        ops.load()
+        self.words = words
+        self.rank = dist.get_rank(cpu_group)
+        self.size = dist.get_world_size(cpu_group)
+        box = [f"/mlop-chan-{uuid.uuid4().hex[:16]}" if self.rank == 0 else None]
+        name = None
+        if self.rank == 0:
+            name = box[0]
+            self.h = torch.ops.mlop.chan_create(name, self.SLOTS, self.size - 1)
+        dist.broadcast_object_list(box, src=dist.get_global_rank(cpu_group, 0), group=cpu_group)
+        if self.rank != 0:
+            self.h = torch.ops.mlop.chan_open(box[0])
+        dist.barrier(group=cpu_group)
+        if self.rank == 0:
+            torch.ops.mlop.chan_unlink(name)
+        self._buf = torch.zeros(words, dtype=torch.int64)
+
+    def send(self, vals: torch.Tensor, timeout_s: float = 600.0) -> None:
+        import time
+
+        t0 = time.monotonic()
+        while not torch.ops.mlop.chan_send(self.h, vals, 20000):
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError("host channel: consumers stopped reading")
+
+    def recv(self, out: torch.Tensor, timeout_s: float = 3600.0) -> torch.Tensor:
+        """Blocks (20 ms slices, the GIL dropped in between) until the next message arrives."""
+        import time
+
+        t0 = time.monotonic()
+        while not torch.ops.mlop.chan_recv(self.h, self.rank - 1, out, 20000):
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError("host channel: no message from the producer")
+        return out
+
+    def close(self):
+        if getattr(self, "h", 0):
+            torch.ops.mlop.chan_close(self.h, False)
+            self.h = 0

@@ -61,15 +61,30 @@ class StepSync:
     NHDR = 9
 
     def __init__(self, group, cpu_group=None):
+        import os
+
         self.g = group
         self.cpu = cpu_group
         self.is_leader = group.rank == 0
         self.hdr = torch.zeros(self.NHDR, dtype=torch.int64)
+        # the header's host path: the native shared-memory channel (TP groups live on one node),
+        # gloo's broadcast as the fallback (MLOP_TP_HEADER=gloo, or the channel cannot be built)
+        self.chan = None
+        if cpu_group is not None and os.environ.get("MLOP_TP_HEADER", "shm") == "shm":
+            from ..parallel.comm import HostChannel
+
+            self.chan = HostChannel(cpu_group, words=self.NHDR)
 
     def _bcast_header(self):
         import torch.distributed as dist
 
         if self.cpu is None:  # no host group (single process): nothing to agree on
+            return
+        if self.chan is not None:
+            if self.is_leader:
+                self.chan.send(self.hdr)
+            else:
+                self.chan.recv(self.hdr)
             return
         dist.broadcast(self.hdr, src=dist.get_global_rank(self.cpu, 0), group=self.cpu)
 

@@ -256,3 +256,45 @@ def test_chunked_row_parallel_matches_unchunked(fn, world):
     for r in run_ranks(fn, world):
         tol = 0.0 if world == 2 else 1e-4
         assert r["x"] <= tol and r["r"] <= tol, r
+
+
+def _chan_stress(rank, world):
+    """parallel/comm.HostChannel (ops/csrc/shm_channel.cc): one producer, world-1 consumers,
+    far more messages than ring slots (back-pressure), every consumer sees every message in
+    order; the segment name is already unlinked once every rank mapped it."""
+    import glob
+
+    from mlopamd.parallel.comm import HostChannel
+
+    import torch.distributed as dist
+
+    cpu = dist.new_group(list(range(world)), backend="gloo")
+    ch = HostChannel(cpu, words=9)
+    dist.barrier(group=cpu)  # rank 0 unlinked the name right after the construction barrier
+    leftover = glob.glob("/dev/shm/mlop-chan-*")
+    n, got = 5000, []
+    v = torch.zeros(9, dtype=torch.int64)
+    for i in range(n):
+        if rank == 0:
+            v[:] = torch.arange(9, dtype=torch.int64) + 9 * i
+            ch.send(v)
+        else:
+            ch.recv(v)
+            got.append(int(v[0]) == 9 * i and int(v[8]) == 9 * i + 8)
+    ch.close()
+    return {"ok": all(got) if rank else True, "n": len(got), "leftover": leftover}
+
+
+def chan2(rank, world):
+    return _chan_stress(rank, world)
+
+
+def chan4(rank, world):
+    return _chan_stress(rank, world)
+
+
+@pytest.mark.parametrize("fn,world", [("chan2", 2), ("chan4", 4)])
+def test_host_channel_broadcast(fn, world):
+    res = run_ranks(fn, world)
+    assert all(r["ok"] for r in res) and all(r["n"] == 5000 for r in res[1:])
+    assert not any(r["leftover"] for r in res)
