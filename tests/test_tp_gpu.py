@@ -77,7 +77,7 @@ def _overlap_worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     from mlopamd import ops
     from mlopamd.parallel.comm import make_parallel_state
-    from mlopamd.parallel.overlap import row_parallel_add_norm
+    from mlopamd.parallel.overlap import chunks_of, row_parallel_add_norm
 
     ps = make_parallel_state(tp_size=2)
     dev = torch.device("cuda", 0)
@@ -92,7 +92,9 @@ def _overlap_worker(rank, world, port, out_dir):
         nw = (torch.rand(N, device=dev, generator=gr) + 0.5).to(torch.bfloat16)
         r1, r2 = res0.clone(), res0.clone()
         x1 = row_parallel_add_norm(a, w, ps.tp, r1, nw, 1e-5)  # 3 chunks, comm stream
-        o = ops.gemm(a, w)
+        # reference: the same per-chunk GEMMs (a GEMM's rounding may depend on the M it is
+        # planned for), then ONE all-reduce + norm over all rows on the compute stream
+        o = torch.cat([ops.gemm(a[lo:hi], w) for lo, hi in chunks_of(M)])
         ps.tp.all_reduce(o)
         x2 = ops.add_rmsnorm(o, r2, nw, 1e-5)
         torch.cuda.synchronize()
