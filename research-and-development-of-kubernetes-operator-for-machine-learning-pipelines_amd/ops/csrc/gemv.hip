@@ -278,47 +278,69 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   } else if constexpr (EPI == EPI_ADDNORM) {
     // Epilogue form of the decoder's residual add + RMSNorm (the norm AFTER this projection,
     // fused into its launch): lane m*R + r owns output (m, set*R + r):
-    //   residual = bf16(residual + bf16(y)) in place; its square -> the set's row partial;
-    // every workgroup then takes a grid ticket, and the last one (its acquire after every other
-    // workgroup's release) sums the partials per row in a FIXED order (deterministic) and
-    // writes out = bf16(bf16(residual * rsqrt(mean + eps)) * w) for all M rows: norm.hip's
-    // rounding, one launch instead of two.  Writer waves: every wave (KW == 1: 4 sets per
-    // workgroup) or wave 0 (KW > 1: one set).
+    //   residual = bf16(residual + bf16(y)) (in place: read by later launches only) and the same
+    //   values into a scratch copy, the set's row partial of squares into the partials;
+    // then the grid hand-off of MI355X_MICROARCH.md "Valid forms" table row 1 (no L2 write-back
+    // fence per workgroup: 2048 of them cost ~60 us per launch): every handed-off byte is stored
+    // sc1 (4- / 8-B scratch words, 4-B partials) into scratch no workgroup of this launch read
+    // before, every storing wave drains (vmcnt(0)), a barrier, ONE lane's relaxed agent-scope
+    // ticket; the workgroup whose add returned last loads the partials and the scratch residual
+    // with sc1 loads only, sums each row's partials in a FIXED order (deterministic) and writes
+    // out = bf16(bf16(residual * rsqrt(mean + eps)) * w) for all M rows (norm.hip's rounding).
+    // Writer waves: every wave (KW == 1: 4 sets per workgroup) or wave 0 (KW > 1: one set).
     __shared__ float s_red[16];
     __shared__ int s_last;
     const bool wwave = KW == 1 || wv == 0;
     const int nsets = N / R;
+    float* part = np.part;                               // [nsets, M] fp32
+    uint16_t* rsc = reinterpret_cast<uint16_t*>(np.part + (size_t)nsets * M);  // [M, N] bf16 copy
+    const auto rs_part = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)((uint32_t)nsets * M * 4u), 0x00020000);
+    const auto rs_rsc = __builtin_amdgcn_make_buffer_rsrc(rsc, 0, (int)((uint32_t)M * N * 2u), 0x00020000);
     if (wwave) {
       float sq = 0.f;
+      uint32_t rb = 0;
       const int m = lane / R, r = lane % R;
       if (lane < M * R) {
         uint16_t* rp = np.res_out + (size_t)m * ldc + set * R + r;
-        const float rn = bf2f(f2bf(bf2f(*rp) + bf2f(f2bf(acc_pick(acc, r, m)))));
-        *rp = f2bf(rn);
+        const uint16_t nb = f2bf(bf2f(*rp) + bf2f(f2bf(acc_pick(acc, r, m))));
+        *rp = nb;
+        const float rn = bf2f(nb);
         sq = rn * rn;
+        rb = nb;
       }
-      // row partial of this set: lanes m*R .. m*R+R-1 (R <= 4, adjacent lanes)
+      // the row's R adjacent values and their squares gather in lane m*R (R = 2 or 4, adjacent lanes)
 #pragma unroll
       for (int o = 1; o < R; o <<= 1) sq += __shfl_xor(sq, o, 64);
-      if (lane < M * R && lane % R == 0) np.part[(size_t)set * M + lane / R] = sq;
+      // every lane shuffles (no inactive source lanes), lane m*R stores
+      const uint32_t r1 = __shfl_down(rb, 1, 64);
+      const uint32_t r2 = R == 4 ? __shfl_down(rb, 2, 64) : 0u, r3 = R == 4 ? __shfl_down(rb, 3, 64) : 0u;
+      if (lane < M * R && r == 0) {
+        const uint32_t off = (uint32_t)(m * N + set * R) * 2u;
+        if constexpr (R == 2)
+          __builtin_amdgcn_raw_buffer_store_b32(rb | (r1 << 16), rs_rsc, off, 0, 16 /* sc1 */);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{rb | (r1 << 16), r2 | (r3 << 16)}, rs_rsc, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq), rs_part, (uint32_t)(set * M + m) * 4u, 0, 16);
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __threadfence();  // agent-scope release of this workgroup's residual + partial stores
-      const int tk = atomicAdd(np.cnt, 1);
+      const int tk = __hip_atomic_fetch_add(np.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = tk == (int)gridDim.x - 1;
-      if (s_last) atomicExch(np.cnt, 0);  // re-armed for the next launch (stream-ordered)
+      if (s_last) __hip_atomic_store(np.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: every workgroup's stores are visible
     for (int m = 0; m < M; ++m) {
       float t = 0.f;
-      for (int sidx = threadIdx.x; sidx < nsets; sidx += blockDim.x) t += __builtin_nontemporal_load(np.part + (size_t)sidx * M + m);
+      for (int sidx = threadIdx.x; sidx < nsets; sidx += blockDim.x)
+        t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_part, (uint32_t)(sidx * M + m) * 4u, 0, 16));
       t = block_sum(t, s_red);
       const float inv = rsqrtf(t / (float)N + np.eps);
       for (int c = threadIdx.x * 8; c < N; c += blockDim.x * 8) {
-        const u32x4 rv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(np.res_out + (size_t)m * ldc + c));
+        const u32x4 rv = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_rsc, (uint32_t)(m * N + c) * 2u, 0, 16 /* sc1 */));
         const u32x4 wv8 = *reinterpret_cast<const u32x4*>(np.w + c);
         u32x4 o;
 #pragma unroll
@@ -493,7 +515,7 @@ long gemv_addnorm_ws_floats(int M, int N, int K) {
   // whole row sets in every wave of every workgroup (the grid ticket needs no early exits)
   static const int on = env_int("MLOP_GEMV_ADDNORM", 1);
   if (!on || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
-  return (long)(N / 2) * M;  // >= sets x M for either row-set size (R = 2 or 4)
+  return (long)(N / 2) * M + (long)(N / 2) * M;  // partials (>= sets x M, R = 2 or 4) + the bf16 residual copy
 }
 
 bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
