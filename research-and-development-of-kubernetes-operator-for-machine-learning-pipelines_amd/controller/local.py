@@ -220,6 +220,7 @@ class ProcessLauncher:
                                                              delete=False)
         pod.extra["cmd"] = cmd = self.command(pod, port)
         pod.extra["t_start"] = time.perf_counter()
+        env["MLOP_LAUNCH_EPOCH"] = repr(time.time())  # the predictor reports its start-up phases against it
         pod.proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL,
                                     stderr=log_f, start_new_session=True)
         pod.endpoint = f"http://127.0.0.1:{port}"

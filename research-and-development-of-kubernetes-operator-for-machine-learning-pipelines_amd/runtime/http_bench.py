@@ -100,6 +100,14 @@ async def cr_ready_process(model: str = "llama3-8b", batch: int = 2048, engine_e
         try:
             last = await _create_and_wait_ready(kube, ctl, batch, ready_timeout_s)
             vals.append(last["cr_ready_process_s"])
+            try:  # the predictor's own start-up phases (runtime/server.py STARTUP)
+                import aiohttp
+
+                async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=5)) as s:
+                    async with s.get(last["pod"].endpoint + "/v2/debug/startup") as r:
+                        last["predictor_startup"] = await r.json()
+            except Exception:  # noqa: BLE001
+                pass
         finally:
             await ctl.stop()
             await op.stop()
@@ -108,7 +116,7 @@ async def cr_ready_process(model: str = "llama3-8b", batch: int = 2048, engine_e
     p50 = vals[n // 2] if n % 2 else 0.5 * (vals[n // 2 - 1] + vals[n // 2])
     return {"p50_cr_ready_process_s": round(p50, 3), "cr_ready_process_samples_s": vals,
             "predictor_process_ready_s": last.get("predictor_process_ready_s"),
-            "predictor_gpus": last.get("predictor_gpus")}
+            "predictor_gpus": last.get("predictor_gpus"), "predictor_startup": last.get("predictor_startup")}
 
 
 async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256, output_len: int = 256,

@@ -31,7 +31,31 @@ import time
 
 import numpy as np
 
-from .sampler import SamplingParams
+# start-up phases of this predictor process, seconds since the OS created it (GET /v2/debug/startup;
+# bench.py's fresh-process CR -> ready probe reports them): what the 2 s of a cold start go to
+STARTUP: dict = {}
+
+
+def _since_process_start() -> float:
+    """Seconds since the launcher started this process (MLOP_LAUNCH_EPOCH, its wall clock right
+    before the spawn: exact on one host), else since the kernel's process creation time (psutil:
+    clock-tick resolution on an integer-second boot time, so only differences are meaningful)."""
+    t0 = os.environ.get("MLOP_LAUNCH_EPOCH")
+    if t0:
+        return round(time.time() - float(t0), 3)
+    try:
+        import psutil
+
+        return round(time.time() - psutil.Process().create_time(), 3)
+    except Exception:  # noqa: BLE001
+        return -1.0
+
+
+STARTUP["server_module_imported_s"] = _since_process_start()
+
+from .sampler import SamplingParams  # noqa: E402 (imports torch: timed below)
+
+STARTUP["torch_imported_s"] = _since_process_start()
 
 _DT = {"FP32": np.float32, "FP64": np.float64, "INT64": np.int64, "INT32": np.int32, "FP16": np.float16,
        "BOOL": np.bool_, "UINT8": np.uint8}
@@ -199,6 +223,15 @@ def make_app(backend, metrics, version: str = "1", inject_latency_s: float | Non
     r.add_get("/metrics", prom)
     r.add_get("/v2/debug/trace", trace)            # Chrome / Perfetto trace of recent engine steps
     r.add_get("/v2/debug/steps", trace_summary)
+
+    async def startup(_):
+        return web.json_response(STARTUP)
+
+    async def on_start(_app):
+        STARTUP["http_listening_s"] = _since_process_start()
+
+    r.add_get("/v2/debug/startup", startup)
+    app.on_startup.append(on_start)
     return app
 
 
@@ -216,9 +249,12 @@ def build_backend(runtime: str, model_uri: str | None, architecture: str | None,
     import torch
 
     t0 = time.perf_counter()
+    STARTUP["engine_build_start_s"] = _since_process_start()
     dtype = {"float32": torch.float32, "bfloat16": torch.bfloat16}[os.environ.get("MLOP_DTYPE", "bfloat16")]
     eng = build_engine(architecture or "llama3-8b", device=device, seed=seed, tp_state=tp_state,
                        model_uri=model_uri, dtype=dtype, **(engine_kwargs or {}))
+    STARTUP["engine_built_s"] = _since_process_start()
+    STARTUP["engine"] = {k: int(eng.stats.get(k, 0)) for k in ("model_build_ms", "kv_alloc_ms", "graph_capture_ms")}
     from .. import ops
 
     # serving must never time GEMM candidates mid-request (a canary's latency would spike on
