@@ -326,9 +326,28 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int tk = __hip_atomic_fetch_add(np.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = tk == (int)gridDim.x - 1;
-      if (s_last) __hip_atomic_store(np.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      // two-level ticket: one counter serialises its adds (~10 ns each at the memory side, so
+      // 2048 workgroups on ONE counter cost ~20 us per launch); 16 shards on their own 32-B
+      // words take the adds in parallel and the last of each shard adds to the top counter.
+      // Every add follows its workgroup's drained sc1 stores, so whoever sees the final count
+      // sees every workgroup's bytes in memory.
+      constexpr int kShards = 16, kStride = 8;
+      const int G = gridDim.x, sh = blockIdx.x % kShards;
+      const int in_shard = (G - sh + kShards - 1) / kShards;  // workgroups of shard sh
+      const int nsh = G < kShards ? G : kShards;
+      int* sc = np.cnt + sh * kStride;
+      int* top = np.cnt + kShards * kStride;
+      int last = 0;
+      const int t1 = __hip_atomic_fetch_add(sc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t1 == in_shard - 1) {
+        __hip_atomic_store(sc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+        const int t2 = __hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t2 == nsh - 1) {
+          __hip_atomic_store(top, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = 1;
+        }
+      }
+      s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
@@ -389,7 +408,9 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
   const int pairs = N / 2;
   const int rp = (EPI != EPI_ROPE && pairs / 2 >= 2048) ? 2 : 1;
   const int sets = pairs / rp;
-  const bool kw4 = sets < gemv_kw4_sets(M);
+  // ADDNORM: one set per wave (4 per workgroup) keeps the grid ticket to N / 8 workgroups; the
+  // K-split form is for gate_up-size shards, o / down stream as fast without it (run56.sh)
+  const bool kw4 = EPI != EPI_ADDNORM && sets < gemv_kw4_sets(M);
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \

@@ -52,6 +52,14 @@ def row_parallel_add_norm(a: torch.Tensor, w: torch.Tensor, tp, residual: torch.
     chunk = CHUNK_ROWS if chunk is None else chunk
     min_rows = MIN_ROWS if min_rows is None else min_rows
     parts = [(0, M)]
+    if cuda:
+        # a chunk must still fill the chip: >= one 256 x 256 tile per CU (256 tiles), else its
+        # GEMM runs on part of the GPU and the overlap costs more than it hides (measured on one
+        # GPU, scripts/tp_overlap_trace.py: 1024-row chunks of a N = 8192 projection, 128 tiles
+        # each, 311 vs 196 us per call)
+        fill = (256 * 256 * 256 + N - 1) // N
+        chunk = max(chunk, (fill + 255) // 256 * 256)
+        min_rows = max(min_rows, 2 * chunk)
     if tp.size > 1 and M >= min_rows and not (cuda and torch.cuda.is_current_stream_capturing()):
         parts = chunks_of(M, chunk)
     if len(parts) == 1:

@@ -83,7 +83,7 @@ def _overlap_worker(rank, world, port, out_dir):
     dev = torch.device("cuda", 0)
     res = {}
     try:
-        M, K, N = 2600, 1024, 2048
+        M, K, N = 20000, 1024, 2048  # chunks of 8192 rows: each still >= 256 tiles of 256 x 256
         g = torch.Generator(device=dev).manual_seed(rank)
         a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
         w = (0.05 * torch.randn(N, K, device=dev, generator=g)).to(torch.bfloat16)
@@ -91,11 +91,14 @@ def _overlap_worker(rank, world, port, out_dir):
         res0 = torch.randn(M, N, device=dev, generator=gr).to(torch.bfloat16)
         nw = (torch.rand(N, device=dev, generator=gr) + 0.5).to(torch.bfloat16)
         r1, r2 = res0.clone(), res0.clone()
-        x1 = row_parallel_add_norm(a, w, ps.tp, r1, nw, 1e-5)  # 3 chunks, comm stream
+        x1 = row_parallel_add_norm(a, w, ps.tp, r1, nw, 1e-5)  # chunked on the comm stream
         # reference: the same per-chunk GEMMs (a GEMM's rounding may depend on the M it is
         # planned for), then ONE all-reduce + norm over all rows on the compute stream
-        o = torch.cat([ops.gemm(a[lo:hi], w) for lo, hi in chunks_of(M)])
-        ps.tp.all_reduce(o)
+        parts = chunks_of(M, 8192)
+        assert len(parts) == 3
+        o = torch.cat([ops.gemm(a[lo:hi], w) for lo, hi in parts])
+        for lo, hi in parts:  # the same K15 two-shot messages, on the compute stream
+            ps.tp.all_reduce(o[lo:hi])
         x2 = ops.add_rmsnorm(o, r2, nw, 1e-5)
         torch.cuda.synchronize()
         res["equal"] = bool(torch.equal(x1, x2) and torch.equal(r1, r2))
