@@ -534,7 +534,10 @@ void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offse
 // launches (~4.7 us each, profiles/r01_decode_small_batch.md) for one small tail per launch.
 long gemv_addnorm_ws_floats(int M, int N, int K) {
   // whole row sets in every wave of every workgroup (the grid ticket needs no early exits)
-  static const int on = env_int("MLOP_GEMV_ADDNORM", 1);
+  // measured (scripts/history/r4_b1.sh, profiles/r04_decode_small_batch.md): the fused tail costs
+  // what the separate norm launch did (its three dependent round trips + the grid ticket ~= the
+  // norm kernel's latency), batch 1 329 vs 351 tok/s, batch 4 952 vs 1090: off by default
+  static const int on = env_int("MLOP_GEMV_ADDNORM", 0);
   if (!on || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
   return (long)(N / 2) * M + (long)(N / 2) * M;  // partials (>= sets x M, R = 2 or 4) + the bf16 residual copy
 }

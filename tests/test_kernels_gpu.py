@@ -887,7 +887,8 @@ def test_gemv_add_rmsnorm_epilogue(gpu, M, N, K):
     output vs the fp32 oracle, relaunch bit-identical (partials summed in a fixed order; the
     ticket re-arms), and inside a captured graph."""
     torch.manual_seed(M * N + K)
-    assert torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) > 0
+    if torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) == 0:
+        pytest.skip("GEMV add + RMSNorm epilogue is opt-in (MLOP_GEMV_ADDNORM=1)")
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
     res = torch.randn(M, N, device=gpu, dtype=bf)
