@@ -272,6 +272,131 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
   if (tid == 0) epochs[b] = e;
 }
 
+// Broadcast from `root` over the same buffers and per-block epochs (the TP leader's packed step
+// metadata: a worker's copy is one hop from the leader's IPC buffer, no host round trip):
+//   root: block b publishes its slice into its own buffer (parity e & 1), raises (root, b) at
+//         every peer; every other rank waits for (root, b), copies the slice into `out`, raises
+//         (rank, b); then EVERY rank waits for every rank's (p, b) >= e before the block ends --
+//         nobody starts call e + 2 (the same parity) before everyone finished copying call e.
+template <int NR>
+__global__ void __launch_bounds__(kThreads) car_bcast_kernel(uint4* __restrict__ out, const uint4* __restrict__ in,
+                                                             long n16, Peers peers, int rank, int root,
+                                                             uint32_t* epochs, int* err, size_t max_bytes) {
+  __shared__ uint32_t s_e;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) s_e = epochs[b] + 1;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const long per = (n16 + kBlocks - 1) / kBlocks;
+  const long lo = min(n16, (long)b * per), hi = min(n16, lo + per);
+  auto raise_flag = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < NR; ++p) {
+        uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[p]) + (size_t)(rank * kBlocks + b) * kFlagStride;
+        __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  };
+  auto wait_from = [&](int p) {
+    const uint32_t* f = reinterpret_cast<const uint32_t*>(peers.base[rank]) + (size_t)(p * kBlocks + b) * kFlagStride;
+    long spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++spins > kMaxSpins) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  };
+  if (rank == root) {
+    uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+    for (long i = lo + tid; i < hi; i += kThreads) {
+      const uint4 v = in[i];
+      mine[i] = v;
+      if (out != in) out[i] = v;
+    }
+    raise_flag();
+  } else {
+    if (tid == 0) wait_from(root);
+    if (tid < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(peers.base[root] + doff);
+    for (long i = lo + tid; i < hi; i += kThreads) out[i] = src[i];
+    raise_flag();
+  }
+  if (tid < NR) wait_from(tid);  // everyone done with this call's parity
+  __syncthreads();
+  if (tid == 0) epochs[b] = e;
+}
+
+// All-gather (the TP vocab-parallel logits / greedy (max, index) pairs): every rank publishes
+// its piece (n4 4-B words) into its own buffer, block b raises (rank, b) at every peer, waits
+// for every peer's (p, b) and copies slice b of each piece p into out[p * n4 ...] -- one hop
+// per piece, as the one-shot all-reduce, whose flags / parity / epochs it shares.
+template <int NR>
+__global__ void __launch_bounds__(kThreads) car_allgather_kernel(uint32_t* __restrict__ out,
+                                                                 const uint32_t* __restrict__ in, long n4,
+                                                                 Peers peers, int rank, uint32_t* epochs,
+                                                                 int* err, size_t max_bytes) {
+  __shared__ uint32_t s_e;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) s_e = epochs[b] + 1;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const long per = (n4 + kBlocks - 1) / kBlocks;
+  const long lo = min(n4, (long)b * per), hi = min(n4, lo + per);
+  uint32_t* mine = reinterpret_cast<uint32_t*>(peers.base[rank] + doff);
+  for (long i = lo + tid; i < hi; i += kThreads) {
+    const uint32_t v = in[i];
+    mine[i] = v;
+    out[(long)rank * n4 + i] = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < NR; ++p) {
+      uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[p]) + (size_t)(rank * kBlocks + b) * kFlagStride;
+      __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (tid < 64) {
+    if (tid < NR) {
+      const uint32_t* f = reinterpret_cast<const uint32_t*>(peers.base[rank]) + (size_t)(tid * kBlocks + b) * kFlagStride;
+      long spins = 0;
+      while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+        if (++spins > kMaxSpins) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NR; ++p) {
+    if (p == rank) continue;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(peers.base[p] + doff);
+    for (long i = lo + tid; i < hi; i += kThreads) out[(long)p * n4 + i] = src[i];
+  }
+  if (tid == 0) epochs[b] = e;
+}
+
 CarState* get(long h) {
   if (h == 0) throw std::runtime_error("custom all-reduce: null handle");
   return reinterpret_cast<CarState*>(h);
@@ -359,6 +484,47 @@ void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t s
     case 4: car_oneshot_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
     case 8: car_oneshot_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
     default: throw std::runtime_error("custom all-reduce: world must be 1, 2, 4 or 8");
+  }
+  CAR_CHECK(hipGetLastError());
+}
+
+void car_broadcast(long h, void* out, const void* in, long nbytes, int root, hipStream_t st) {
+  CarState* s = get(h);
+  if (nbytes % 16) throw std::runtime_error("custom broadcast: bytes must be a multiple of 16");
+  if ((size_t)nbytes > s->max_bytes) throw std::runtime_error("custom broadcast: message too large");
+  if (root < 0 || root >= s->world) throw std::runtime_error("custom broadcast: bad root");
+  for (int p = 0; p < s->world; ++p)
+    if (!s->peers.base[p]) throw std::runtime_error("custom broadcast: peers not opened");
+  const long n16 = nbytes / 16;
+  auto* o = static_cast<uint4*>(out);
+  auto* i = static_cast<const uint4*>(in);
+  dim3 g(kBlocks), blk(kThreads);
+  switch (s->world) {
+    case 1: car_bcast_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, root, s->epochs, s->err, s->max_bytes); break;
+    case 2: car_bcast_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, root, s->epochs, s->err, s->max_bytes); break;
+    case 4: car_bcast_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, root, s->epochs, s->err, s->max_bytes); break;
+    case 8: car_bcast_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, root, s->epochs, s->err, s->max_bytes); break;
+    default: throw std::runtime_error("custom broadcast: world must be 1, 2, 4 or 8");
+  }
+  CAR_CHECK(hipGetLastError());
+}
+
+void car_all_gather(long h, void* out, const void* in, long nbytes, hipStream_t st) {
+  CarState* s = get(h);
+  if (nbytes % 4) throw std::runtime_error("custom all-gather: bytes must be a multiple of 4");
+  if ((size_t)nbytes > s->max_bytes) throw std::runtime_error("custom all-gather: piece too large");
+  for (int p = 0; p < s->world; ++p)
+    if (!s->peers.base[p]) throw std::runtime_error("custom all-gather: peers not opened");
+  const long n4 = nbytes / 4;
+  auto* o = static_cast<uint32_t*>(out);
+  auto* i = static_cast<const uint32_t*>(in);
+  dim3 g(kBlocks), blk(kThreads);
+  switch (s->world) {
+    case 1: car_allgather_kernel<1><<<g, blk, 0, st>>>(o, i, n4, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 2: car_allgather_kernel<2><<<g, blk, 0, st>>>(o, i, n4, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 4: car_allgather_kernel<4><<<g, blk, 0, st>>>(o, i, n4, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 8: car_allgather_kernel<8><<<g, blk, 0, st>>>(o, i, n4, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    default: throw std::runtime_error("custom all-gather: world must be 1, 2, 4 or 8");
   }
   CAR_CHECK(hipGetLastError());
 }

@@ -60,6 +60,9 @@ class Group:
     def all_gather(self, x: torch.Tensor, dim: int = -1) -> torch.Tensor:
         if self.size == 1:
             return x
+        if self.car is not None and self.car.can_all_gather(x):
+            parts = self.car.all_gather(x.contiguous())
+            return torch.cat(list(parts.unbind(0)), dim=dim)
         parts = [torch.empty_like(x) for _ in range(self.size)]
         dist.all_gather(parts, x.contiguous(), group=self.handle)
         return torch.cat(parts, dim=dim)
@@ -73,6 +76,8 @@ class Group:
 
     def broadcast(self, x: torch.Tensor, src_rank_in_group: int = 0) -> torch.Tensor:
         if self.size > 1:
+            if self.car is not None and self.car.can_broadcast(x):
+                return self.car.broadcast(x, src_rank_in_group)
             src = dist.get_global_rank(self.handle, src_rank_in_group) if self.handle is not None else src_rank_in_group
             dist.broadcast(x, src=src, group=self.handle)
         return x

@@ -64,6 +64,28 @@ class CustomAllReduce:
         torch.ops.mlop.car_all_reduce(self.h, out, x, bool(two_shot))
         return out
 
+    def can_broadcast(self, x: torch.Tensor) -> bool:
+        n = x.numel() * x.element_size()
+        return x.is_cuda and x.is_contiguous() and n % 16 == 0 and n <= self.max_bytes
+
+    def broadcast(self, x: torch.Tensor, root: int = 0) -> torch.Tensor:
+        """In-place broadcast from group rank ``root``: ONE kernel; every other rank copies the
+        root's bytes straight out of its IPC buffer (one xGMI hop, no host round trip, no RCCL
+        launch).  Shares the per-block epochs with the all-reduce kernels."""
+        torch.ops.mlop.car_broadcast(self.h, x, int(root))
+        return x
+
+    def can_all_gather(self, x: torch.Tensor) -> bool:
+        n = x.numel() * x.element_size()
+        return x.is_cuda and x.is_contiguous() and n % 4 == 0 and 0 < n <= self.max_bytes
+
+    def all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """[world, *x.shape] of every rank's ``x`` in rank order: ONE kernel, each peer's piece
+        read straight from its IPC buffer (the TP vocab-parallel logits / greedy pairs)."""
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        torch.ops.mlop.car_all_gather(self.h, out, x)
+        return out
+
     @property
     def uncached(self) -> bool:
         """True when the IPC buffer (flags + data) is uncached device memory (allreduce.hip)."""

@@ -84,22 +84,25 @@ class MetaBuffers:
         self.npt = 0                 # flash tiles of the last fill
         sizes = [("positions", max_tokens), ("slots", max_tokens), ("tile_seq", self.max_tiles),
                  ("tile_q0", self.max_tiles), ("ptile_seq", self.max_tiles), ("ptile_q0", self.max_tiles),
-                 ("q_start", max_seqs), ("q_len", max_seqs),
-                 ("ctx_len", max_seqs), ("block_tables", max_seqs * max_blocks_per_seq)]
-        # ONE int32 buffer per side: [header | int32 metadata | ids (int64) | logits index (int64)],
-        # every region 64-int aligned.  One H2D ships a step; a tensor-parallel step is ONE
-        # broadcast of the device buffer (engine.StepSync: header + metadata + ids together)
+                 ("q_start", max_seqs), ("q_len", max_seqs), ("ctx_len", max_seqs)]
+        # ONE int32 buffer per side: [header | int32 metadata | ids (int64) | logits index (int64) |
+        # block tables], every region 64-int aligned.  One H2D ships a step; a tensor-parallel
+        # step is ONE broadcast of the device buffer (engine.StepSync: header + metadata + ids
+        # together).  The block tables come last, so both move only the prefix up to the highest
+        # row in use (extent()): [max_seqs, max_blocks] is most of the buffer at long contexts.
         self.HDR = 16
         self.off = {}
         o = self.HDR
         for name, n in sizes:
             self.off[name] = (o, n)
             o += (n + 63) // 64 * 64
-        meta_lo, meta_hi = self.HDR, o
+        meta_hi = o
         ids_lo = o
         o += (2 * max_tokens + 63) // 64 * 64
         lidx_lo = o
         o += (2 * max_seqs + 63) // 64 * 64
+        self.off["block_tables"] = (o, max_seqs * max_blocks_per_seq)
+        o += (max_seqs * max_blocks_per_seq + 63) // 64 * 64
         self.total = o
         pin = self.device.type == "cuda"
         self.hbuf = torch.zeros(o, dtype=torch.int32, pin_memory=pin)
@@ -135,9 +138,20 @@ class MetaBuffers:
         o, cap = self.off[name]
         return self.d[o:o + (cap if n is None else n)]
 
-    def upload(self, n_ids: int = 0, n_logits: int = 0):
-        """ONE async H2D of header + metadata + ids + logits index on the current stream."""
-        self.dbuf.copy_(self.hbuf, non_blocking=True)
+    def extent(self, rows_hi: int | None = None) -> int:
+        """int32 words of the buffer a step needs: everything up to block-table row ``rows_hi``
+        (the engine's high-water row: graph-padding rows attend to nothing and read no block
+        table), a multiple of 64 words; None = the whole buffer."""
+        if rows_hi is None:
+            return self.total
+        o, _ = self.off["block_tables"]
+        return min(self.total, o + (max(0, rows_hi) * self.mb + 63) // 64 * 64)
+
+    def upload(self, n_ids: int = 0, n_logits: int = 0, rows_hi: int | None = None):
+        """ONE async H2D of header + metadata + ids + logits index (+ the block-table rows in
+        use) on the current stream."""
+        n = self.extent(rows_hi)
+        self.dbuf[:n].copy_(self.hbuf[:n], non_blocking=True)
 
     def set_header(self, vals) -> None:
         self.hdr_hn[:len(vals)] = vals

@@ -54,11 +54,14 @@ class StepSync:
         scheduling, and no worker ever reads a device tensor back to decide what to run;
       * the step's packed metadata buffer (attn_meta.MetaBuffers: int32 metadata, ids and
         logits index in ONE device buffer, already uploaded by one H2D, decode ids gathered on
-        the device from the previous step's tokens) as ONE in-stream device broadcast (RCCL on
-        GPU, gloo on CPU), ordered after the previous forward on every rank's stream.
+        the device from the previous step's tokens) as ONE in-stream device broadcast of its
+        used prefix (header word 9: up to the highest block-table row in use): the K15 IPC
+        broadcast kernel on GPU (parallel/custom_ar.py: each worker copies the leader's bytes in
+        one hop, no host round trip), RCCL / gloo otherwise, ordered after the previous forward
+        on every rank's stream.
     STOP / BARRIER steps carry the header only."""
 
-    NHDR = 9
+    NHDR = 10
 
     def __init__(self, group, cpu_group=None):
         import os
@@ -89,17 +92,18 @@ class StepSync:
         dist.broadcast(self.hdr, src=dist.get_global_rank(self.cpu, 0), group=self.cpu)
 
     def send(self, eng, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
-        self.hdr[:] = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt, greedy], dtype=torch.int64)
+        n = eng.meta.extent(eng.rows_hi)
+        self.hdr[:] = torch.tensor([kind, T, nt, nl, part, nparts, bucket, npt, greedy, n], dtype=torch.int64)
         self._bcast_header()
         if kind not in (KIND_STOP, KIND_BARRIER):
-            self.g.broadcast(eng.meta.dbuf, 0)
+            self.g.broadcast(eng.meta.dbuf[:n], 0)
 
     def recv(self, eng):
         self._bcast_header()
         hdr = tuple(self.hdr.tolist())
         if hdr[0] not in (KIND_STOP, KIND_BARRIER):
-            self.g.broadcast(eng.meta.dbuf, 0)
-        return hdr
+            self.g.broadcast(eng.meta.dbuf[:hdr[9]], 0)
+        return hdr[:9]
 
 
 class _Tokens:
@@ -294,6 +298,7 @@ class Engine:
                                 cfg.max_num_seqs + self.buckets[-1], self.max_blocks_per_seq,
                                 self.G, model.n_kv, self.max_model_len, self.device)
         self.free_rows = list(range(cfg.max_num_seqs - 1, -1, -1))
+        self.rows_hi = 0  # high-water row + 1: the block-table rows a step's upload / broadcast moves
         # struct-of-arrays state of running rows: the decode hot path is vectorised
         R = cfg.max_num_seqs
         self.r_len = np.zeros(R, np.int64)      # tokens in the sequence (prompt + output)
@@ -523,12 +528,12 @@ class Engine:
         empty = np.zeros(0, dtype=np.int32)
         if eager or bucket not in self.graphs:
             self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=1)
-            self.meta.upload(1, 1)
+            self.meta.upload(1, 1, self.rows_hi)
             self.model.moe_capacity_tokens = t_max
             self.model.forward(self.meta.ids_d[:1], self.meta.meta(1, 1, 1, 32, 1), self.kv)
         else:
             self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=bucket)
-            self.meta.upload(bucket, bucket)
+            self.meta.upload(bucket, bucket, self.rows_hi)
             self.graphs[bucket][0].replay()
         if self._async and self.device.type == "cuda":
             self._meta_ev = torch.cuda.Event()
@@ -573,6 +578,7 @@ class Engine:
         while budget > 0 and self.waiting and self.free_rows:
             seq = self.waiting[0]
             seq.row = self.free_rows.pop()
+            self.rows_hi = max(self.rows_hi, seq.row + 1)
             if self.cfg.enable_prefix_caching:
                 self._match_prefix(seq)
             n = min(seq.length - seq.num_cached, budget)
@@ -1106,7 +1112,7 @@ class Engine:
         npt = self.meta.npt  # flash-prefill tiles of the metadata just filled
         if self.ep_sync is not None:
             kind, T, nt, nl, part, nparts, bucket = self._ep_agree(kind, T, nt, nl, part, nparts, bucket)
-        self.meta.upload(T, nl)
+        self.meta.upload(T, nl, self.rows_hi)
         g = self._ids_gather
         if g is not None:
             # async: decode rows' input ids = the previous (in-flight) step's sampled tokens,

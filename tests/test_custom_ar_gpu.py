@@ -5,7 +5,9 @@ exercised exactly as across xGMI peers (the fabric path itself needs a
 multi-GPU node).  Messages of 512 KiB and more take the two-shot kernel
 (reduce-scatter + all-gather over peer memory); small ones are also forced
 through it.  Oracle: fp32 sum in rank order of the known per-rank inputs,
-rounded once to bf16 — the kernel must match it bit for bit on every rank."""
+rounded once to bf16 — the kernel must match it bit for bit on every rank.  The
+broadcast kernel (the TP step-metadata path) must deliver the root's bytes exactly, and the
+all-gather kernel every rank's piece in rank order."""
 import os
 import socket
 import tempfile
@@ -69,6 +71,38 @@ def _worker(rank, world, port, out_dir):
             car.all_reduce(y, two_shot=it % 2 == 0)
             torch.cuda.synchronize()
             res["two_shot"].append(torch.equal(out.cpu(), _oracle(xs)) and torch.equal(y.cpu(), _oracle(xs)))
+        # broadcast (the TP step metadata path): int32 buffers from either root, uneven arrival
+        # on both sides, interleaved with all-reduces on the same epochs
+        res["bcast"] = []
+        for it, (n, root) in enumerate([(4, 0), (64, 1), (4096 * 4, 0), (1 << 20, 1), (12, 0), (300 * 1024, 0)]):
+            src = torch.randint(-2 ** 31, 2 ** 31 - 1, (n,), generator=torch.Generator().manual_seed(700 + it),
+                                dtype=torch.int32)
+            buf = src.cuda() if rank == root else torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            if it % 3 == 1 and rank == root:
+                time.sleep(0.05)
+            if it % 3 == 2 and rank != root:
+                time.sleep(0.05)
+            car.broadcast(buf, root)
+            xs = _inputs(300 + it, 4096, world)
+            y = xs[rank].cuda()
+            car.all_reduce(y)
+            torch.cuda.synchronize()
+            res["bcast"].append(torch.equal(buf.cpu(), src) and torch.equal(y.cpu(), _oracle(xs)))
+        # all-gather (TP logits / greedy pairs): fp32 and int32 pieces, uneven arrival,
+        # interleaved with all-reduces on the same epochs
+        res["gather"] = []
+        for it, n in enumerate([2, 4, 4096, 3 * 1000 + 1, 64 * 1024]):
+            pieces = [torch.randn(n, generator=torch.Generator().manual_seed(900 + 10 * it + p)) for p in range(world)]
+            if it % 2:
+                pieces = [(1e6 * x).to(torch.int32) for x in pieces]
+            if rank == 1 and it % 2:
+                time.sleep(0.05)
+            got = car.all_gather(pieces[rank].cuda())
+            xs = _inputs(400 + it, 4096, world)
+            y = xs[rank].cuda()
+            car.all_reduce(y)
+            torch.cuda.synchronize()
+            res["gather"].append(torch.equal(got.cpu(), torch.stack(pieces)) and torch.equal(y.cpu(), _oracle(xs)))
         # in place, back to back (parity reuse every second call)
         for it in range(6):
             xs = _inputs(50 + it, 4096, world)
@@ -121,3 +155,5 @@ def test_custom_all_reduce_two_processes_one_gpu():
         assert all(res["inplace"]), (r, res["inplace"])
         assert all(res["graph"]), (r, res["graph"])
         assert all(res["two_shot"]), (r, res["two_shot"])
+        assert all(res["bcast"]), (r, res["bcast"])
+        assert all(res["gather"]), (r, res["gather"])
