@@ -239,7 +239,9 @@ class ProcessLauncher:
                             break
                 except (aiohttp.ClientError, asyncio.TimeoutError, OSError):
                     pass
-                await asyncio.sleep(0.1)
+                # readiness probe period: 20 ms (a connection refused costs ~0.1 ms, and the
+                # probe granularity is part of every measured CR->ready)
+                await asyncio.sleep(0.02)
         if self.scraper is not None:
             self.scraper.add_target(pod.endpoint + "/metrics")
 

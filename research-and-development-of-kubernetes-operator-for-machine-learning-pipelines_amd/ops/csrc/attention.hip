@@ -1,9 +1,13 @@
 // Paged attention over the block-table KV cache (K6 decode, and the ragged /
 // chunked-prefill path of K7) with MFMA 16x16x32 bf16 on gfx950.
 //
-// Layouts (written by rope_cache.hip):
+// Layouts (written by rope_cache.hip and the fused QKV GEMM epilogues):
 //   k_cache[page, Hkv, 16, 128]  token-major  -> A operand of  S^T = K . Q^T
-//   v_cache[page, Hkv, 128, 16]  dim-major    -> A operand of  O^T = V^T . P^T
+//   v_cache[page, Hkv, 16, 128]  token-major  -> staged in LDS, read back transposed
+//                                                (ds_read_b64_tr_b16) as the A operand of
+//                                                O^T = V^T . P^T
+// A token's V row is one contiguous 256-B store for its writer (a decode token used to scatter
+// 128 2-B stores over a dim-major page; scripts/bench_vt.py measured the two layouts).
 // Both products keep the q-row on the lane (col = lane&15), so the online
 // softmax (max, exp2, rescale of O) is entirely lane-local except the two
 // cross-lane max steps (xor 16, xor 32), and P^T feeds the second MFMA straight
@@ -12,9 +16,8 @@
 // Decode kernel token order of a page pair (A, B; pair token t = 16*page + offset):
 // lane group g = lane>>4 owns the 8 CONSECUTIVE pair tokens 8g..8g+7 - the first S
 // MFMA produces 8g..8g+3 of every group, the second 8g+4..8g+7 (its K rows are
-// loaded in that permuted row order) - so each lane's V^T fragment is ONE 16-B load
-// of a dim-major page row (8-B loads stream at 0.54-0.70x the 16-B rate,
-// MI355X_MICROARCH.md "visibility" table) and P^T = {S1 rows, S2 rows} as before.
+// loaded in that permuted row order) - so each lane's V^T fragment is two transposed
+// 4-row reads of the pair's LDS image and P^T = {S1 rows, S2 rows} as before.
 //
 // MFMA rows: 16 q-rows per tile = (16/G query tokens) x (G heads of one kv head).
 // A workgroup = 4 waves = one (tile, kv head, kv partition); the waves split
@@ -22,8 +25,9 @@
 // Partitions > 1 (long context, small batch: fill 256 CUs) write fp32 partials
 // that attn_reduce_kernel combines.
 //
-// Memory-bound: each K/V byte is loaded once per tile into VGPRs (no LDS
-// staging: "GEMV / M <= 16" row of the glds table, cdna_hip_programming.md §5).
+// Memory-bound: each K byte is loaded once per tile straight into VGPRs ("GEMV / M <= 16" row
+// of the glds table, cdna_hip_programming.md §5); each V byte once into the wave's LDS image
+// by LDS-DMA (the transpose needs it in LDS).
 //
 // REQUIREMENT: the cache is zero-initialised at allocation (masked lanes multiply
 // p = 0 with whatever the unused slots hold; NaN garbage would poison O).
@@ -43,6 +47,39 @@ constexpr int kD = 128;
 constexpr int kBS = 16;
 constexpr float kNegBig = -1.0e30f;
 
+// token-major V image in LDS: [rows][256 B], 16-B chunk c of row t at slot c ^ vswz(t)
+// (cdna_hip_programming.md T10 image (b)); filled by LDS-DMA through the source address and
+// read back transposed with ds_read_b64_tr_b16: a half-wave's two 4-row blocks 8 rows apart in
+// the same columns are conflict-free
+__device__ __forceinline__ int vswz(int t) { return ((t & 3) << 2) | ((t >> 2) & 3); }
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
+
+// V^T fragment (A operand of O^T = V^T . P^T, 16x16x32) for dims 16d .. 16d+15 and image rows
+// 8 g4 .. 8 g4 + 7 of lane group g4 = lane >> 4 (two ds_read_b64_tr_b16: rows +0..3, +4..7).
+// Lane 4q + p of a group addresses row t = 8 g4 + 4h + q, dims 16d + 4p .. +3, i.e. byte
+//   256 t + 16 ((2d + (p >> 1)) ^ vswz(t)) + 8 (p & 1) = vt_base(lane) ^ 32 d          (h = 0)
+// because 2d only moves bits 5-7, which the rest leaves 0 (the image is 256-B aligned); rows
+// t + 4 flip bit 0 of vswz and nothing else the offset uses, so h = 1 is (that ^ 16) + 1024: ONE
+// base VGPR, two v_xor and an immediate offset per fragment.
+__device__ __forceinline__ uint32_t vt_base(int lane) {
+  const int g4 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int row = 8 * g4 + q, sw = vswz(row & 15);
+  return 256u * row + 16u * ((p >> 1) ^ (sw & 1)) + 8u * (p & 1) + 32u * (sw >> 1);
+}
+__device__ __forceinline__ bf16x8 vt_frag(uint32_t b, int d) {
+  const uint32_t a0 = b ^ (32u * d), a1 = (a0 ^ 16u) + 1024u;
+  const v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(uintptr_t)a0);
+  const v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(uintptr_t)a1);
+  bf16x8 f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[e] = lo[e];
+    f[4 + e] = hi[e];
+  }
+  return f;
+}
+
 template <int G>
 __global__ void __launch_bounds__(256) paged_attn_kernel(
     uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -53,7 +90,9 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int part_tokens,
     int nparts, int num_blocks, int* __restrict__ sem) {
   constexpr int QT = 16 / G;
-  __shared__ float sm_o[4][16][kD + 4];
+  // wave w stages its page pair's V (2 x 16 token rows x 256 B = 8 KB) inside sm_o[w]
+  // (8448 B, 256-B aligned: vt_frag), which it alone writes after its loop
+  __shared__ __attribute__((aligned(256))) float sm_o[4][16][kD + 4];
   __shared__ float sm_m[4][16];
   __shared__ float sm_l[4][16];
   __shared__ int sm_last;
@@ -125,10 +164,20 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       kb[kk] = *reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8);
     }
     // V^T fragment of lane group g4: dims d*16 + r, pair tokens 8*g4 .. 8*g4+7 (16 B)
-    const uint16_t* vR = (g4 >> 1 ? vB : vA) + r * kBS + 8 * (g4 & 1);
     bf16x8 vf8[8];
+    // (a generic pointer's low 32 bits are the LDS offset)
+    const uint32_t vimg = (uint32_t)(uintptr_t)&sm_o[0][0][0] + wid * 8448u;
+    {
+      // the pair's 32 token rows by LDS-DMA into this wave's image, issued after the K loads
+      // (the S MFMAs wait for those only); the previous pair's transposed reads are complete
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int d = 0; d < 8; ++d) vf8[d] = *reinterpret_cast<const bf16x8*>(vR + d * 16 * kBS);
+      for (int i = 0; i < 8; ++i) {
+        const int trow = (4 * i + g4) & 15;
+        const uint16_t* src = (i < 4 ? vA : vB) + trow * kD + ((r ^ vswz(trow)) << 3);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(vimg + 1024u * i), 16, 0, 0);
+      }
+    }
 
     // S^T[token][row]: lane holds row r, tokens 4*g4 + i of each page
     f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
@@ -164,6 +213,13 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     for (int i = 0; i < 4; ++i) {
       pf[i] = (short)f2bf(pa[i]);
       pf[4 + i] = (short)f2bf(pb[i]);
+    }
+    {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V image has landed
+      uint32_t b0 = vimg + vt_base(lane);
+      asm volatile("" : "+v"(b0));  // no hoisting of the 16 read addresses out of the loop
+#pragma unroll
+      for (int d = 0; d < 8; ++d) vf8[d] = vt_frag(b0, d);
     }
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
@@ -352,7 +408,7 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
 // stream through a 3-deep LDS ring by LDS-DMA (global_load_lds, counted vmcnt,
 // one raw barrier per pair), swizzled through the SOURCE address:
 //   K page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ k        (ds_read_b128, 16 keys/group)
-//   V page [128 dims][4 x 8 B]:  chunk c of dim d at c ^ ((d>>3&1)<<1) (ds_read_b64, dims d, d+8)
+//   V page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ vswz(k)  (ds_read_b64_tr_b16)
 // both conflict-free for the fragment reads below.
 #ifndef FLASH_WG_PER_CU
 #define FLASH_WG_PER_CU 3
@@ -368,7 +424,7 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   constexpr int STAGES = 3;
   constexpr int STAGE = 4 * kBS * kD;    // bf16 per stage: K page A | K page B | V page A | V page B
   constexpr int PAGE = kBS * kD;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[STAGES * STAGE];
+  __shared__ __attribute__((aligned(256))) uint16_t smem[STAGES * STAGE];
 
   // 1-D grid, kv head fastest: blocks are dealt to the 8 XCDs round-robin, so with 8 kv
   // heads every workgroup of one head runs on ONE XCD and the 64+ q-tiles of a sequence
@@ -415,10 +471,12 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   // {0-3, 8-11} (or {4-7, 12-15}) of BOTH pages in one 16-lane group, all 16 slots distinct
   const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
   const int k_offB = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15) ^ 4) << 3);
-  const int vdim = wid * 32 + (lane >> 1);
-  const int v_off = kvh * PAGE + vdim * kBS + ((((lane & 1) ^ ((vdim >> 3) & 1))) << 3);
+  // V image: [16 token rows][256 B] per page, 16-B chunk c of row t at slot c ^ vswz(t)
+  const int v_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ vswz(kkey)) << 3);
   // page ids of pair pp; the loop reads them one iteration ahead of their DMA, so the
   // block-table load's latency is not paid in front of every issue
+  // per-lane transposed-read base of the stage-0 V image (stage ST adds a constant)
+  const uint32_t vt_b0 = (uint32_t)(uintptr_t)smem + vt_base(lane);
   auto page_of = [&](int idx) { return idx < n_pages ? min(max(bt[idx], 0), num_blocks - 1) : -1; };
   auto issue_pages = [&](int buf, int pgA, int pgB) {
     if (pgB < 0) pgB = pgA;
@@ -508,14 +566,20 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     }
     // O^T += V^T . P^T: one V fragment per 16-dim block, read just in time and used by
     // both column tiles (8 VGPRs of V live instead of 32: 3 waves per SIMD fit)
+    {
+      // rows 8 g4 .. 8 g4 + 7 of the two stacked page images (page g4 >> 1), one fragment per
+      // 16-dim block read just in time and used by both column tiles
+      constexpr uint32_t vo = (uint32_t)(ST * STAGE * 2 + 4 * PAGE);
+      // opaque per pair: otherwise the 16 loop-invariant read addresses are hoisted out of the
+      // loop and spilled (168-VGPR budget of 3 workgroups per CU)
+      uint32_t vb = vt_b0 + vo;
+      asm volatile("" : "+v"(vb));
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      const int dim = d * 16 + r;
-      const int c8 = ((2 * (g4 & 1)) ^ (((dim >> 3) & 1) << 1)) << 2;
-      // tokens 8g4..8g4+7 = page g4>>1, 8-B chunks 2(g4&1), +1 (swizzled pair stays adjacent)
-      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sV + (g4 >> 1) * PAGE + dim * kBS + c8);
+      for (int d = 0; d < 8; ++d) {
+        const bf16x8 vf = vt_frag(vb, d);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
+        for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
+      }
     }
   };
   for (int pp = 0; pp < n_pairs; pp += STAGES) {

@@ -63,9 +63,8 @@ void rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor qkv, Tensor
   TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "rope_cache ranks");
   const int T = (int)q_out.size(0), Hq = (int)q_out.size(1), D = (int)q_out.size(2);
   const int Hkv = (int)k_cache.size(1), BS = (int)k_cache.size(2);
-  TORCH_CHECK(k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
-                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
-              "cache layouts: k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(k_cache.size(3) == D && v_cache.sizes() == k_cache.sizes(),
+              "cache layouts: k and v [NB,Hkv,BS,D] (token-major)");
   TORCH_CHECK(D % 16 == 0, "head dim must be a multiple of 16");
   TORCH_CHECK(qkv.size(0) == T && qkv.size(-1) >= (Hq + 2 * Hkv) * D, "qkv shape");
   TORCH_CHECK(pos.numel() == T && slots.numel() == T, "pos/slots length");
@@ -109,8 +108,8 @@ void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor 
   TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
               "k_cache must be [NB, Hkv, 16, 128]");
-  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 128, 16}),
-              "v_cache must be [NB, Hkv, 128, 16]");
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 16, 128}),
+              "v_cache must be [NB, Hkv, 16, 128] (token-major, as k_cache)");
   const int Hq = (int)q.size(1), Hkv = (int)k_cache.size(1);
   TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
   const int G = Hq / Hkv;
@@ -141,8 +140,8 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem,
   TORCH_CHECK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 16 && k_cache.size(3) == 128,
               "k_cache must be [NB, Hkv, 16, 128]");
-  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 128, 16}),
-              "v_cache must be [NB, Hkv, 128, 16]");
+  TORCH_CHECK(v_cache.sizes() == at::IntArrayRef({k_cache.size(0), k_cache.size(1), 16, 128}),
+              "v_cache must be [NB, Hkv, 16, 128] (token-major, as k_cache)");
   const int Hq = (int)q.size(1), Hkv = (int)k_cache.size(1);
   TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
   const int G = Hq / Hkv;
@@ -260,10 +259,6 @@ void gemm(Tensor out, Tensor a, Tensor w, Tensor ws, int64_t epi) {
 
 // QKV projection with RoPE + paged-cache stores in the GEMM epilogue; false = this M
 // does not take the fused tiling (caller runs gemm + rope_cache)
-bool gemm_rope_stages_v_op(int64_t M, int64_t N, int64_t K) {
-  return mlop::gemm_rope_stages_v((int)M, (int)N, (int)K);
-}
-
 bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor w, Tensor pos,
                      Tensor cos_sin, Tensor slots) {
   TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
@@ -276,9 +271,8 @@ bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Ten
   TORCH_CHECK(w.dim() == 2 && w.size(1) == K && K % 64 == 0, "w [N, K], K % 64");
   TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "ranks");
   const int64_t Hq = q_out.size(1), D = q_out.size(2), Hkv = k_cache.size(1), BS = k_cache.size(2);
-  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
-                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
-              "head_dim 128; k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.sizes() == k_cache.sizes(),
+              "head_dim 128; k and v [NB,Hkv,BS,D]");
   TORCH_CHECK(N == (Hq + 2 * Hkv) * D && q_out.size(0) == M, "qkv width / q_out rows");
   TORCH_CHECK(pos.numel() == M && slots.numel() == M, "pos/slots length");
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin [max_pos, D]");
@@ -286,14 +280,6 @@ bool gemm_rope_cache(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Ten
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
-  // large-M fused path: V staged token-major, then paged by a chip-wide scatter (MLOP_V_STAGE=0:
-  // the epilogue's own 2-B page-row stores, A/B).  Caching-allocator memory: capture-safe.
-  static const bool stage_v = std::getenv("MLOP_V_STAGE") == nullptr || std::string(std::getenv("MLOP_V_STAGE")) != "0";
-  at::Tensor vtmp;
-  if (stage_v && mlop::gemm_rope_stages_v((int)M, (int)N, (int)K)) {
-    vtmp = at::empty({M, Hkv, D}, a.options());
-    re.v_tmp = (uint16_t*)vtmp.data_ptr();
-  }
   return mlop::launch_gemm_rope(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)M, (int)N, (int)K,
                                 re, cur_stream());
 }
@@ -365,9 +351,8 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
   TORCH_CHECK(w.dim() == 2 && w.size(1) == K && K % 64 == 0, "w [N, K], K % 64");
   TORCH_CHECK(q_out.dim() == 3 && k_cache.dim() == 4 && v_cache.dim() == 4, "ranks");
   const int64_t Hq = q_out.size(1), D = q_out.size(2), Hkv = k_cache.size(1), BS = k_cache.size(2);
-  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.size(2) == D && v_cache.size(3) == BS &&
-                  v_cache.size(1) == Hkv && v_cache.size(0) == k_cache.size(0),
-              "head_dim 128; k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+  TORCH_CHECK(D == 128 && k_cache.size(3) == D && v_cache.sizes() == k_cache.sizes(),
+              "head_dim 128; k and v [NB,Hkv,BS,D]");
   TORCH_CHECK(N == (Hq + 2 * Hkv) * D && q_out.size(0) == M, "qkv width / q_out rows");
   TORCH_CHECK(pos.numel() == M && slots.numel() == M, "pos/slots length");
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin [max_pos, D]");
@@ -377,8 +362,6 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
-  at::Tensor vtmp = at::empty({M, Hkv, D}, a.options());  // token-major V, paged by launch_v_scatter
-  re.v_tmp = (uint16_t*)vtmp.data_ptr();
   re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
   re.ss_inv_k = 1.f / (float)K;
   re.ss_eps = (float)eps;
@@ -427,8 +410,8 @@ bool gemm_norm_impl(Tensor* out, Tensor* q_out, Tensor* k_cache, Tensor* v_cache
     check_i32(*pos, "pos"); check_i32(*slots, "slots");
     const int64_t Hq = q_out->size(1), D = q_out->size(2), Hkv = k_cache->size(1), BS = k_cache->size(2);
     TORCH_CHECK(D == 128 && N == (Hq + 2 * Hkv) * D && q_out->size(0) == M && pos->numel() == M &&
-                    slots->numel() == M && v_cache->size(2) == D && v_cache->size(3) == BS,
-                "qkv layout: head_dim 128, q_out [M, Hq, 128], k [NB,Hkv,BS,D], v [NB,Hkv,D,BS]");
+                    slots->numel() == M && v_cache->sizes() == k_cache->sizes(),
+                "qkv layout: head_dim 128, q_out [M, Hq, 128], k and v [NB,Hkv,BS,D]");
     TORCH_CHECK(cos_sin->is_cuda() && cos_sin->scalar_type() == at::kFloat && cos_sin->size(1) == D, "cos_sin");
     mlop::RopeEpi re{(uint16_t*)q_out->data_ptr(), (uint16_t*)k_cache->data_ptr(),
                      (uint16_t*)v_cache->data_ptr(), pos->data_ptr<int>(), cos_sin->data_ptr<float>(),
@@ -627,6 +610,22 @@ void car_all_reduce(int64_t h, Tensor out, Tensor inp, bool two_shot) {
   c10::DeviceGuard g(inp.device());
   mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream(), two_shot);
 }
+// in-place broadcast of any contiguous device tensor (bytes % 16 == 0) from `root`
+void car_broadcast(int64_t h, Tensor buf, int64_t root) {
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "broadcast: contiguous device tensor");
+  const long nbytes = (long)(buf.numel() * buf.element_size());
+  c10::DeviceGuard g(buf.device());
+  mlop::car_broadcast((long)h, buf.data_ptr(), buf.data_ptr(), nbytes, (int)root, cur_stream());
+}
+// out [world * piece] <- every rank's contiguous piece (bytes % 4 == 0), rank order
+void car_all_gather(int64_t h, Tensor out, Tensor piece) {
+  TORCH_CHECK(piece.is_cuda() && piece.is_contiguous() && out.is_cuda() && out.is_contiguous() &&
+                  out.scalar_type() == piece.scalar_type(), "all-gather: contiguous device tensors of one dtype");
+  const long nbytes = (long)(piece.numel() * piece.element_size());
+  TORCH_CHECK(out.numel() % piece.numel() == 0 || piece.numel() == 0, "all-gather: out = world x piece");
+  c10::DeviceGuard g(piece.device());
+  mlop::car_all_gather((long)h, out.data_ptr(), piece.data_ptr(), nbytes, cur_stream());
+}
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
@@ -700,6 +699,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);
   m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp, bool two_shot=False) -> ()");
+  m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
+  m.def("car_all_gather(int h, Tensor(a!) out, Tensor piece) -> ()");
   m.def("car_error(int h) -> int", &car_error);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
@@ -737,7 +738,6 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_rs(Tensor(a!) out, Tensor a, Tensor w, Tensor ss_in, float eps, int epi) -> bool");
   m.def("gemm_rs_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots, Tensor ss_in, float eps) -> bool");
-  m.def("gemm_rope_stages_v(int M, int N, int K) -> bool", &gemm_rope_stages_v_op);
   m.def("gemm_rope_cache(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor a, Tensor w, "
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
@@ -802,6 +802,8 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
   m.impl("car_all_reduce", &car_all_reduce);
+  m.impl("car_broadcast", &car_broadcast);
+  m.impl("car_all_gather", &car_all_gather);
   m.impl("ep_dispatch", &ep_dispatch);
   m.impl("ep_combine", &ep_combine);
 }

@@ -541,9 +541,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       const int gm_here = min(group_m, m_tiles - band * group_m);
       m0 = (band * group_m + in_band % gm_here) * BM;
       n0 = (in_band / gm_here) * BN;
-      // RoPE epilogue: the V heads (last columns) write their dim-major pages with 2-B
-      // scattered stores and are the slow tiles; walk each band's n-tiles backwards so they
-      // are dispatched in the first round and their CUs take no second tile
+      // RoPE epilogue: walk each band's n-tiles backwards (the V heads, last columns, first;
+      // they were the slow tiles while V pages were dim-major, and the order costs nothing)
       if constexpr (EPI == EPI_ROPE) n0 = (n_tiles_x - 1) * BN - n0;
     }
   };
@@ -1157,7 +1156,6 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
   p.k_chunk = K;
   launch_plan<EPI_ROPE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, 0, nullptr,
                                M, N, K, nullptr, 0, st, re);
-  if (re.v_tmp != nullptr) launch_v_scatter(re.v_tmp, re.v_cache, re.slots, M, re.Hkv, re.BS, st);
   return true;
 }
 
@@ -1181,14 +1179,7 @@ bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, in
   if (M == 0) return true;
   if (!w4_chain_ok(M, N, K) || !gemm_w4_ok(M, N, K, lda, K, ldc)) return false;
   if (!run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re)) return false;
-  if ((epi & 3) == EPI_ROPE && re.v_tmp != nullptr) launch_v_scatter(re.v_tmp, re.v_cache, re.slots, M, re.Hkv, re.BS, st);
   return true;
-}
-
-bool gemm_rope_stages_v(int M, int N, int K) {
-  if (M == 0 || !gemm_rope_supported(M, N, K) || gemv_takes(M, N, K, EPI_ROPE)) return false;
-  const Plan p = plan(M, N, K, false, 0, 0);
-  return p.BM == 256 && p.BN >= 128;
 }
 
 long gemm_workspace_floats(int M, int N, int K, int epi) {

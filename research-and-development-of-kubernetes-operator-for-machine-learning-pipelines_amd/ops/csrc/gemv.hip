@@ -270,9 +270,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       } else if (slot >= 0) {
         const int vr = 2 * set - 2 * rope_sets;  // first v row (0 .. Hkv*128)
         const int kh = vr / kHeadD, dd = vr % kHeadD;
-        uint16_t* dst = re.v_cache + (((size_t)blk * re.Hkv + kh) * kHeadD + dd) * re.BS + off;
-        dst[0] = f2bf(acc[0][m]);
-        dst[re.BS] = f2bf(acc[1][m]);
+        // token-major page row (as K): dims dd, dd + 1 are adjacent
+        uint16_t* dst = re.v_cache + (((size_t)blk * re.Hkv + kh) * re.BS + off) * kHeadD + dd;
+        *reinterpret_cast<uint32_t*>(dst) = pack2(acc[0][m], acc[1][m]);
       }
     }
   } else if constexpr (EPI == EPI_ADDNORM) {

@@ -43,10 +43,6 @@ struct RopeEpi {
   const float* cos_sin;
   const int* slots;
   int Hq, Hkv, BS;
-  // token-major [M, Hkv, 128] staging for the V heads (large-M fused QKV epilogue): the GEMM
-  // writes it with 16-B stores and launch_v_scatter moves it into the dim-major pages over
-  // the whole chip (nullptr: the epilogue scatters V itself)
-  uint16_t* v_tmp = nullptr;
   // four-wave norm chain (run_w4 only; the large-M TP=1 decoder with unit norm weights, see
   // launch_w4_chain).  Producer (C += A.B^T): ss_out = [M, N / 128] partial sums of squares of
   // the updated residual rows (one per row and wave column block), then ss_tot [M] = their row
@@ -59,11 +55,6 @@ struct RopeEpi {
   int* ss_cnt = nullptr;
   float ss_inv_k = 0.f, ss_eps = 0.f;
 };
-// V rows staged token-major -> dim-major paged cache ([NB, Hkv, 128, BS]); slot < 0 skipped
-void launch_v_scatter(const uint16_t* v_tmp, uint16_t* v_cache, const int* slots, int M, int Hkv, int BS,
-                      hipStream_t st);
-// true when launch_gemm_rope takes the large-M fused path, which stages V in re.v_tmp
-bool gemm_rope_stages_v(int M, int N, int K);
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st);
@@ -172,6 +163,8 @@ void car_ipc_handle(long h, void* out64);
 void car_open(long h, const void* handles);
 long car_max_bytes(long h);
 void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot = false);
+void car_broadcast(long h, void* out, const void* in, long nbytes, int root, hipStream_t st);
+void car_all_gather(long h, void* out, const void* in, long nbytes, hipStream_t st);
 int car_error(long h);
 int car_mem_mode(long h);
 void car_destroy(long h);

@@ -6,7 +6,8 @@
 // cos/sin table: no on-device trig, cdna_hip_programming.md App. B) and
 //   * writes q to q_out[t, Hq, D] (contiguous, the attention kernel's input);
 //   * writes k to k_cache[block, Hkv, BS, D]   (token-major rows, the A operand of S^T = K.Q^T);
-//   * writes v to v_cache[block, Hkv, D, BS]   (dim-major, the A operand of O^T = V^T.P^T).
+//   * writes v to v_cache[block, Hkv, BS, D]   (token-major rows too: attention.hip stages a
+//     page pair in LDS and reads the A operand of O^T = V^T.P^T with ds_read_b64_tr_b16).
 // slot[t] = block*BS + offset, or < 0 for padding tokens (no cache write).
 #include "common.h"
 #include "launch.h"
@@ -86,12 +87,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
       const int iv = it - n_rope;
       const int kh = iv / (D >> 3), c = (iv % (D >> 3)) * 8;
       u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, (Hq + Hkv + kh) * D + c);
-      uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c) * BS + off;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dst[(2 * j) * BS] = (uint16_t)(a[j] & 0xffff);
-        dst[(2 * j + 1) * BS] = (uint16_t)(a[j] >> 16);
-      }
+      *reinterpret_cast<u32x4*>(v_cache + (((size_t)blk * Hkv + kh) * BS + off) * D + c) = a;
     }
   }
 }
@@ -109,42 +105,6 @@ void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int
   if (T == 0) return;
   rope_cache_kernel<true><<<T, 256, 0, st>>>(re.q_out, re.k_cache, re.v_cache, nullptr, re.pos, re.cos_sin,
                                              re.slots, re.Hq, re.Hkv, 128, N, re.BS, ws, splits);
-}
-
-// V staged token-major by the fused QKV GEMM epilogue -> the dim-major paged cache.  Block =
-// 64 tokens (lane = token) x one kv head; wave w moves dims [32w, 32w + 32): per dim ONE store
-// instruction writes that dim of 64 tokens -- consecutive slots of a prefill chunk land in the
-// same 32-B page row, decode rows in separate pages.  Spread over M/64 x Hkv workgroups (the
-// whole chip) instead of the few V-column tiles of the GEMM, whose 2-B page-row stores made
-// them the launch's tail (profiles/r03_gemm_fourwave.md, "fused QKV").
-__global__ void __launch_bounds__(256) v_scatter_kernel(const uint16_t* __restrict__ v_tmp,
-                                                         uint16_t* __restrict__ v_cache,
-                                                         const int* __restrict__ slots, int M, int Hkv,
-                                                         int BS) {
-  constexpr int D = 128;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m = blockIdx.x * 64 + lane, kh = blockIdx.y;
-  if (m >= M) return;
-  const int slot = slots[m];
-  if (slot < 0) return;
-  const u32x4* src = reinterpret_cast<const u32x4*>(v_tmp + ((size_t)m * Hkv + kh) * D + w * 32);
-  u32x4 v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = src[i];
-  uint16_t* dst = v_cache + (((size_t)(slot / BS) * Hkv + kh) * D + w * 32) * BS + slot % BS;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      dst[(i * 8 + 2 * j) * BS] = (uint16_t)(v[i][j] & 0xffffu);
-      dst[(i * 8 + 2 * j + 1) * BS] = (uint16_t)(v[i][j] >> 16);
-    }
-}
-
-void launch_v_scatter(const uint16_t* v_tmp, uint16_t* v_cache, const int* slots, int M, int Hkv, int BS,
-                      hipStream_t st) {
-  if (M <= 0) return;
-  v_scatter_kernel<<<dim3((M + 63) / 64, Hkv), 256, 0, st>>>(v_tmp, v_cache, slots, M, Hkv, BS);
 }
 
 }  // namespace mlop

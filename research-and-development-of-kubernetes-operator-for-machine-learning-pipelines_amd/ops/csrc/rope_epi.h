@@ -1,5 +1,6 @@
-// RoPE + paged K/V cache stores from a GEMM's LDS-staged C tile (EPI_ROPE of
-// gemm.hip's kernels and gemm4.hip's four-wave kernel).
+// RoPE + paged K/V cache stores from a GEMM's LDS-staged C tile (EPI_ROPE of gemm.hip's
+// kernels).  K and V pages are both token-major [NB, Hkv, 16, 128]: a token's head is one
+// contiguous 256-B row (attention.hip reads V transposed out of LDS).
 #pragma once
 #include "common.h"
 #include "launch.h"
@@ -16,26 +17,26 @@ namespace mlop {
 template <int NT, typename At>
 __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nheads, int m0, int rows,
                                                 const RopeEpi& re, int tid) {
-  constexpr int D = 128, HALF = 64, BM = 256;
-  constexpr int QK = BM * (HALF / 8) / NT;  // (row, 8-column) items per thread, q/k heads
-  // v heads: lane -> row, so one store instruction writes a dim of 64 consecutive rows
-  // (a prefill chunk's consecutive slots: 16 tokens = one contiguous 32-B run of the
-  // dim-major [NB, Hkv, D, BS] page instead of 64 scattered 2-B writes)
-  constexpr int VD = D / (NT / BM);          // dims per thread
-  const int cq = (tid & 7) * 8, rq = tid >> 3;       // q/k item k: row rq + k * NT/8
-  const int rv = tid % BM, dv0 = (tid / BM) * VD;
+  constexpr int D = 128, HALF = 64;
+  constexpr int QK = 256 * (HALF / 8) / NT;  // (row, 8-column) items per thread and head
+  const int cq = (tid & 7) * 8, rq = tid >> 3;       // item k: row rq + k * NT/8
   const int n_rope = re.Hq + re.Hkv, n_all = re.Hq + 2 * re.Hkv;
-  const bool any_rope = head0 < n_rope, any_k = head0 + nheads > re.Hq && head0 < n_rope;
-  const bool any_v = head0 + nheads > n_rope;
-  int slot_q[QK], slot_v = -1;
+  const bool any_rope = head0 < n_rope, any_kv = head0 + nheads > re.Hq;
+  int slot_q[QK];
   float4 cs[QK][4];
+  if (any_kv) {  // K and V rows go to the same token-major page slot
+#pragma unroll
+    for (int k = 0; k < QK; ++k) {
+      const int r = rq + k * (NT / 8);
+      slot_q[k] = r < rows ? re.slots[m0 + r] : -1;
+    }
+  }
   if (any_rope) {
     int p[QK];
 #pragma unroll
     for (int k = 0; k < QK; ++k) {
       const int r = rq + k * (NT / 8);
       p[k] = r < rows ? re.pos[m0 + r] : 0;
-      slot_q[k] = (any_k && r < rows) ? re.slots[m0 + r] : -1;
     }
 #pragma unroll
     for (int k = 0; k < QK; ++k) {
@@ -46,7 +47,6 @@ __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nhe
       cs[k][3] = row[(HALF + cq) / 4 + 1];
     }
   }
-  if (any_v && rv < rows && re.v_tmp == nullptr) slot_v = re.slots[m0 + rv];
   for (int hh = 0; hh < nheads; ++hh) {
     const int head = head0 + hh;
     if (head >= n_all) break;
@@ -78,14 +78,15 @@ __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nhe
         *reinterpret_cast<u32x4*>(dst + cq) = oa;
         *reinterpret_cast<u32x4*>(dst + HALF + cq) = ob;
       }
-    } else if (re.v_tmp != nullptr) {
-      // token-major staging: 16-B stores of whole 8-dim chunks (launch_v_scatter pages them)
+    } else {
+      // V head: the token's row of its token-major page [NB, Hkv, BS, 128], 16-B stores
       const int kh = head - n_rope;
 #pragma unroll
       for (int k = 0; k < QK; ++k) {
         const int r = rq + k * (NT / 8);
-        if (r >= rows) continue;
-        uint16_t* dst = re.v_tmp + ((size_t)(m0 + r) * re.Hkv + kh) * D;
+        const int slot = slot_q[k];
+        if (r >= rows || slot < 0) continue;
+        uint16_t* dst = re.v_cache + (((size_t)(slot / re.BS) * re.Hkv + kh) * re.BS + slot % re.BS) * D;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           u32x4 o;
@@ -96,14 +97,6 @@ __device__ __forceinline__ void rope_tile_store(const At& at, int head0, int nhe
           }
           *reinterpret_cast<u32x4*>(dst + half * HALF + cq) = o;
         }
-      }
-    } else {
-      const int kh = head - n_rope;
-      if (slot_v >= 0) {
-        uint16_t* dst = re.v_cache + (((size_t)(slot_v / re.BS) * re.Hkv + kh) * D + dv0) * re.BS +
-                        slot_v % re.BS;
-#pragma unroll 16
-        for (int j = 0; j < VD; ++j) dst[j * re.BS] = f2bf(at(rv, hh * D + dv0 + j));
       }
     }
   }

@@ -3,7 +3,7 @@
 They are the numerics oracle of the GPU tests (``tests/test_kernels_gpu.py``)
 and the execution path for CPU tensors, so the scheduler / engine / TP logic is
 unit-testable in a GPU-less container.  Layouts match the kernels exactly:
-``k_cache[NB, Hkv, BS, D]`` (token-major) and ``v_cache[NB, Hkv, D, BS]``.
+``k_cache[NB, Hkv, BS, D]`` and ``v_cache[NB, Hkv, BS, D]`` (both token-major).
 """
 from __future__ import annotations
 
@@ -61,7 +61,7 @@ def rope_cache(qkv, positions, cos_sin, slots, k_cache, v_cache, n_q_heads):
             continue
         b, o = divmod(s, BS)
         k_cache[b, :, o, :] = k[t]
-        v_cache[b, :, :, o] = v[t]
+        v_cache[b, :, o, :] = v[t]
     return q
 
 
@@ -74,7 +74,7 @@ def gather_kv(k_cache, v_cache, block_table, n):
         z = torch.zeros(0, Hkv, D, dtype=k_cache.dtype, device=k_cache.device)
         return z, z
     k = torch.cat([k_cache[p].permute(1, 0, 2) for p in pages], 0)[:n]          # [n, Hkv, D]
-    v = torch.cat([v_cache[p].permute(2, 0, 1) for p in pages], 0)[:n]          # [n, Hkv, D]
+    v = torch.cat([v_cache[p].permute(1, 0, 2) for p in pages], 0)[:n]          # [n, Hkv, D]
     return k, v
 
 

@@ -81,7 +81,7 @@ async def _create_and_wait_ready(kube, ctl, batch: int, ready_timeout_s: float) 
                 raise RuntimeError(f"predictor {p.predictor} failed to start: {p.extra['error']}")
         return (o.get("status") or {}).get("ready") == "True"
 
-    await wait_for(ready, ready_timeout_s, poll_s=0.05)
+    await wait_for(ready, ready_timeout_s, poll_s=0.01)
     cr_ready = time.perf_counter() - t0
     pod = next(iter(ctl.pods.values()))
     return {"cr_ready_process_s": round(cr_ready, 3), "predictor_process_ready_s": round(pod.extra.get("ready_s", 0.0), 3),

@@ -2,7 +2,8 @@
 
 Device side: one K and one V tensor per layer, pages of 16 tokens:
   k[layer] : [num_blocks, Hkv, 16, D]   (token-major: A operand of S^T = K.Q^T)
-  v[layer] : [num_blocks, Hkv, D, 16]   (dim-major:  A operand of O^T = V^T.P^T)
+  v[layer] : [num_blocks, Hkv, 16, D]   (token-major too: a token's row is one contiguous
+                                          store; attention.hip reads V^T out of LDS transposed)
 zeroed before first use (the attention kernel relies on finite unused slots).
 
 Two ways to back it:
@@ -64,7 +65,7 @@ class KVCache:
         else:
             self.k_all = torch.empty(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
                                      device=device, dtype=dtype)
-            self.v_all = torch.empty(num_layers, num_blocks, num_kv_heads, head_dim, BLOCK_SIZE,
+            self.v_all = torch.empty(num_layers, num_blocks, num_kv_heads, BLOCK_SIZE, head_dim,
                                      device=device, dtype=dtype)
             _sync(device)
             t1 = time.perf_counter()
@@ -93,7 +94,7 @@ class KVCache:
         base = self._flat.view(self.dtype)
         rs = region // esz
         self.k_all = base.as_strided((L, self.num_blocks, Hkv, BLOCK_SIZE, D), (rs, page, BLOCK_SIZE * D, D, 1), 0)
-        self.v_all = base.as_strided((L, self.num_blocks, Hkv, D, BLOCK_SIZE), (rs, page, D * BLOCK_SIZE, BLOCK_SIZE, 1),
+        self.v_all = base.as_strided((L, self.num_blocks, Hkv, BLOCK_SIZE, D), (rs, page, BLOCK_SIZE * D, D, 1),
                                      L * rs)
         if initial_blocks is None:
             initial_blocks = max(2, INITIAL_BYTES // (n_regions * page_bytes))

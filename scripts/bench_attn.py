@@ -51,7 +51,7 @@ if m.nparts > 1:
 m.part_o = torch.empty(B * Hkv * m.nparts * 16 * D, device=dev)
 m.part_ml = torch.empty(B * Hkv * m.nparts * 16 * 2, device=dev)
 kc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
-vc = torch.randn(NB, Hkv, D, BS, device=dev, dtype=bf)
+vc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
 q = torch.randn(B, Hq, D, device=dev, dtype=bf)
 out = torch.empty_like(q)
 for _ in range(3):

@@ -40,7 +40,7 @@ for B, L in cases:
     ctx = np.random.randint(max(16, L // 2), L * 3 // 2 + 1, size=B).tolist()
     NB = sum((c + 15) // 16 for c in ctx) + 8
     kc = torch.randn(NB, Hkv, 16, D, device=dev, dtype=bf)
-    vc = torch.randn(NB, Hkv, D, 16, device=dev, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, D, device=dev, dtype=bf)
     m, T = make_meta(dev, [1] * B, ctx, Hkv, Hq // Hkv, NB)
     nparts = m.nparts
     q = torch.randn(T, Hq, D, device=dev, dtype=bf)

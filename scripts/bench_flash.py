@@ -46,7 +46,7 @@ m.ptile_seq, m.ptile_q0 = d(pts), d(ptq)
 m.part_tokens, m.nparts = L, 1
 m.part_o = m.part_ml = torch.empty(1, device=dev)
 kc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
-vc = torch.randn(NB, Hkv, D, BS, device=dev, dtype=bf)
+vc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
 q = torch.randn(S * L, Hq, D, device=dev, dtype=bf)
 out = torch.empty_like(q)
 for _ in range(3):

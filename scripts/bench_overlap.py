@@ -39,7 +39,7 @@ class Half:
         ctx = np.random.randint(CTX // 2, CTX * 3 // 2 + 1, size=B).tolist()
         NB = sum((c + 15) // 16 for c in ctx) + 8
         self.kc = torch.randn(NB, Hkv, 16, D, device=dev, dtype=bf)
-        self.vc = torch.randn(NB, Hkv, D, 16, device=dev, dtype=bf)
+        self.vc = torch.randn(NB, Hkv, 16, D, device=dev, dtype=bf)
         self.meta, T = make_meta(dev, [1] * B, ctx, Hkv, Hq // Hkv, NB)
         self.q = torch.randn(T, Hq, D, device=dev, dtype=bf)
         self.x = torch.randn(M, H, device=dev, dtype=bf)

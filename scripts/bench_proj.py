@@ -85,7 +85,7 @@ for M in Ms:
     pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
     slots = torch.randperm(NB * BS, device=dev)[:M].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=dev, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=bf)
     cases = {
         "qkv": lambda: ops.qkv_rope_cache(x, w_qkv, pos, cs, slots, kc, vc, Hq),
         "gate_up": lambda: ops.gemm(x, w_gu, epi=ops.EPI_SILU_MUL),

@@ -38,7 +38,7 @@ for M in [int(m) for m in os.environ.get("BENCH_MS", "512,1024,2048,3072,4096").
     pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
     slots = torch.randperm(NB * BS, device=dev)[:M].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.zeros(NB, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
     q = torch.empty(M, Hq, D, device=dev, dtype=torch.bfloat16)
     fused = lambda: torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)  # noqa: E731
     unf = lambda: ops.rope_cache(torch.matmul(x, w.t()), pos, cs, slots, kc, vc, Hq, q)  # noqa: E731

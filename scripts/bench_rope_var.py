@@ -40,7 +40,7 @@ for M in [int(m) for m in os.environ.get("BENCH_MS", "4088,2048").split(",")]:
     pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
     slots = torch.randperm(NB * BS, device=dev)[:M].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.zeros(NB, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
     q = torch.empty(M, Hq, D, device=dev, dtype=torch.bfloat16)
     res = {}
     for _ in range(3):

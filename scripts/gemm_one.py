@@ -29,7 +29,7 @@ if epi == 3:
     pos = torch.randint(0, 8000, (M,), device="cuda", dtype=torch.int32)
     slots = torch.randperm(NB * BS, device="cuda")[:M].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
-    vc = torch.zeros(NB, Hkv, D, BS, device="cuda", dtype=torch.bfloat16)
+    vc = torch.zeros(NB, Hkv, BS, D, device="cuda", dtype=torch.bfloat16)
 for _ in range(iters):
     if be == "mlop" and epi == 3:
         ops.qkv_rope_cache(x, w, pos, cs, slots, kc, vc, Hq)

@@ -74,7 +74,7 @@ def test_w4_qkv_rope_cache(gpu, w4, M, Hq, Hkv):
     slots[5] = -1
     slots[M - 1] = -1
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
     assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
     qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()

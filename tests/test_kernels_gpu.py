@@ -60,7 +60,7 @@ def test_rope_cache(gpu, Hq, Hkv):
     slots = torch.randperm(NB * BS, device=gpu)[:T].to(torch.int32)
     slots[3] = -1
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     kc2, vc2 = kc.clone(), vc.clone()
     q = ops.rope_cache(qkv, pos, cs, slots, kc, vc, Hq)
     q_ref = ref.rope_cache(qkv.cpu(), pos.cpu(), cs.cpu(), slots.cpu(), kc2.cpu(), vc2.cpu(), Hq)
@@ -98,7 +98,7 @@ def test_qkv_rope_cache_fused(gpu, M, Hq, Hkv):
     try:
         assert torch.ops.mlop.gemm_rope_supported(M, N, K)
         kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-        vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+        vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
         q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
         assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
         qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
@@ -178,7 +178,7 @@ def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
     G = Hq // Hkv
     NB = sum((c + 15) // 16 for c in ctx_lens) + 8
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, flash_min_q=17)
     assert m.ptile_seq.numel() > 0
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
@@ -203,7 +203,7 @@ def test_paged_attention(gpu, Hq, Hkv, case):
     else:  # forced split-KV with a reduce pass
         q_lens, ctx_lens = [1, 1, 3], [1500, 33, 900]
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     kw = dict(part_tokens=256, nparts=6) if case.startswith("split") else {}
     m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, **kw)
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
@@ -231,7 +231,7 @@ def test_paged_attention_padded_bucket(gpu, fused):
     Hq, Hkv, NB = 32, 8, 400
     q_lens, ctx_lens = [1, 1, 3, 1, 1], [1500, 33, 900, 0, 0]
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, Hq // Hkv, NB, part_tokens=256, nparts=6,
                      shuffle_rows=False)
     if fused:
@@ -252,7 +252,7 @@ def test_attention_spike_rescale(gpu):
     """Force the online-softmax rescale branch: a late key dominates."""
     Hq, Hkv = 32, 8
     kc = 0.1 * torch.randn(100, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(100, Hkv, 128, 16, device=gpu, dtype=bf)
+    vc = torch.randn(100, Hkv, 16, 128, device=gpu, dtype=bf)
     m, T = make_meta(gpu, [1, 4], [600, 700], Hkv, 4, 100, shuffle_rows=False)
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
     bt = m.block_tables.cpu()
@@ -531,8 +531,8 @@ def test_gemv_silu_mul(gpu, M, I, K):
 
 @pytest.mark.parametrize("consecutive", [False, True])
 def test_qkv_rope_fused_in_graph(gpu, consecutive):
-    """Large-M fused QKV+RoPE (V staged token-major in a caching-allocator tensor, then paged by
-    the chip-wide scatter) captured in a hipGraph and replayed with new positions / slots:
+    """Large-M fused QKV+RoPE (K rotated, K and V rows stored into their token-major pages
+    from the GEMM epilogue) captured in a hipGraph and replayed with new positions / slots:
     replay == eager reference.  Consecutive slots = a prefill chunk; random = decode rows."""
     from mlopamd.models.layers import rope_table
 
@@ -546,9 +546,9 @@ def test_qkv_rope_fused_in_graph(gpu, consecutive):
     pos = torch.zeros(M, device=gpu, dtype=torch.int32)
     slots = torch.zeros(M, device=gpu, dtype=torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
-    assert torch.ops.mlop.gemm_rope_stages_v(M, N, K)
+    assert torch.ops.mlop.gemm_rope_supported(M, N, K)
     torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)  # warm-up outside capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -586,7 +586,7 @@ def test_gemv_rope_cache(gpu, M, Hq, Hkv):
         slots[1] = -1  # padding row: no cache write
     assert torch.ops.mlop.gemm_rope_supported(M, N, K)
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     q = torch.empty(M, Hq, D, device=gpu, dtype=bf)
     assert torch.ops.mlop.gemm_rope_cache(q, kc, vc, x, w, pos, cs, slots)
     qkv_ref = (x.float() @ w.float().t()).to(bf).cpu()
@@ -863,7 +863,7 @@ def test_norm_qkv_rope_fused(gpu, M, Hq, Hkv):
     pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
     slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     ops.NORM_FUSION = True
     try:
         q, r2 = ops.norm_qkv_rope_cache(y, res.clone(), nw, w, pos, cs, slots, kc, vc, Hq, 1e-5)

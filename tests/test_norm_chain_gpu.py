@@ -88,7 +88,7 @@ def test_gemm_rs_rope(gpu, w4, M):
     ss = ops.ss_buffer(M, H, gpu).fill_(float("nan"))
     ops.ss_parts(ss, M, H)[1].copy_(x.float().pow(2).sum(-1))
     kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, D, BS, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
     q = ops.qkv_rope_cache_rs(x, w, pos, cs, slots, kc, vc, Hq, ss, EPS)
     qkv_ref = (_unit_norm(x) @ w.float().t()).to(bf).cpu()
     kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()

@@ -129,7 +129,7 @@ def test_split_kv_fused_combine_under_contention(gpu):
     q_lens = [1] * 12
     ctx_lens = [1500, 33, 900, 1400, 17, 1024, 1530, 640, 1, 1200, 777, 1499]
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
-    vc = torch.randn(NB, Hkv, 128, 16, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     m, T = make_meta(gpu, q_lens, ctx_lens, Hkv, Hq // Hkv, NB, part_tokens=256, nparts=6)
     m.part_sem = torch.zeros(m.tile_seq.numel() * Hkv, dtype=torch.int32, device=gpu)
     q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
