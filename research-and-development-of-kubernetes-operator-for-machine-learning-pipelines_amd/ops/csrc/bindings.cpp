@@ -626,6 +626,7 @@ void car_all_gather(int64_t h, Tensor out, Tensor piece) {
   c10::DeviceGuard g(piece.device());
   mlop::car_all_gather((long)h, out.data_ptr(), piece.data_ptr(), nbytes, cur_stream());
 }
+int64_t gemv_addnorm_enable(int64_t on) { return mlop::gemv_addnorm_enable((int)on); }
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
@@ -702,6 +703,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
   m.def("car_all_gather(int h, Tensor(a!) out, Tensor piece) -> ()");
   m.def("car_error(int h) -> int", &car_error);
+  m.def("gemv_addnorm_enable(int on) -> int", &gemv_addnorm_enable);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("chan_create(str name, int slots, int consumers) -> int", &chan_create);

@@ -152,6 +152,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int m = 0; m < M; ++m) ss[m] = 0.f;
   const bool writer = NORM && (KW == 1 ? set == 0 : blockIdx.x == 0);
 
+  // EPI_ROPE: the epilogue's per-row slot, position and the position's cos / sin are loaded
+  // right after the first weight loads are issued, so their round trips (position -> cos / sin
+  // is a dependent pair) run under the weight stream instead of after the dot products (lane m
+  // holds row m's values; only the waves that store load them)
+  const bool rope_lane = EPI == EPI_ROPE && (KW == 1 || wv == 0) && lane < M;
+  int pf_slot = -1;
+  float pf_c = 0.f, pf_s = 0.f;
+  const int rope_d = (set % (kHeadD / 2));
+  const bool rope_set = EPI == EPI_ROPE && set < (re.Hq + re.Hkv) * (kHeadD / 2);
   const int lane_off = (KW == 1 ? 0 : wv * 64) + lane;
   constexpr int STEP = 64 * KW;  // chunk stride between a lane's consecutive loads
   for (int c0 = 0; c0 < KC; c0 += STEP * U) {
@@ -184,6 +193,16 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       } else {
 #pragma unroll
         for (int m = 0; m < M; ++m) x[u][m] = (ok && m < mc) ? Av[m][c] : u32x4{0, 0, 0, 0};
+      }
+    }
+    if constexpr (EPI == EPI_ROPE) {
+      if (c0 == 0 && rope_lane) {  // issued behind the weight loads
+        pf_slot = re.slots[lane];
+        if (rope_set) {
+          const float* cs = re.cos_sin + (size_t)re.pos[lane] * kHeadD;
+          pf_c = cs[rope_d];
+          pf_s = cs[kHeadD / 2 + rope_d];
+        }
       }
     }
 #pragma unroll
@@ -250,12 +269,11 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       if (lane != m) continue;
-      const int slot = re.slots[m];
+      const int slot = pf_slot;
       const int blk = slot >= 0 ? slot / re.BS : 0, off = slot >= 0 ? slot % re.BS : 0;
       if (set < rope_sets) {
         const int h = set / (kHeadD / 2), d = set % (kHeadD / 2);
-        const float* cs = re.cos_sin + (size_t)re.pos[m] * kHeadD;
-        const float c = cs[d], s = cs[kHeadD / 2 + d];
+        const float c = pf_c, s = pf_s;
         const float x = bf2f(f2bf(acc[0][m])), y = bf2f(f2bf(acc[1][m]));
         const uint16_t oa = f2bf(x * c - y * s), ob = f2bf(y * c + x * s);
         uint16_t* dst;
@@ -532,13 +550,21 @@ void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offse
 // The epilogue form: residual add + RMSNorm fused into the projection that PRODUCES the
 // residual update (O, down), so the batch-1..4 decode step loses its 64 separate add_rmsnorm
 // launches (~4.7 us each, profiles/r01_decode_small_batch.md) for one small tail per launch.
+// measured (scripts/history/r4_b1.sh, profiles/r04_decode_small_batch.md): the fused tail costs
+// what the separate norm launch did (its three dependent round trips + the grid ticket ~= the
+// norm kernel's latency), batch 1 329 vs 351 tok/s, batch 4 952 vs 1090: off by default
+// (MLOP_GEMV_ADDNORM=1, or gemv_addnorm_enable() in-process: the GPU tests keep it verified)
+static int g_gemv_addnorm = -1;
+int gemv_addnorm_enable(int on) {
+  if (g_gemv_addnorm < 0) g_gemv_addnorm = env_int("MLOP_GEMV_ADDNORM", 0);
+  const int prev = g_gemv_addnorm;
+  if (on >= 0) g_gemv_addnorm = on ? 1 : 0;
+  return prev;
+}
+
 long gemv_addnorm_ws_floats(int M, int N, int K) {
   // whole row sets in every wave of every workgroup (the grid ticket needs no early exits)
-  // measured (scripts/history/r4_b1.sh, profiles/r04_decode_small_batch.md): the fused tail costs
-  // what the separate norm launch did (its three dependent round trips + the grid ticket ~= the
-  // norm kernel's latency), batch 1 329 vs 351 tok/s, batch 4 952 vs 1090: off by default
-  static const int on = env_int("MLOP_GEMV_ADDNORM", 0);
-  if (!on || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
+  if (!gemv_addnorm_enable(-1) || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
   return (long)(N / 2) * M + (long)(N / 2) * M;  // partials (>= sets x M, R = 2 or 4) + the bf16 residual copy
 }
 

@@ -102,6 +102,8 @@ struct NormPro {
 // epilogue form, M <= 4): residual <- bf16(residual + bf16(A.B^T)); out <- rmsnorm(residual) * w.
 // ws: gemv_addnorm_ws_floats(M, N, K) floats; false = shape not on this path.
 long gemv_addnorm_ws_floats(int M, int N, int K);
+// the epilogue's opt-in switch: on = 0 / 1 sets it, -1 queries; returns the previous state
+int gemv_addnorm_enable(int on);
 bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
                          float* ws, long ws_floats, int M, int N, int K, hipStream_t st);
 bool gemv_norm_takes(int M, int N, int K, int epi);

@@ -37,3 +37,16 @@ def pp_variant(gpu):
         yield
     finally:
         torch.ops.mlop.gemm_big_variant(prev)
+
+
+@pytest.fixture
+def gemv_addnorm_on(gpu):
+    """Turn the opt-in GEMV add + RMSNorm epilogue on for the test (off by default: a measured
+    loss, profiles/r04_decode_small_batch.md), so its numerics and race tests keep running."""
+    import torch
+
+    prev = torch.ops.mlop.gemv_addnorm_enable(1)
+    try:
+        yield
+    finally:
+        torch.ops.mlop.gemv_addnorm_enable(prev)

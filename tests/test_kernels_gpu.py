@@ -266,9 +266,12 @@ def test_attention_spike_rescale(gpu):
 @pytest.mark.parametrize("n,V", [(1, 128256), (2, 128256), (64, 128256), (5, 32000), (100, 32000), (3, 1000),
                                  (2, 1003), (1, 16040)])
 def test_argmax(gpu, n, V, dtype):
-    if V % (8 if dtype == torch.bfloat16 else 4):
-        pytest.skip("rows must be 16-B aligned")
     x = torch.randn(n, V, device=gpu).to(dtype)
+    if V % (8 if dtype == torch.bfloat16 else 4):
+        # rows that are not 16-B aligned are refused loudly, never read misaligned
+        with pytest.raises(RuntimeError, match="16-B aligned"):
+            ops.argmax(x)
+        return
     if dtype == torch.bfloat16:
         x[:, 7] = x.max()  # exact ties (common in bf16): the smallest index wins, as in torch
     assert torch.equal(ops.argmax(x).cpu(), x.float().argmax(-1).cpu())
@@ -881,14 +884,13 @@ def test_norm_qkv_rope_fused(gpu, M, Hq, Hkv):
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (2, 4096, 14336), (3, 4096, 4096), (4, 8192, 1024),
                                    (1, 1024, 4096)])
-def test_gemv_add_rmsnorm_epilogue(gpu, M, N, K):
+def test_gemv_add_rmsnorm_epilogue(gpu, gemv_addnorm_on, M, N, K):
     """Decode sizes: residual add + RMSNorm as the GEMV's epilogue (grid ticket, the last
     workgroup normalises): residual bit-equal to GEMV -> add_rmsnorm (same roundings), the normed
     output vs the fp32 oracle, relaunch bit-identical (partials summed in a fixed order; the
     ticket re-arms), and inside a captured graph."""
     torch.manual_seed(M * N + K)
-    if torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) == 0:
-        pytest.skip("GEMV add + RMSNorm epilogue is opt-in (MLOP_GEMV_ADDNORM=1)")
+    assert torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) > 0
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
     res = torch.randn(M, N, device=gpu, dtype=bf)

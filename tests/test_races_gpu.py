@@ -173,14 +173,13 @@ def test_w4_gemm_under_contention(gpu, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (4, 4096, 14336), (2, 8192, 1024)])
-def test_gemv_add_rmsnorm_ticket_under_contention(gpu, M, N, K):
+def test_gemv_add_rmsnorm_ticket_under_contention(gpu, gemv_addnorm_on, M, N, K):
     """The decode GEMV's add + RMSNorm epilogue (gemv.hip EPI_ADDNORM): sc1 scratch copies of the
     new residual + sc1 row partials, one relaxed agent ticket per workgroup, the last workgroup
     normalises with sc1 loads and re-arms the ticket.  Every launch under a racing GEMM stream
     must give the quiet launch's bits (residual and normed output)."""
     torch.manual_seed(N + K + M)
-    if torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) == 0:
-        pytest.skip("GEMV add + RMSNorm epilogue is opt-in (MLOP_GEMV_ADDNORM=1)")
+    assert torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) > 0
     x = torch.randn(M, K, device=gpu, dtype=bf)
     w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
     res0 = torch.randn(M, N, device=gpu, dtype=bf)
