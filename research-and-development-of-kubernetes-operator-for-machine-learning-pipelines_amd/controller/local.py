@@ -177,6 +177,9 @@ class ProcessLauncher:
             gpus = 8  # CPU emulation of an 8-GPU node: device indices are labels only
         self.gpus = GpuPool(gpus) if isinstance(gpus, int) else (gpus or GpuPool.detect())
         self.gpu_resource = gpu_resource
+        # the readiness probe's HTTP client, imported now: a kubelet is a running process, and a
+        # first `import aiohttp` (0.15-0.3 s) inside start() would be charged to every CR -> ready
+        import aiohttp  # noqa: F401
 
     def command(self, pod: Pod, port: int) -> list[str]:
         c = _container_of(pod.spec)

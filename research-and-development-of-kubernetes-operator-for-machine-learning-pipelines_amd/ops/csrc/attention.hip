@@ -90,8 +90,9 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int part_tokens,
     int nparts, int num_blocks, int* __restrict__ sem) {
   constexpr int QT = 16 / G;
-  // wave w stages its page pair's V (2 x 16 token rows x 256 B = 8 KB) inside sm_o[w]
-  // (8448 B, 256-B aligned: vt_frag), which it alone writes after its loop
+  // wave w stages its page pair's V image (2 x 16 token rows x 256 B = 8 KB) inside sm_o[w]
+  // (8448 B, 256-B aligned: vt_frag), which it alone writes after its loop.  (A second image per
+  // wave, prefetching the next pair, measured 1-4 % SLOWER on every decode shape: r04 profile.)
   __shared__ __attribute__((aligned(256))) float sm_o[4][16][kD + 4];
   __shared__ float sm_m[4][16];
   __shared__ float sm_l[4][16];
@@ -146,14 +147,32 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
   const int n_pages = (p_end + kBS - 1) / kBS;
   const size_t page_stride = (size_t)Hkv * kBS * kD;
 
+  // (a generic pointer's low 32 bits are the LDS offset)
+  const uint32_t vimg = (uint32_t)(uintptr_t)&sm_o[0][0][0] + wid * 8448u;
+  // clamp: a corrupt block table must not become an out-of-bounds fault
+  auto page_a = [&](int pp) { return min(max(bt[2 * pp], 0), num_blocks - 1); };
+  auto page_b = [&](int pp, int pa) { return (2 * pp + 1 < n_pages) ? min(max(bt[2 * pp + 1], 0), num_blocks - 1) : pa; };
+  // the pair's 32 token rows of this kv head by LDS-DMA into this wave's V image
+  auto issue_v = [&](int pa, int pb) {
+    const uint16_t* vA = vc + pa * page_stride + (size_t)kvh * kBS * kD;
+    const uint16_t* vB = vc + pb * page_stride + (size_t)kvh * kBS * kD;
+    const uint32_t dst = vimg;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int trow = (4 * i + g4) & 15;
+      const uint16_t* src = (i < 4 ? vA : vB) + trow * kD + ((r ^ vswz(trow)) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(dst + 1024u * i), 16, 0, 0);
+    }
+  };
+  // page ids one pair ahead: the block-table loads of pair pp + 4 run under pair pp
+  int pgA = 0, pgB = 0;
+  if (pp_begin + wid < pp_end) {
+    pgA = page_a(pp_begin + wid);
+    pgB = page_b(pp_begin + wid, pgA);
+  }
   for (int pp = pp_begin + wid; pp < pp_end; pp += 4) {
-    // clamp: a corrupt block table must not become an out-of-bounds fault
-    const int pgA = min(max(bt[2 * pp], 0), num_blocks - 1);
-    const int pgB = (2 * pp + 1 < n_pages) ? min(max(bt[2 * pp + 1], 0), num_blocks - 1) : pgA;
     const uint16_t* kA = kc + pgA * page_stride + (size_t)kvh * kBS * kD;
     const uint16_t* kB = kc + pgB * page_stride + (size_t)kvh * kBS * kD;
-    const uint16_t* vA = vc + pgA * page_stride + (size_t)kvh * kD * kBS;
-    const uint16_t* vB = vc + pgB * page_stride + (size_t)kvh * kD * kBS;
 
     // K rows of MFMA row r: pair tokens 8*(r>>2) + (r&3) (first S MFMA) and +4 (second)
     const uint16_t* kR = (r >> 3 ? kB : kA) + (8 * ((r >> 2) & 1) + (r & 3)) * kD;
@@ -163,22 +182,15 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       ka[kk] = *reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8);
       kb[kk] = *reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8);
     }
-    // V^T fragment of lane group g4: dims d*16 + r, pair tokens 8*g4 .. 8*g4+7 (16 B)
-    bf16x8 vf8[8];
-    // (a generic pointer's low 32 bits are the LDS offset)
-    const uint32_t vimg = (uint32_t)(uintptr_t)&sm_o[0][0][0] + wid * 8448u;
-    {
-      // the pair's 32 token rows by LDS-DMA into this wave's image, issued after the K loads
-      // (the S MFMAs wait for those only); the previous pair's transposed reads are complete
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int trow = (4 * i + g4) & 15;
-        const uint16_t* src = (i < 4 ? vA : vB) + trow * kD + ((r ^ vswz(trow)) << 3);
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(vimg + 1024u * i), 16, 0, 0);
-      }
+    // this pair's V image, issued behind the K loads (the S MFMAs wait for those only; the
+    // previous pair's transposed reads are complete: their MFMAs consumed them)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    issue_v(pgA, pgB);
+    if (pp + 4 < pp_end) {
+      pgA = page_a(pp + 4);
+      pgB = page_b(pp + 4, pgA);
     }
-
+    bf16x8 vf8[8];
     // S^T[token][row]: lane holds row r, tokens 4*g4 + i of each page
     f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

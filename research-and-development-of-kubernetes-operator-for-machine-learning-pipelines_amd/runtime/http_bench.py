@@ -85,6 +85,8 @@ async def _create_and_wait_ready(kube, ctl, batch: int, ready_timeout_s: float) 
     cr_ready = time.perf_counter() - t0
     pod = next(iter(ctl.pods.values()))
     return {"cr_ready_process_s": round(cr_ready, 3), "predictor_process_ready_s": round(pod.extra.get("ready_s", 0.0), 3),
+            # CR create -> the launcher's spawn (operator reconcile, SeldonDeployment, GPU grant)
+            "predictor_spawn_s": round(pod.extra.get("t_start", t0) - t0, 3),
             "predictor_gpus": pod.extra.get("gpus"), "pod": pod}
 
 
@@ -115,6 +117,7 @@ async def cr_ready_process(model: str = "llama3-8b", batch: int = 2048, engine_e
     n = len(vals)
     p50 = vals[n // 2] if n % 2 else 0.5 * (vals[n // 2 - 1] + vals[n // 2])
     return {"p50_cr_ready_process_s": round(p50, 3), "cr_ready_process_samples_s": vals,
+            "predictor_spawn_s": last.get("predictor_spawn_s"),
             "predictor_process_ready_s": last.get("predictor_process_ready_s"),
             "predictor_gpus": last.get("predictor_gpus"), "predictor_startup": last.get("predictor_startup")}
 

@@ -53,6 +53,35 @@ def _since_process_start() -> float:
 
 STARTUP["server_module_imported_s"] = _since_process_start()
 
+
+def _warm_hip() -> None:
+    """Initialise the HIP runtime and this rank's device context on a helper thread WHILE torch
+    imports (~1.4 s of Python and dlopen): the C calls release the GIL, and torch's own first
+    device call then finds the runtime up (first allocation 0.15-0.35 s -> ~0.1 s,
+    scripts/probe_startup.py).  Off for CPU predictors and with MLOP_HIP_WARMUP=0."""
+    import ctypes
+    import importlib.util
+
+    try:
+        # torch's OWN copy of the runtime (its lib/ directory, found without importing torch): a
+        # bare "libamdhip64.so" could resolve to the system ROCm copy, and a second HIP runtime
+        # in the process would not be the one torch and _C.so launch on
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.origin:
+            return
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so"))
+        if lib.hipInit(0) == 0 and lib.hipSetDevice(int(os.environ.get("LOCAL_RANK", "0"))) == 0:
+            lib.hipFree(ctypes.c_void_p(0))  # creates the device context
+        STARTUP["hip_warm_s"] = _since_process_start()
+    except OSError:
+        pass
+
+
+if os.environ.get("MLOP_DEVICE", "cuda") != "cpu" and os.environ.get("MLOP_HIP_WARMUP", "1") != "0":
+    import threading
+
+    threading.Thread(target=_warm_hip, name="hip-warmup", daemon=True).start()
+
 from .sampler import SamplingParams  # noqa: E402 (imports torch: timed below)
 
 STARTUP["torch_imported_s"] = _since_process_start()

@@ -244,3 +244,26 @@ def test_kernel_time_shares_exported():
     m.update_kernel_shares(sh)
     txt = m.exposition().decode()
     assert 'mlop_kernel_time_fraction{' in txt and 'kernel="attention"' in txt
+
+
+def test_hip_warmup_loads_torchs_own_runtime():
+    """The predictor's start-up thread initialises HIP while torch imports (server._warm_hip).  It
+    must load torch's OWN libamdhip64 (torch/lib): a second HIP runtime in the process (e.g. the
+    system ROCm copy) would not be the one torch and _C.so launch on.  After the server module,
+    torch and the extension are loaded, exactly one HIP runtime file is mapped."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import time, mlopamd.runtime.server as s; time.sleep(0.5); from mlopamd import ops; ops.load(); "
+            "print(sorted({l.split()[-1] for l in open('/proc/self/maps') if 'amdhip' in l}))")
+    env = {k: v for k, v in os.environ.items() if k not in ("MLOP_DEVICE", "MLOP_HIP_WARMUP")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import ast
+
+    maps = ast.literal_eval(out.stdout.strip().splitlines()[-1])
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    assert len(maps) == 1 and maps[0].startswith(torch_lib), maps
