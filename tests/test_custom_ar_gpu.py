@@ -103,6 +103,31 @@ def _worker(rank, world, port, out_dir):
             car.all_reduce(y)
             torch.cuda.synchronize()
             res["gather"].append(torch.equal(got.cpu(), torch.stack(pieces)) and torch.equal(y.cpu(), _oracle(xs)))
+        # under contention: a side stream keeps a GEMM running on this rank (uneven, per-iteration
+        # amounts) while all-reduce, broadcast and all-gather run their flag protocols
+        res["contention"] = []
+        side = torch.cuda.Stream()
+        na = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        nc = torch.empty_like(na)
+        for it in range(12):
+            with torch.cuda.stream(side):
+                for _ in range(1 + (it + rank) % 3):
+                    torch.matmul(na, na, out=nc)
+            xs = _inputs(600 + it, 64 * 1024 + 8 * it, world)
+            x = xs[rank].cuda()
+            car.all_reduce(x)
+            root = it % world
+            src = torch.randint(-2 ** 31, 2 ** 31 - 1, (4096,), generator=torch.Generator().manual_seed(650 + it),
+                                dtype=torch.int32)
+            buf = src.cuda() if rank == root else torch.full((4096,), -1, dtype=torch.int32, device="cuda")
+            car.broadcast(buf, root)
+            pieces = [torch.randn(1000 + it, generator=torch.Generator().manual_seed(700 + 10 * it + p))
+                      for p in range(world)]
+            got = car.all_gather(pieces[rank].cuda())
+            torch.cuda.synchronize()
+            res["contention"].append(torch.equal(x.cpu(), _oracle(xs)) and torch.equal(buf.cpu(), src) and
+                                     torch.equal(got.cpu(), torch.stack(pieces)))
+        side.synchronize()
         # in place, back to back (parity reuse every second call)
         for it in range(6):
             xs = _inputs(50 + it, 4096, world)
@@ -157,3 +182,4 @@ def test_custom_all_reduce_two_processes_one_gpu():
         assert all(res["two_shot"]), (r, res["two_shot"])
         assert all(res["bcast"]), (r, res["bcast"])
         assert all(res["gather"]), (r, res["gather"])
+        assert all(res["contention"]), (r, res["contention"])
