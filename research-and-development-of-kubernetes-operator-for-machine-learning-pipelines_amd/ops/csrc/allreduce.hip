@@ -65,7 +65,8 @@ struct CarState {
   size_t max_bytes = 0;  // per parity
   uint8_t* buf = nullptr;
   uint32_t* epochs = nullptr;
-  int* err = nullptr;
+  int* err = nullptr;       // device alias of err_host
+  int* err_host = nullptr;
   Peers peers{};
 };
 
@@ -124,7 +125,7 @@ __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restr
       long spins = 0;
       while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
         if (++spins > kMaxSpins) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -201,7 +202,7 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
     long spins = 0;
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (++spins > kMaxSpins) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -308,7 +309,7 @@ __global__ void __launch_bounds__(kThreads) car_bcast_kernel(uint4* __restrict__
     long spins = 0;
     while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (++spins > kMaxSpins) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(kThreads) car_allgather_kernel(uint32_t* __res
       long spins = 0;
       while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
         if (++spins > kMaxSpins) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -426,8 +427,11 @@ long car_create(int rank, int world, long max_bytes, int device) {
   CAR_CHECK(hipMemset(s->buf, 0, kFlagsBytes));
   CAR_CHECK(hipMalloc(&s->epochs, kBlocks * sizeof(uint32_t)));
   CAR_CHECK(hipMemset(s->epochs, 0, kBlocks * sizeof(uint32_t)));
-  CAR_CHECK(hipMalloc(&s->err, sizeof(int)));
-  CAR_CHECK(hipMemset(s->err, 0, sizeof(int)));
+  // error word in host-mapped (coherent) memory: the host polls it every engine step with a
+  // plain load, no device sync (a wedged or dead peer becomes a Python error, not silent garbage)
+  CAR_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s->err_host), sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *s->err_host = 0;
+  CAR_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->err), s->err_host, 0));
   CAR_CHECK(hipDeviceSynchronize());
   s->peers.base[rank] = s->buf;
   return reinterpret_cast<long>(s);
@@ -531,10 +535,7 @@ void car_all_gather(long h, void* out, const void* in, long nbytes, hipStream_t 
 
 int car_error(long h) {
   CarState* s = get(h);
-  int v = 0;
-  CAR_CHECK(hipSetDevice(s->device));
-  CAR_CHECK(hipMemcpy(&v, s->err, sizeof(int), hipMemcpyDeviceToHost));
-  return v;
+  return __atomic_load_n(s->err_host, __ATOMIC_ACQUIRE);
 }
 
 void car_destroy(long h) {
@@ -545,7 +546,7 @@ void car_destroy(long h) {
     if (p != s->rank && s->peers.base[p]) hipIpcCloseMemHandle(s->peers.base[p]);
   hipFree(s->buf);
   hipFree(s->epochs);
-  hipFree(s->err);
+  hipHostFree(s->err_host);
   delete s;
 }
 

@@ -66,7 +66,8 @@ struct EpState {
   EpPeers peers{};
   uint32_t* epoch = nullptr;  // [1]
   int* tickets = nullptr;     // [2]
-  int* err = nullptr;         // [1]
+  int* err = nullptr;         // [1] device alias of err_host (host-mapped, polled without a sync)
+  int* err_host = nullptr;
   int* wcnt = nullptr;        // [kEpMaxCountWg][E]
   int* wbase = nullptr;       // [kEpMaxCountWg][E]
   int* lrank = nullptr;       // [tcap * k]
@@ -94,7 +95,7 @@ __device__ __forceinline__ void wait_flags(uint8_t* mine, int phase, int P, uint
       long spins = 0;
       while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
         if (++spins > kEpMaxSpins) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -246,7 +247,7 @@ __global__ void __launch_bounds__(256) ep_recv_kernel(uint16_t* __restrict__ xp,
   wait_flags(peers.base[rank], 1, P, epoch[0], err);
   long n = info[n_local];
   if (n > xp_rows) {  // a peer sent more than the agreed capacity: never write past xp
-    if (threadIdx.x == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     n = xp_rows;
   }
   const long n16 = (long)H / 8;
@@ -356,8 +357,9 @@ long ep_create(int rank, int world, int E, int k, int H, int tcap, int device) {
   EP_CHECK(hipMemset(s->epoch, 0, sizeof(uint32_t)));
   EP_CHECK(hipMalloc(&s->tickets, 2 * sizeof(int)));
   EP_CHECK(hipMemset(s->tickets, 0, 2 * sizeof(int)));
-  EP_CHECK(hipMalloc(&s->err, sizeof(int)));
-  EP_CHECK(hipMemset(s->err, 0, sizeof(int)));
+  EP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s->err_host), sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *s->err_host = 0;
+  EP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->err), s->err_host, 0));
   EP_CHECK(hipMalloc(&s->wcnt, (size_t)kEpMaxCountWg * E * sizeof(int)));
   EP_CHECK(hipMalloc(&s->wbase, (size_t)kEpMaxCountWg * E * sizeof(int)));
   EP_CHECK(hipMalloc(&s->lrank, rows_out * sizeof(int)));
@@ -427,10 +429,7 @@ void ep_combine(long h, void* out, const void* y, long y_rows, const float* topw
 
 int ep_error(long h) {
   EpState* s = ep_get(h);
-  int v = 0;
-  EP_CHECK(hipSetDevice(s->device));
-  EP_CHECK(hipMemcpy(&v, s->err, sizeof(int), hipMemcpyDeviceToHost));
-  return v;
+  return __atomic_load_n(s->err_host, __ATOMIC_ACQUIRE);
 }
 
 void ep_destroy(long h) {
@@ -440,9 +439,10 @@ void ep_destroy(long h) {
   for (int p = 0; p < s->world; ++p)
     if (p != s->rank && s->peers.base[p]) hipIpcCloseMemHandle(s->peers.base[p]);
   hipFree(s->buf);
-  for (void* q : {(void*)s->epoch, (void*)s->tickets, (void*)s->err, (void*)s->wcnt, (void*)s->wbase,
-                  (void*)s->lrank, (void*)s->info, (void*)s->meta_l})
+  for (void* q : {(void*)s->epoch, (void*)s->tickets, (void*)s->wcnt, (void*)s->wbase, (void*)s->lrank,
+                  (void*)s->info, (void*)s->meta_l})
     hipFree(q);
+  hipHostFree(s->err_host);
   delete s;
 }
 

@@ -505,11 +505,27 @@ class Engine:
         t0 = time.perf_counter()
         n0d, n0p = self.stats["decode_tokens"], self.stats["prefill_tokens"]
         kind, out = self._step()
+        self._check_peers()
         self.tracer.record(kind, t0, time.perf_counter(), decode_tokens=self.stats["decode_tokens"] - n0d,
                            prefill_tokens=self.stats["prefill_tokens"] - n0p, running=len(self.running),
                            waiting=len(self.waiting))
         self.profile_window.after_step()
         return out
+
+    def _check_peers(self):
+        """Error words of the device-side collectives (K15 all-reduce / broadcast / all-gather, the
+        EP exchange; host-mapped, so this is a plain load, no sync): a flag wait that timed out
+        means a peer rank died or wedged and its results are garbage.  Fail loudly -- the launcher
+        restarts the predictor -- instead of serving them."""
+        ps = getattr(self.model, "ps", None)
+        if ps is None:
+            return
+        for name, obj in (("tensor-parallel custom collectives", getattr(ps.tp, "car", None)),
+                          ("expert-parallel exchange", getattr(getattr(ps, "ep", None), "ex", None))):
+            code = obj.error() if obj is not None else 0
+            if code:
+                raise RuntimeError(f"{name}: a peer flag wait timed out (error word {code}): a rank died "
+                                   f"or wedged, results since then are invalid")
 
     def _step(self):
         self._launched = False
@@ -1197,6 +1213,7 @@ class Engine:
                 self._world_barrier()
                 continue
             self._execute(*hdr)
+            self._check_peers()
             self.stats["worker_steps"] += 1
 
     def sync_point(self):

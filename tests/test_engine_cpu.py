@@ -389,3 +389,28 @@ def test_async_scheduling_matches_sync(tiny, graphs_like_bucket):
     assert st["async_host_us"] > 0
     assert asy == sync
     assert any(r == "stop" for _, r in asy) and any(r == "abort" for _, r in asy)
+
+
+def test_dead_peer_error_word_fails_the_step():
+    """A device-side collective whose flag wait timed out (a peer rank died or wedged) reports it
+    in its host-mapped error word; the engine checks it after every step and raises instead of
+    serving the garbage results (the launcher then restarts the predictor)."""
+    model = build_model(TINY_LLAMA, device="cpu", dtype=torch.float32, seed=1)
+    eng = Engine(model, EngineConfig(max_num_seqs=4, max_model_len=128, num_kv_blocks=32, use_graphs=False))
+
+    class _Car:
+        code = 0
+
+        def error(self):
+            return self.code
+
+    car = _Car()
+    model.ps.tp.car = car
+    try:
+        eng.add_request([5, 6, 7], SamplingParams(max_tokens=4, ignore_eos=True))
+        eng.step()  # healthy
+        car.code = 1
+        with pytest.raises(RuntimeError, match="peer flag wait timed out"):
+            eng.step()
+    finally:
+        model.ps.tp.car = None
