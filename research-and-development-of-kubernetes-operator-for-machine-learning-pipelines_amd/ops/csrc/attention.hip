@@ -586,11 +586,16 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
       // loop and spilled (168-VGPR budget of 3 workgroups per CU)
       uint32_t vb = vt_b0 + vo;
       asm volatile("" : "+v"(vb));
+      // fragment d + 1 is read while d's two MFMAs run (two register sets; 1.5-3 % faster than
+      // reading each just in time, scripts/history/r4_flash.sh)
+      bf16x8 vf = vt_frag(vb, 0);
 #pragma unroll
       for (int d = 0; d < 8; ++d) {
-        const bf16x8 vf = vt_frag(vb, d);
+        bf16x8 nx = vf;
+        if (d < 7) nx = vt_frag(vb, d + 1);
 #pragma unroll
         for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
+        vf = nx;
       }
     }
   };

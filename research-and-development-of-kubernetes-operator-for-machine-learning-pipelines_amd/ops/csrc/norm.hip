@@ -22,6 +22,14 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ ou
   const size_t base = (size_t)row * H;
   float v[VPT][8];
   float ss = 0.f;
+  // the norm weights are loaded with the row, not after the reduction (no dependent round trip
+  // after it; at batch 1 the launch stayed 4.7 us either way, scripts/history/r4_norm1.sh)
+  u32x4 wv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    wv[i] = vi < nvec ? *reinterpret_cast<const u32x4*>(w + vi * 8) : u32x4{0, 0, 0, 0};
+  }
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int vi = threadIdx.x + i * blockDim.x;
@@ -57,13 +65,12 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ ou
   for (int i = 0; i < VPT; ++i) {
     const int vi = threadIdx.x + i * blockDim.x;
     if (vi < nvec) {
-      u32x4 wv = *reinterpret_cast<const u32x4*>(w + vi * 8);
       u32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         // HF LlamaRMSNorm: weight * bf16(x * inv)
-        float a0 = bf2f(f2bf(v[i][2 * j] * inv)) * lo_bf(wv[j]);
-        float a1 = bf2f(f2bf(v[i][2 * j + 1] * inv)) * hi_bf(wv[j]);
+        float a0 = bf2f(f2bf(v[i][2 * j] * inv)) * lo_bf(wv[i][j]);
+        float a1 = bf2f(f2bf(v[i][2 * j + 1] * inv)) * hi_bf(wv[i][j]);
         o[j] = pack2(a0, a1);
       }
       *reinterpret_cast<u32x4*>(out + base + vi * 8) = o;
@@ -86,9 +93,11 @@ __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(uint16_t* __restrict_
   const int lane = threadIdx.x & 63;
   if (row >= M) return;  // whole wave; no barrier below
   const size_t base = (size_t)row * H;
-  u32x4 a[VPL];
+  u32x4 a[VPL], wv[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) a[i] = *reinterpret_cast<const u32x4*>(x + base + (lane + i * 64) * 8);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) wv[i] = *reinterpret_cast<const u32x4*>(w + (lane + i * 64) * 8);  // with the row
   if constexpr (ADD) {
     u32x4 r[VPL];
 #pragma unroll
@@ -114,23 +123,25 @@ __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(uint16_t* __restrict_
   const float inv = rsqrtf(ss / (float)H + eps);
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const u32x4 wv = *reinterpret_cast<const u32x4*>(w + (lane + i * 64) * 8);
     u32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j)  // HF LlamaRMSNorm: weight * bf16(x * inv)
-      o[j] = pack2(bf2f(f2bf(lo_bf(a[i][j]) * inv)) * lo_bf(wv[j]),
-                   bf2f(f2bf(hi_bf(a[i][j]) * inv)) * hi_bf(wv[j]));
+      o[j] = pack2(bf2f(f2bf(lo_bf(a[i][j]) * inv)) * lo_bf(wv[i][j]),
+                   bf2f(f2bf(hi_bf(a[i][j]) * inv)) * hi_bf(wv[i][j]));
     *reinterpret_cast<u32x4*>(out + base + (lane + i * 64) * 8) = o;
   }
 }
 
-constexpr int kWaveRowsMinM = 256;  // fewer rows: the block form's 8-wave fan-out per row wins
+// fewer rows: the block form's 8-wave fan-out per row wins (MLOP_NORM_WAVE_MIN_M: A/B; at batch 1
+// the wave form measured 345 vs 351 tok/s, scripts/history/r4_norm1.sh)
+constexpr int kWaveRowsMinM = 256;
 
 template <bool ADD>
 static bool dispatch_wave(uint16_t* out, uint16_t* residual, const uint16_t* x, const uint16_t* w,
                           float eps, int M, int H, hipStream_t st) {
   static const bool on = !getenv("MLOP_NORM_WAVE") || atoi(getenv("MLOP_NORM_WAVE")) != 0;
-  if (!on || M < kWaveRowsMinM || H % 512) return false;
+  static const int min_m = getenv("MLOP_NORM_WAVE_MIN_M") ? atoi(getenv("MLOP_NORM_WAVE_MIN_M")) : kWaveRowsMinM;
+  if (!on || M < min_m || H % 512) return false;
   const int g = cdiv(M, 4);
   switch (H / 512) {
     case 1: rmsnorm_wave_kernel<1, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;
