@@ -165,11 +165,12 @@ def _worker(rank, world, port, out_dir):
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
 
 
-def test_custom_all_reduce_two_processes_one_gpu():
+@pytest.mark.parametrize("world", [2, 8])
+def test_custom_all_reduce_two_processes_one_gpu(world):
+    """world = 8: the NR = 8 kernels (Llama-3-70B TP = 8) with 8 processes sharing the GPU."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     d = tempfile.mkdtemp()
-    world = 2
     mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
     for r in range(world):
         res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
