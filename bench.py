@@ -251,6 +251,7 @@ def main(argv=None):
             model=a.model, device=dev, use_operator=not a.no_operator, seed=a.seed + rank, engine_kwargs=ekw)
     for k in ("model_build_ms", "kv_alloc_ms", "kv_malloc_ms", "kv_zero_ms", "graph_capture_ms"):  # start-up breakdown
         deploy_info[k] = engine.stats.get(k, 0)
+    _progress(rank, f"engine ready in {ready_s:.1f} s (graph capture {engine.stats.get('graph_capture_ms', 0)} ms)")
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()
         _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine, None)
@@ -302,10 +303,16 @@ def main(argv=None):
             more = bool(t.item())
         return more
 
+    t_log = time.perf_counter()
     while a.ramp and ramp_more():
         run_steps(1)
         ramp += 1
+        if time.perf_counter() - t_log > 20:  # a long ramp keeps saying it is alive
+            t_log = time.perf_counter()
+            _progress(rank, f"ramp step {ramp}: {engine.stats['prefill_tokens']} prompt tokens in, "
+                            f"{len(engine.running)} running")
     deploy_info["ramp_steps"] = ramp
+    _progress(rank, f"ramp done ({ramp} steps); {a.warmup} warmup + {a.steps} timed steps")
     run_steps(a.warmup)
     if not a.tune_in_timed:
         # shapes first seen from here on take the nearest tuned row count's GEMM backend
@@ -340,6 +347,11 @@ def http_main(a):
            "p50_cr_ready_s": r["p50_cr_ready_process_s"], "http": r}
     print(json.dumps(res), flush=True)
     return res
+
+
+def _progress(rank: int, msg: str) -> None:
+    """One stderr line per phase (the JSON result line alone goes to stdout)."""
+    print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
 
 
 def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine, proc_ready=None):

@@ -26,6 +26,8 @@ from __future__ import annotations
 import collections
 import itertools
 import operator
+import os
+import sys
 import time
 from dataclasses import dataclass, field
 from enum import Enum
@@ -1246,6 +1248,7 @@ class Engine:
         self.graph_pool = torch.cuda.graph_pool_handle()
         empty = np.zeros(0, dtype=np.int32)
         t0 = time.perf_counter()
+        verbose = os.environ.get("MLOP_VERBOSE", "0") == "1"
         with torch.cuda.stream(stream):
             for bi, b in enumerate(sorted(self.buckets, reverse=True)):
                 self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=b)
@@ -1257,6 +1260,9 @@ class Engine:
                 for _ in range(2 if bi == 0 else 1):  # warm-up (allocator, autotune, lazy init)
                     m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
                 stream.synchronize()
+                if verbose:
+                    print(f"[engine] capturing decode graph {bi + 1}/{len(self.buckets)} (batch {b}) "
+                          f"at {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                     logits = m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
