@@ -513,9 +513,10 @@ void car_broadcast(long h, void* out, const void* in, long nbytes, int root, hip
   CAR_CHECK(hipGetLastError());
 }
 
-void car_all_gather(long h, void* out, const void* in, long nbytes, hipStream_t st) {
+void car_all_gather(long h, void* out, long out_bytes, const void* in, long nbytes, hipStream_t st) {
   CarState* s = get(h);
   if (nbytes % 4) throw std::runtime_error("custom all-gather: bytes must be a multiple of 4");
+  if (out_bytes != nbytes * (long)s->world) throw std::runtime_error("custom all-gather: out must be world x piece");
   if ((size_t)nbytes > s->max_bytes) throw std::runtime_error("custom all-gather: piece too large");
   for (int p = 0; p < s->world; ++p)
     if (!s->peers.base[p]) throw std::runtime_error("custom all-gather: peers not opened");

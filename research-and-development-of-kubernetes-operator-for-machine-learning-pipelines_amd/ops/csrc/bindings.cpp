@@ -622,9 +622,9 @@ void car_all_gather(int64_t h, Tensor out, Tensor piece) {
   TORCH_CHECK(piece.is_cuda() && piece.is_contiguous() && out.is_cuda() && out.is_contiguous() &&
                   out.scalar_type() == piece.scalar_type(), "all-gather: contiguous device tensors of one dtype");
   const long nbytes = (long)(piece.numel() * piece.element_size());
-  TORCH_CHECK(out.numel() % piece.numel() == 0 || piece.numel() == 0, "all-gather: out = world x piece");
   c10::DeviceGuard g(piece.device());
-  mlop::car_all_gather((long)h, out.data_ptr(), piece.data_ptr(), nbytes, cur_stream());
+  mlop::car_all_gather((long)h, out.data_ptr(), (long)(out.numel() * out.element_size()), piece.data_ptr(), nbytes,
+                       cur_stream());
 }
 int64_t gemv_addnorm_enable(int64_t on) { return mlop::gemv_addnorm_enable((int)on); }
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }

@@ -166,7 +166,7 @@ void car_open(long h, const void* handles);
 long car_max_bytes(long h);
 void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot = false);
 void car_broadcast(long h, void* out, const void* in, long nbytes, int root, hipStream_t st);
-void car_all_gather(long h, void* out, const void* in, long nbytes, hipStream_t st);
+void car_all_gather(long h, void* out, long out_bytes, const void* in, long nbytes, hipStream_t st);
 int car_error(long h);
 int car_mem_mode(long h);
 void car_destroy(long h);
