@@ -42,13 +42,13 @@ struct Arena {
   ~Arena() {
     stop = true;
     if (worker.joinable()) worker.join();
-    hipSetDevice(device);
-    hipDeviceSynchronize();
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
     for (auto& m : maps) {
-      hipMemUnmap(base + m.first, m.second.first);
-      hipMemRelease(m.second.second);
+      (void)hipMemUnmap(base + m.first, m.second.first);
+      (void)hipMemRelease(m.second.second);
     }
-    if (base) hipMemAddressFree(base, reserved);
+    if (base) (void)hipMemAddressFree(base, reserved);
   }
 };
 
@@ -77,7 +77,7 @@ hipError_t map_range(Arena& a, size_t off, size_t bytes) {
   if (e != hipSuccess) return e;
   e = hipMemMap(a.base + off, bytes, 0, h, 0);
   if (e != hipSuccess) {
-    hipMemRelease(h);
+    (void)hipMemRelease(h);
     return e;
   }
   hipMemAccessDesc acc{};
@@ -127,7 +127,7 @@ std::shared_ptr<void> vmm_reserve(long bytes, int device, void** base_out, long*
   auto a = std::make_shared<Arena>();
   a->device = device;
   a->reserved = (size_t)((bytes + g - 1) / g * g);
-  hipSetDevice(device);
+  (void)hipSetDevice(device);
   void* p = nullptr;
   if (hipMemAddressReserve(&p, a->reserved, (size_t)g, nullptr, 0) != hipSuccess) return nullptr;
   a->base = (char*)p;
@@ -157,7 +157,7 @@ bool vmm_map_chunks(void* base, long region_stride, int n_regions, long chunk_by
       (size_t)region_stride * n_regions > a->reserved || (first + count) * chunk_bytes > region_stride)
     return false;
   if (!async) {
-    hipSetDevice(a->device);
+    (void)hipSetDevice(a->device);
     hipStream_t st;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
     bool ok = true;
@@ -165,14 +165,14 @@ bool vmm_map_chunks(void* base, long region_stride, int n_regions, long chunk_by
       ok = map_chunk(*a, c, (size_t)region_stride, n_regions, (size_t)chunk_bytes, st) == hipSuccess;
       if (ok) a->chunks_ready.store(c + 1);
     }
-    hipStreamDestroy(st);
+    (void)hipStreamDestroy(st);
     if (!ok) a->error = 1;
     return ok;
   }
   if (a->worker.joinable()) return false;  // one background fill per arena
   Arena* ap = a.get();  // the arena's destructor joins the worker before anything is freed
   a->worker = std::thread([ap, region_stride, n_regions, chunk_bytes, first, count] {
-    hipSetDevice(ap->device);
+    (void)hipSetDevice(ap->device);
     hipStream_t st;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
       ap->error = 1;
@@ -185,7 +185,7 @@ bool vmm_map_chunks(void* base, long region_stride, int n_regions, long chunk_by
       }
       ap->chunks_ready.store(c + 1);
     }
-    hipStreamDestroy(st);
+    (void)hipStreamDestroy(st);
   });
   return true;
 }
