@@ -128,6 +128,20 @@ void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor 
                              (int)k_cache.size(0), cur_stream());
 }
 
+// Largest (tile, kv head) pair count that takes the in-launch split-KV combine
+// (MLOP_ATTN_FUSED_MAX_PAIRS; attn_fused_max_pairs() in-process, -1 reads it back).
+static int g_attn_fused_pairs = -1;
+static int attn_fused_pairs_cap() {
+  if (g_attn_fused_pairs < 0)
+    g_attn_fused_pairs = getenv("MLOP_ATTN_FUSED_MAX_PAIRS") ? atoi(getenv("MLOP_ATTN_FUSED_MAX_PAIRS")) : (1 << 30);
+  return g_attn_fused_pairs;
+}
+int64_t attn_fused_max_pairs(int64_t n) {
+  const int prev = attn_fused_pairs_cap();
+  if (n >= 0) g_attn_fused_pairs = (int)n;
+  return prev;
+}
+
 void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem, Tensor q, Tensor k_cache,
                      Tensor v_cache, Tensor block_tables, Tensor tile_seq, Tensor tile_q0,
                      Tensor q_start, Tensor q_len, Tensor ctx_len, double scale,
@@ -162,10 +176,11 @@ void paged_attention(Tensor out, Tensor part_o, Tensor part_ml, Tensor part_sem,
   }
   // part_sem: zero-initialised int32 tickets, one per (tile, kv head), re-armed by the
   // kernel; empty -> the split-KV combine runs as a second launch
-  // Only for launches of few (tile, kv head) pairs: there the saved launch (~4.7 us in a
-  // graph) outweighs every partition's release fence (batch 1: 309.7 -> 316.7-318.6 tok/s;
-  // batch 8, 64 pairs: 1800 -> 1783, scripts/run52.sh)
-  static const int max_pairs = getenv("MLOP_ATTN_FUSED_MAX_PAIRS") ? atoi(getenv("MLOP_ATTN_FUSED_MAX_PAIRS")) : 32;
+  // Round 3 capped it at 32 pairs: every partition's agent release fence outweighed the
+  // saved launch above that (batch 8: 1800 -> 1783 tok/s, scripts/run52.sh).  With the
+  // partials stored sc1 and no producer fence it wins at every batch measured (batch 8 / 16
+  // / 64: +0.7 / +0.7 / +0.2 %, scripts/history/r4_fusedc.sh), so the cap is off by default.
+  const int max_pairs = attn_fused_pairs_cap();
   int* sem = nullptr;
   if (nparts > 1 && part_sem.numel() > 0 && num_tiles * Hkv <= max_pairs) {
     check_i32(part_sem, "part_sem");
@@ -704,6 +719,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_all_gather(int h, Tensor(a!) out, Tensor piece) -> ()");
   m.def("car_error(int h) -> int", &car_error);
   m.def("gemv_addnorm_enable(int on) -> int", &gemv_addnorm_enable);
+  m.def("attn_fused_max_pairs(int n) -> int", &attn_fused_max_pairs);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
   m.def("chan_create(str name, int slots, int consumers) -> int", &chan_create);

@@ -50,3 +50,16 @@ def gemv_addnorm_on(gpu):
         yield
     finally:
         torch.ops.mlop.gemv_addnorm_enable(prev)
+
+
+@pytest.fixture
+def attn_fused_all(gpu):
+    """Lift the (tile, kv head) pair cap of paged attention's in-launch split-KV combine
+    (MLOP_ATTN_FUSED_MAX_PAIRS) so a test's part_sem launch takes the fused path at any size."""
+    import torch
+
+    prev = torch.ops.mlop.attn_fused_max_pairs(1 << 30)
+    try:
+        yield
+    finally:
+        torch.ops.mlop.attn_fused_max_pairs(prev)

@@ -188,7 +188,7 @@ def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
 @pytest.mark.parametrize("case", ["decode", "prefill", "mixed", "split", "split_fused"])
-def test_paged_attention(gpu, Hq, Hkv, case):
+def test_paged_attention(gpu, Hq, Hkv, case, attn_fused_all):
     torch.manual_seed(0)
     np.random.seed(0)
     G = Hq // Hkv
@@ -222,7 +222,7 @@ def test_paged_attention(gpu, Hq, Hkv, case):
 
 
 @pytest.mark.parametrize("fused", [False, True])
-def test_paged_attention_padded_bucket(gpu, fused):
+def test_paged_attention_padded_bucket(gpu, fused, attn_fused_all):
     """Graph-bucket padding rows (q_len 1, ctx 0) under forced split-KV: both combine
     paths (second-launch reduce and in-launch last-ticket combine) must write a zero
     row there, not leave the buffer's old contents (NaN here) for o_proj / MoE routing."""

@@ -117,7 +117,7 @@ def test_grouped_stream_k_under_contention(gpu, counts, epi, N, K):
         torch.testing.assert_close(y0[a:b].float(), r.float(), atol=3e-2, rtol=3e-2)
 
 
-def test_split_kv_fused_combine_under_contention(gpu):
+def test_split_kv_fused_combine_under_contention(gpu, attn_fused_all):
     """Decode batch with long contexts forced into 6 KV partitions: the in-launch
     last-ticket combine must give the same bits every launch and leave every
     semaphore re-armed (zero) for the next one."""
