@@ -80,6 +80,8 @@ __device__ __forceinline__ bf16x8 vt_frag(uint32_t b, int d) {
   return f;
 }
 
+__device__ __forceinline__ int wid_of(unsigned t) { return __builtin_amdgcn_readfirstlane((int)(t >> 6)); }
+
 template <int G>
 __global__ void __launch_bounds__(256) paged_attn_kernel(
     uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -90,6 +92,8 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int part_tokens,
     int nparts, int num_blocks, int* __restrict__ sem) {
   constexpr int QT = 16 / G;
+  // (3 waves per SIMD at 134 VGPRs; forcing 4 (127 VGPRs, amdgpu_waves_per_eu) measured the
+  // same on every decode shape and the headline, scripts/history/r4_occ.sh)
   // wave w stages its page pair's V image (2 x 16 token rows x 256 B = 8 KB) inside sm_o[w]
   // (8448 B, 256-B aligned: vt_frag), which it alone writes after its loop.  (A second image per
   // wave, prefetching the next pair, measured 1-4 % SLOWER on every decode shape: r04 profile.)
@@ -101,10 +105,16 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
   const int tile = blockIdx.x, kvh = blockIdx.y, part = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = tile_seq[tile], q0 = tile_q0[tile];
+  const int p_begin = part * part_tokens;
+  // The wave's first page pair, read as soon as the sequence id is known (clamped into the
+  // row, used only if the pair exists): in the same round trip as ctx_len / q_len instead of
+  // behind them, so the chain to the first K load is tile_seq -> block table -> K.
+  const int* bt = block_tables + (size_t)s * bt_stride;
+  const int bt0 = 2 * ((p_begin >> 5) + wid_of(threadIdx.x));
+  const int rawA = bt[min(bt0, bt_stride - 1)], rawB = bt[min(bt0 + 1, bt_stride - 1)];
   const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
   const int last_q = min(q0 + QT, ql) - 1;           // last valid query of the tile
   const int kv_end = last_q >= 0 ? ctx - ql + last_q + 1 : 0;
-  const int p_begin = part * part_tokens;
   const int p_end = min(kv_end, p_begin + part_tokens);
   if (p_begin >= p_end && nparts > 1) {              // reducer skips empty partitions
     // kv_end == 0 (graph-bucket padding rows, ctx 0): no partition draws the last ticket of
@@ -141,7 +151,6 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
   for (int d = 0; d < 8; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = kNegBig, l = 0.f;
 
-  const int* bt = block_tables + (size_t)s * bt_stride;
   const int pp_begin = p_begin >> 5;
   const int pp_end = (p_end + 31) >> 5;
   const int n_pages = (p_end + kBS - 1) / kBS;
@@ -167,8 +176,8 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
   // page ids one pair ahead: the block-table loads of pair pp + 4 run under pair pp
   int pgA = 0, pgB = 0;
   if (pp_begin + wid < pp_end) {
-    pgA = page_a(pp_begin + wid);
-    pgB = page_b(pp_begin + wid, pgA);
+    pgA = min(max(rawA, 0), num_blocks - 1);
+    pgB = (bt0 + 1 < n_pages) ? min(max(rawB, 0), num_blocks - 1) : pgA;
   }
   for (int pp = pp_begin + wid; pp < pp_end; pp += 4) {
     const uint16_t* kA = kc + pgA * page_stride + (size_t)kvh * kBS * kD;
