@@ -196,9 +196,14 @@ class LlamaModel:
         h = ops.embedding(ids, self.embed, self.vocab_start)
         tp.all_reduce(h)
         residual = h
-        x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
-        chain = tp.size == 1 and self._chain_ok(ids.shape[0])
+        M = ids.shape[0]
+        chain = tp.size == 1 and self._chain_ok(M)
         ss = None  # norm chain: x is None and ss holds the residual's row partials
+        if chain and M <= ops.GEMV_CHAIN_MAX_M:
+            # decode form: the QKV GEMV takes the embedding rows' factors itself (ss unused)
+            x, ss = None, ops.ss_init(h, ops.ss_buffer(M, cfg.hidden_size, h.device))
+        else:
+            x = ops.rmsnorm(h, self.layers[0]["in_norm"], eps)
         for i, L in enumerate(self.layers):
             if ss is None:
                 q = ops.qkv_rope_cache(x, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i],
@@ -230,11 +235,12 @@ class LlamaModel:
     def _chain_ok(self, M: int) -> bool:
         """Large-M TP=1 layers without add + RMSNorm passes: every GEMM of the chain on the
         four-wave kernel (ops.norm_chain_ok) and unit norm weights (folded into qkv / gate_up)."""
-        if not self.unit_norms or M < 2 or len(self.layers) < 1:
+        if not self.unit_norms or len(self.layers) < 1:
             return False
         cfg, H = self.cfg, self.cfg.hidden_size
         return ops.norm_chain_ok(M, H, ((self.layers[0]["qkv"].shape[0], H), (H, self.n_q * cfg.head_dim),
-                                        (2 * self.inter, H), (H, self.inter)), device=self.device)
+                                        (2 * self.inter, H), (H, self.inter)), device=self.device,
+                                 epis=(ops.EPI_ROPE, ops.EPI_NONE, ops.EPI_SILU_MUL, ops.EPI_NONE))
 
     def _chain_layer(self, i, a, residual, last, eps):
         """O (+= residual, row partials), gate_up + SiLU on the row-scaled residual, down (+=

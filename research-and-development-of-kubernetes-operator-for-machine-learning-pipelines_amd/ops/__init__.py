@@ -476,17 +476,29 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
 NORM_CHAIN = os.environ.get("MLOP_NORM_CHAIN", "1")
 
 
-def norm_chain_ok(M: int, H: int, shapes, device=None) -> bool:
+# The decode (M <= 4) form of the chain runs on the GEMV (gemv.hip EPI_RES / PRO_RS): O and down
+# add into the residual in place, QKV and gate_up take each row's factor from the residual
+# chunks they stream, so a layer has no add + RMSNorm launch.  "0" keeps the decode norms.
+GEMV_CHAIN = os.environ.get("MLOP_GEMV_CHAIN", "1") == "1"
+GEMV_CHAIN_MAX_M = 4
+
+
+def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
     """True when the chain can run at M rows: hidden size H (ss groups of 128 columns, 16 per
     quad of lanes) and every (N, K) GEMM of the chain on the four-wave kernel, with the band
     tickets' scratch reserved on ``device`` and one ticket per 256-row band (w4_chain_ok checks
     everything launch_w4_chain does, so the chain is decided once per forward and never refused
-    after a residual was updated in place)."""
+    after a residual was updated in place).  At M <= 4 every GEMM must take the GEMV form
+    instead (``epis``: each shape's epilogue, default plain)."""
     if NORM_CHAIN == "force":
         return H % 128 == 0
     if NORM_CHAIN == "0" or GEMM_BACKEND != "mlop" or H % 256:
         return False
     _need_gpu()
+    if M <= GEMV_CHAIN_MAX_M:
+        epis = epis or [EPI_NONE] * len(shapes)
+        return GEMV_CHAIN and all(bool(torch.ops.mlop.gemv_chain_supported(M, N, K, e))
+                                  for (N, K), e in zip(shapes, epis))
     if device is not None and torch.device(device).type == "cuda":
         _sk_reserve(torch.device(device))
     return all(bool(torch.ops.mlop.w4_chain_ok(M, N, K)) for N, K in shapes)
@@ -495,6 +507,18 @@ def norm_chain_ok(M: int, H: int, shapes, device=None) -> bool:
 def ss_buffer(M: int, H: int, device) -> torch.Tensor:
     """fp32 [M * (H / 128 + 1)]: the [M, H / 128] partials, then the [M] row totals."""
     return torch.empty(M * (H // 128 + 1), dtype=torch.float32, device=device)
+
+
+def ss_init(x: torch.Tensor, ss: torch.Tensor) -> torch.Tensor:
+    """ss (ss_buffer) <- x's row partials and totals where the torch reference of the chain
+    will read them; the GPU chain's decode (GEMV) form takes its row factors from x itself."""
+    if x.is_cuda and NORM_CHAIN != "force":
+        return ss
+    M, H = x.shape
+    part, tot = ss_parts(ss, M, H)
+    part.copy_(x.float().pow(2).view(M, H // 128, 128).sum(-1))
+    tot.copy_(part.sum(-1))
+    return ss
 
 
 def ss_parts(ss: torch.Tensor, M: int, H: int):

@@ -324,6 +324,14 @@ bool gemm_res_ss(Tensor residual, Tensor a, Tensor w, Tensor ss_out) {
                   residual.stride(0) % 8 == 0, "residual [M, N]");
   TORCH_CHECK(N % 128 == 0, "N % 128");
   check_ss(ss_out, M, N, "ss");
+  if (M <= 4) {  // decode sizes: the GEMV chain (gemv.hip EPI_RES); its consumers take their row
+                 // factors from the residual itself, so ss_out is not written
+    if (residual.stride(0) != N || !mlop::gemv_chain_takes((int)M, (int)N, (int)K, 0)) return false;
+    c10::DeviceGuard g(a.device());
+    mlop::launch_gemv_res(a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(), (int)M, (int)N,
+                          (int)K, cur_stream());
+    return true;
+  }
   mlop::RopeEpi re{};
   re.ss_out = ss_out.data_ptr<float>();
   re.ss_tot = re.ss_out + M * (N / 128);
@@ -345,6 +353,13 @@ bool gemm_rs(Tensor out, Tensor a, Tensor w, Tensor ss_in, double eps, int64_t e
                   out.stride(0) % 8 == 0, "out [M, N or N/2]");
   TORCH_CHECK(K % 128 == 0, "K % 128");
   check_ss(ss_in, M, K, "ss");
+  if (M <= 4) {  // decode sizes: gemv.hip PRO_RS, row factors from the streamed chunks (ss_in unused)
+    if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi)) return false;
+    c10::DeviceGuard g(a.device());
+    mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
+                         (int)N, (int)K, (int)epi, mlop::RopeEpi{}, (float)eps, cur_stream());
+    return true;
+  }
   mlop::RopeEpi re{};
   re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
   re.ss_inv_k = 1.f / (float)K;
@@ -373,10 +388,17 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D, "cos_sin [max_pos, D]");
   TORCH_CHECK(K % 128 == 0, "K % 128");
   check_ss(ss_in, M, K, "ss");
-  if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
+  if (M <= 4) {  // decode sizes: gemv.hip PRO_RS + the RoPE / paged K/V epilogue (ss_in unused)
+    if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, 3)) return false;
+    c10::DeviceGuard g(a.device());
+    mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re,
+                         (float)eps, cur_stream());
+    return true;
+  }
+  if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
   re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
   re.ss_inv_k = 1.f / (float)K;
   re.ss_eps = (float)eps;
@@ -452,6 +474,10 @@ bool gemm_norm_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor res_out
                     Tensor norm_w, Tensor w, Tensor pos, Tensor cos_sin, Tensor slots, double eps) {
   return gemm_norm_impl(nullptr, &q_out, &k_cache, &v_cache, res_out, y, res_in, norm_w, w, &pos, &cos_sin,
                         &slots, eps, 3);
+}
+
+bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return M <= 4 && mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
 }
 
 bool gemm_norm_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
@@ -764,6 +790,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor a, Tensor w, Tensor norm_w, "
         "Tensor(c!) ws, float eps) -> bool");
   m.def("gemm_norm_supported(int M, int N, int K, int epi) -> bool", &gemm_norm_supported);
+  m.def("gemv_chain_supported(int M, int N, int K, int epi) -> bool", &gemv_chain_supported);
   m.def("gemm_norm(Tensor(a!) out, Tensor(b!) res_out, Tensor y, Tensor res_in, Tensor norm_w, Tensor w, "
         "float eps, int epi) -> bool");
   m.def("gemm_norm_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor(d!) res_out, "

@@ -45,7 +45,11 @@ namespace mlop {
 
 namespace {
 
-enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3, EPI_ADDNORM = 4 };
+enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3, EPI_ADDNORM = 4, EPI_RES = 5 };
+// prologues: none; NORM (residual add + RMSNorm of y and res_in, see above); RS (the row-scale
+// chain: A IS the raw residual and the norm weights are folded into B, so the rows'
+// rsqrt(mean(a^2) + eps) comes from the very chunks the dots stream: no extra load at all)
+enum { PRO_NONE = 0, PRO_NORM = 1, PRO_RS = 2 };
 constexpr int kHeadD = 128;
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
@@ -80,12 +84,13 @@ struct GroupArgs {
   int n_groups;
 };
 
-template <int M, int RP, int EPI, int KW, int U, bool NORM, bool GROUPED = false>
+template <int M, int RP, int EPI, int KW, int U, int PRO, bool GROUPED = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ A, int lda,
                                                    const uint16_t* __restrict__ B, int ldb,
                                                    uint16_t* __restrict__ C, int ldc, int N, int K,
                                                    RopeEpi re, NormPro np, GroupArgs ga = GroupArgs{}) {
   constexpr int R = 2 * RP;  // weight rows per wave
+  constexpr bool NORM = PRO == PRO_NORM, RS = PRO == PRO_RS;
   static_assert(EPI != EPI_ROPE || RP == 1, "rope sets are single row pairs");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // row set: KW == 1 -> one per wave; KW == 4 -> one per workgroup (its waves split K)
@@ -147,7 +152,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-  float ss[M];  // NORM: sum of r^2 over this lane's chunks
+  float ss[M];  // NORM / RS: sum of r^2 over this lane's chunks
 #pragma unroll
   for (int m = 0; m < M; ++m) ss[m] = 0.f;
   const bool writer = NORM && (KW == 1 ? set == 0 : blockIdx.x == 0);
@@ -162,6 +167,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   const int rope_d = (set % (kHeadD / 2));
   const bool rope_set = EPI == EPI_ROPE && set < (re.Hq + re.Hkv) * (kHeadD / 2);
   const int lane_off = (KW == 1 ? 0 : wv * 64) + lane;
+  // EPI_RES: lane m*R + r adds output (m, set*R + r) into the residual C; its old value is
+  // loaded behind the first weight loads (the storing waves only)
+  const bool res_lane = EPI == EPI_RES && (KW == 1 || wv == 0) && lane < M * R;
+  uint16_t res_pf = 0;
   constexpr int STEP = 64 * KW;  // chunk stride between a lane's consecutive loads
   for (int c0 = 0; c0 < KC; c0 += STEP * U) {
     u32x4 w[U][R], x[U][M];
@@ -195,6 +204,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         for (int m = 0; m < M; ++m) x[u][m] = (ok && m < mc) ? Av[m][c] : u32x4{0, 0, 0, 0};
       }
     }
+    if constexpr (EPI == EPI_RES) {
+      if (c0 == 0 && res_lane) res_pf = C[(size_t)(lane / R) * ldc + set * R + lane % R];  // behind the weights
+    }
     if constexpr (EPI == EPI_ROPE) {
       if (c0 == 0 && rope_lane) {  // issued behind the weight loads
         pf_slot = re.slots[lane];
@@ -206,32 +218,37 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m)
           if (!GROUPED || m < mc) acc[r][m] = dot8(w[u][r], x[u][m], acc[r][m]);  // mc: wave-uniform
+      if constexpr (RS) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) ss[m] = dot8(x[u][m], x[u][m], ss[m]);  // a^2 pairs, fp32 accumulate
+      }
+    }
   }
 
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
-  if constexpr (NORM) {
+  if constexpr (NORM || RS) {
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = wave_sum(ss[m]);
   }
 
   if constexpr (KW > 1) {
-    constexpr int NV = R * M + (NORM ? M : 0);
+    constexpr int NV = R * M + ((NORM || RS) ? M : 0);
     __shared__ float red[KW][NV];
     if (lane == 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m) red[wv][r * M + m] = acc[r][m];
-      if constexpr (NORM) {
+      if constexpr (NORM || RS) {
 #pragma unroll
         for (int m = 0; m < M; ++m) red[wv][R * M + m] = ss[m];
       }
@@ -244,10 +261,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int k = 0; k < KW; ++k) t += red[k][i];
       if (i < R * M) acc[i / M][i % M] = t;
-      else if constexpr (NORM) ss[i - R * M] = t;
+      else if constexpr (NORM || RS) ss[i - R * M] = t;
     }
   }
-  if constexpr (NORM) {
+  if constexpr (NORM || RS) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const float inv = rsqrtf(ss[m] / (float)K + np.eps);
@@ -292,6 +309,13 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         uint16_t* dst = re.v_cache + (((size_t)blk * re.Hkv + kh) * re.BS + off) * kHeadD + dd;
         *reinterpret_cast<uint32_t*>(dst) = pack2(acc[0][m], acc[1][m]);
       }
+    }
+  } else if constexpr (EPI == EPI_RES) {
+    // residual (C, in place) = bf16(residual + bf16(y)): norm.hip's add rounding; every element
+    // is read and written by its one owning lane only
+    if (res_lane) {
+      const int m = lane / R, r = lane % R;
+      C[(size_t)m * ldc + set * R + r] = f2bf(bf2f(res_pf) + bf2f(f2bf(acc_pick(acc, r, m))));
     }
   } else if constexpr (EPI == EPI_ADDNORM) {
     // Epilogue form of the decoder's residual add + RMSNorm (the norm AFTER this projection,
@@ -418,7 +442,7 @@ int gemv_kw4_sets(int M) {
   return v >= 0 ? v : (M <= 2 ? 8192 : 2048);
 }
 
-template <int M, int EPI, bool NORM>
+template <int M, int EPI, int PRO>
 void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int N,
                 int K, const RopeEpi& re, const NormPro& np, hipStream_t st) {
   constexpr int U = M <= 2 ? 4 : 2;  // chunks per row in flight per lane (VGPR budget)
@@ -432,7 +456,7 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
-    gemv_kernel<M, RP, EPI, KW, U, NORM><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, N, K, re, \
+    gemv_kernel<M, RP, EPI, KW, U, PRO><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, N, K, re, \
                                                                   np);                        \
   } while (0)
   if constexpr (EPI == EPI_ROPE) {
@@ -447,27 +471,27 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 #undef MLOP_GEMV
 }
 
-template <int EPI, bool NORM = false>
+template <int EPI, int PRO = PRO_NONE>
 void run_gemv(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
               int N, int K, const RopeEpi& re, hipStream_t st, const NormPro& np = NormPro{}) {
-  if constexpr (NORM) {  // the fused-norm prologue is built for the decode sizes only (M <= 4)
+  if constexpr (PRO != PRO_NONE || EPI == EPI_RES) {  // the norm-fused forms: decode sizes only (M <= 4)
     switch (M) {
-      case 1: run_gemv_m<1, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      case 2: run_gemv_m<2, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      case 3: run_gemv_m<3, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      default: run_gemv_m<4, EPI, true>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 1: run_gemv_m<1, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 2: run_gemv_m<2, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 3: run_gemv_m<3, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      default: run_gemv_m<4, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
     }
     return;
   }
   switch (M) {
-    case 1: run_gemv_m<1, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 2: run_gemv_m<2, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 3: run_gemv_m<3, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 4: run_gemv_m<4, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 5: run_gemv_m<5, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 6: run_gemv_m<6, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 7: run_gemv_m<7, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    default: run_gemv_m<8, EPI, false>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 1: run_gemv_m<1, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 2: run_gemv_m<2, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 3: run_gemv_m<3, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 4: run_gemv_m<4, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 5: run_gemv_m<5, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 6: run_gemv_m<6, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    case 7: run_gemv_m<7, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    default: run_gemv_m<8, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
   }
 }
 
@@ -511,7 +535,7 @@ void run_gemv_grouped_m(const uint16_t* A, const uint16_t* B, uint16_t* C, int l
   do {                                                                                             \
     const int sets = spg * slots;                                                                  \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
-    gemv_kernel<M, RP, EPI, KW, U, false, true><<<blocks, 256, 0, st>>>(A, K, B, K, C, ldc, N, K,  \
+    gemv_kernel<M, RP, EPI, KW, U, PRO_NONE, true><<<blocks, 256, 0, st>>>(A, K, B, K, C, ldc, N, K,  \
                                                                           RopeEpi{}, NormPro{}, ga); \
   } while (0)
   if (rp == 2) {
@@ -581,10 +605,10 @@ bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void*
   auto* b = (const uint16_t*)B;
   auto* o = (uint16_t*)out;
   switch (M) {
-    case 1: run_gemv_m<1, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    case 2: run_gemv_m<2, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    case 3: run_gemv_m<3, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    default: run_gemv_m<4, EPI_ADDNORM, false>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    case 1: run_gemv_m<1, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    case 2: run_gemv_m<2, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    case 3: run_gemv_m<3, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
+    default: run_gemv_m<4, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
   }
   return true;
 }
@@ -603,9 +627,34 @@ void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M,
                       const RopeEpi& re, hipStream_t st) {
   auto* b = (const uint16_t*)B;
   auto* c = (uint16_t*)C;
-  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
-  else if (epi == EPI_ROPE) run_gemv<EPI_ROPE, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
-  else run_gemv<EPI_NONE, true>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+  else if (epi == EPI_ROPE) run_gemv<EPI_ROPE, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+  else run_gemv<EPI_NONE, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
+}
+
+// The decode norm chain (M <= 4, TP = 1, norm weights folded into the consuming projections:
+// LlamaModel.fold_norms): O and down add their output into the residual in place (EPI_RES),
+// QKV and gate_up read the raw residual and scale each row's sums by rsqrt(mean(a^2) + eps)
+// taken from the chunks they stream anyway (PRO_RS).  A decode layer is then five launches
+// and no add + RMSNorm pass: the GEMV form of gemm_w4.hip's large-M chain (W4_ADD_SS / W4_RS).
+bool gemv_chain_takes(int M, int N, int K, int epi) {
+  return M <= 4 && gemv_takes(M, N, K, epi);
+}
+
+void launch_gemv_rs(const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K, int epi,
+                    const RopeEpi& re, float eps, hipStream_t st) {
+  auto* a = (const uint16_t*)A;
+  auto* b = (const uint16_t*)B;
+  auto* c = (uint16_t*)C;
+  NormPro np{};
+  np.eps = eps;
+  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL, PRO_RS>(a, lda, b, K, c, ldc, M, N, K, re, st, np);
+  else if (epi == EPI_ROPE) run_gemv<EPI_ROPE, PRO_RS>(a, lda, b, K, nullptr, 0, M, N, K, re, st, np);
+  else run_gemv<EPI_NONE, PRO_RS>(a, lda, b, K, c, ldc, M, N, K, re, st, np);
+}
+
+void launch_gemv_res(const void* A, int lda, const void* B, void* residual, int M, int N, int K, hipStream_t st) {
+  run_gemv<EPI_RES>((const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)residual, N, M, N, K, RopeEpi{}, st);
 }
 
 }  // namespace mlop

@@ -131,6 +131,89 @@ def test_llama_forward_chain_on_off(gpu, w4, monkeypatch):
                 toks.append(t)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+def test_gemv_chain_res_rs(gpu, w4, M):
+    """Decode form of the chain (gemv.hip EPI_RES / PRO_RS, M <= 4): O / down add into the
+    residual in place with norm.hip's rounding, gate_up / plain / QKV + RoPE scale each row by
+    rsqrt(mean(a^2) + eps) of the residual chunks they stream.  The ss buffers are NaN: the
+    GEMV form must neither read nor need them (the four-wave form would turn them into NaNs)."""
+    from mlopamd.models.layers import rope_table
+
+    torch.manual_seed(M)
+    for K in (H, I):  # O (K = q_size = H) and down (K = I)
+        assert torch.ops.mlop.gemv_chain_supported(M, H, K, 0)
+        a = torch.randn(M, K, device=gpu, dtype=bf)
+        w = (0.02 * torch.randn(H, K, device=gpu)).to(bf)
+        res = torch.randn(M, H, device=gpu, dtype=bf)
+        exp = (res.float() + (a.float() @ w.float().t()).to(bf).float()).to(bf)
+        r, ss = res.clone(), ops.ss_buffer(M, H, gpu).fill_(float("nan"))
+        ops.gemm_res_ss(a, w, r, ss)
+        close(r, exp, atol=2e-2, rtol=1e-2)
+        r2 = res.clone()
+        ops.gemm_res_ss(a, w, r2, ss)
+        assert torch.equal(r, r2)
+    x = (3 * torch.randn(M, H, device=gpu)).to(bf)
+    ss = ops.ss_buffer(M, H, gpu).fill_(float("nan"))
+    w = (0.02 * torch.randn(2 * I, H, device=gpu)).to(bf)
+    y = ops.gemm_rs(x, w, ss, EPS, ops.EPI_SILU_MUL)
+    exp = ref.silu_mul(ops.deinterleave_cols((_unit_norm(x) @ w.float().t()).to(bf)))
+    close(y, exp, atol=3e-2 * exp.abs().max().item() / 10 + 1e-2, rtol=3e-2)
+    w = (0.02 * torch.randn(1024, H, device=gpu)).to(bf)
+    y = ops.gemm_rs(x, w, ss, EPS, ops.EPI_NONE)
+    close(y, (_unit_norm(x) @ w.float().t()).to(bf), atol=2e-2, rtol=2e-2)
+    Hq, Hkv, D, BS = 32, 8, 128, 16
+    N, NB = (Hq + 2 * Hkv) * D, 64
+    cs = rope_table(D, 8192, 5e5, device=gpu)
+    w = (0.02 * torch.randn(N, H, device=gpu)).to(bf)
+    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
+    if M > 1:
+        slots[1] = -1  # a padding row: q only, no cache stores
+    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
+    q = ops.qkv_rope_cache_rs(x, w, pos, cs, slots, kc, vc, Hq, ss, EPS)
+    qkv_ref = (_unit_norm(x) @ w.float().t()).to(bf).cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
+    close(q, q_ref)
+    close(kc, kr)
+    close(vc, vr)
+
+
+@pytest.mark.parametrize("batch", [1, 4])
+def test_llama_decode_gemv_chain_on_off(gpu, w4, monkeypatch, batch):
+    """2-layer Llama-3-8B-wide engine, graphs on: decode steps of 1 / 4 sequences with the GEMV
+    chain (five launches per layer, no add + RMSNorm) and without it both follow the fp32
+    dense oracle."""
+    from mlopamd.models import build_model
+    from mlopamd.models.config import get_config
+    from mlopamd.models.reference import dense_logits
+    from mlopamd.runtime.engine import Engine, EngineConfig
+    from mlopamd.runtime.sampler import SamplingParams
+
+    cfg = get_config("llama3-8b", num_layers=2)
+    model = build_model(cfg, device=gpu, seed=7)
+    prompts = [torch.randint(1000, 100000, (48,)).tolist() for _ in range(batch)]
+    outs = {}
+    for on in (False, True):
+        monkeypatch.setattr(ops, "GEMV_CHAIN", on)
+        assert model._chain_ok(batch) == on
+        ops._GEMM_USED.clear()  # before the engine: its graph captures run the decode forwards
+        eng = Engine(model, EngineConfig(max_num_seqs=batch, max_num_batched_tokens=512, max_model_len=128,
+                                         num_kv_blocks=batch * 8 + 1, use_graphs=True))
+        outs[on] = eng.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+        small = set(k[3] for k in ops._GEMM_USED if k[0] <= 4)
+        assert (ops.EPI_ADD_SS in small) == on, small
+    for on in (False, True):
+        for p, o in zip(prompts, outs[on]):
+            toks = list(p)
+            for t in o:
+                lg = dense_logits(model, toks)[-1]
+                best = int(lg.argmax())
+                assert t == best or float(lg[best] - lg[t]) < 0.1 * float(lg.std()), (on, len(toks), best, t)
+                toks.append(t)
+
+
 def test_gemm_res_ss_odd_group_count(gpu, w4):
     """N = 3840 = 256 mod 512: the band ticket's row sum reads 30 groups of 128 columns (7
     16-byte loads + one 8-byte tail).  A 4-wide-only loop would add the next row's first two
