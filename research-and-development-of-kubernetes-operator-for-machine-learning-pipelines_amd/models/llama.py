@@ -197,7 +197,8 @@ class LlamaModel:
         tp.all_reduce(h)
         residual = h
         M = ids.shape[0]
-        chain = tp.size == 1 and self._chain_ok(M)
+        # TP > 1: the decode (GEMV) form only, its residual adds riding in the all-reduces
+        chain = (tp.size == 1 or M <= ops.GEMV_CHAIN_MAX_M) and self._chain_ok(M)
         ss = None  # norm chain: x is None and ss holds the residual's row partials
         if chain and M <= ops.GEMV_CHAIN_MAX_M:
             # decode form: the QKV GEMV takes the embedding rows' factors itself (ss unused)
@@ -213,6 +214,9 @@ class LlamaModel:
                                           kv.v[i], self.n_q, ss, eps)
             a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
             nxt = self.layers[i + 1]["in_norm"] if i + 1 < len(self.layers) else self.final_norm
+            if chain and tp.size > 1:
+                x, ss = self._chain_layer_tp(i, a.view(a.shape[0], -1), residual, i + 1 == len(self.layers), eps, ss)
+                continue
             if chain:
                 x, ss = self._chain_layer(i, a.view(a.shape[0], -1), residual, i + 1 == len(self.layers), eps)
                 continue
@@ -256,6 +260,22 @@ class LlamaModel:
         ss = ops.ss_buffer(M, H, residual.device)
         ops.gemm_res_ss(act, L["down"], residual, ss)
         return None, ss
+
+    def _chain_layer_tp(self, i, a, residual, last, eps, ss):
+        """Tensor-parallel decode chain (M <= 4): the row-parallel O / down partial sums are
+        all-reduced AND added into the replicated residual in one launch (Group.all_reduce_add,
+        K15), gate_up and the next QKV take their rows' RMSNorm factors from the residual chunks
+        they stream (gemv.hip PRO_RS).  Two add + RMSNorm launches per layer fewer than
+        row_parallel_add_norm.  ss: the torch reference's row sums (unused by the GPU GEMVs)."""
+        L, tp = self.layers[i], self.ps.tp
+        o = ops.gemm(a, L["o"])
+        tp.all_reduce_add(o, residual)
+        act = ops.gemm_rs(residual, L["gate_up"], ops.ss_init(residual, ss), eps, ops.EPI_SILU_MUL)
+        d = ops.gemm(act, L["down"])
+        tp.all_reduce_add(d, residual)
+        if last:
+            return ops.rmsnorm(residual, self.final_norm, eps), None
+        return None, ops.ss_init(residual, ss)
 
     def logits_local(self, hidden: torch.Tensor) -> torch.Tensor:
         """[n, H] -> this rank's vocab shard of the logits [n, V/TP] (model dtype)."""

@@ -87,12 +87,16 @@ __device__ __forceinline__ void add_bf16x8(float (&acc)[8], const uint4 v) {
   }
 }
 
+// add_out: out is the residual stream, out = bf16(out + bf16(sum)) (norm.hip's add rounding;
+// each element read and written by its one owning thread): the tensor-parallel decode norm
+// chain's all-reduce + residual add in one launch (its consumers take their RMSNorm factors
+// from the residual themselves, gemv.hip PRO_RS)
 template <int NR>
 __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restrict__ out,
                                                                const uint16_t* __restrict__ in,
                                                                long n16, Peers peers, int rank,
                                                                uint32_t* epochs, int* err,
-                                                               size_t max_bytes) {
+                                                               size_t max_bytes, int add_out) {
   __shared__ uint32_t s_e;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) s_e = epochs[b] + 1;
@@ -144,6 +148,12 @@ __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restr
     for (int p = 0; p < NR; ++p) {
       const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.base[p] + doff)[i];
       add_bf16x8(acc, v);
+    }
+    if (add_out) {
+      float res[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      add_bf16x8(res, o[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = res[j] + bf2f(f2bf(acc[j]));
     }
     uint4 r;
     r.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
@@ -460,8 +470,9 @@ long car_max_bytes(long h) { return (long)get(h)->max_bytes; }
 
 int car_mem_mode(long h) { return get(h)->uncached; }
 
-void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot) {
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot, bool add_out) {
   CarState* s = get(h);
+  if (add_out && (two_shot || out == in)) throw std::runtime_error("custom all-reduce: add form is one-shot, out != in");
   if (numel % 8) throw std::runtime_error("custom all-reduce: numel must be a multiple of 8");
   if ((size_t)numel * 2 * (two_shot ? 2 : 1) > s->max_bytes)
     throw std::runtime_error("custom all-reduce: message too large");
@@ -483,10 +494,10 @@ void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t s
     return;
   }
   switch (s->world) {
-    case 1: car_oneshot_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
-    case 2: car_oneshot_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
-    case 4: car_oneshot_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
-    case 8: car_oneshot_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes); break;
+    case 1: car_oneshot_kernel<1><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes, add_out); break;
+    case 2: car_oneshot_kernel<2><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes, add_out); break;
+    case 4: car_oneshot_kernel<4><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes, add_out); break;
+    case 8: car_oneshot_kernel<8><<<g, blk, 0, st>>>(o, i, n16, s->peers, s->rank, s->epochs, s->err, s->max_bytes, add_out); break;
     default: throw std::runtime_error("custom all-reduce: world must be 1, 2, 4 or 8");
   }
   CAR_CHECK(hipGetLastError());

@@ -651,6 +651,17 @@ void car_all_reduce(int64_t h, Tensor out, Tensor inp, bool two_shot) {
   c10::DeviceGuard g(inp.device());
   mlop::car_all_reduce((long)h, out.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream(), two_shot);
 }
+// residual = bf16(residual + bf16(sum over ranks of inp)): one-shot all-reduce + the residual add
+void car_all_reduce_add(int64_t h, Tensor residual, Tensor inp) {
+  check_bf16(residual, "residual"); check_bf16(inp, "inp");
+  TORCH_CHECK(residual.numel() == inp.numel() && residual.is_contiguous() && inp.is_contiguous(),
+              "all_reduce_add: contiguous residual / inp of one size");
+  TORCH_CHECK(residual.data_ptr() != inp.data_ptr(), "all_reduce_add: residual must not alias inp");
+  TORCH_CHECK(inp.numel() % 8 == 0, "all_reduce_add: numel must be a multiple of 8");
+  TORCH_CHECK(inp.numel() * 2 <= mlop::car_max_bytes((long)h), "all_reduce_add: message exceeds the registered buffer");
+  c10::DeviceGuard g(inp.device());
+  mlop::car_all_reduce((long)h, residual.data_ptr(), inp.data_ptr(), (long)inp.numel(), cur_stream(), false, true);
+}
 // in-place broadcast of any contiguous device tensor (bytes % 16 == 0) from `root`
 void car_broadcast(int64_t h, Tensor buf, int64_t root) {
   TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "broadcast: contiguous device tensor");
@@ -741,6 +752,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);
   m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp, bool two_shot=False) -> ()");
+  m.def("car_all_reduce_add(int h, Tensor(a!) residual, Tensor inp) -> ()");
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
   m.def("car_all_gather(int h, Tensor(a!) out, Tensor piece) -> ()");
   m.def("car_error(int h) -> int", &car_error);
@@ -847,6 +859,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("argmax", &argmax);
   m.impl("sample", &sample);
   m.impl("car_all_reduce", &car_all_reduce);
+  m.impl("car_all_reduce_add", &car_all_reduce_add);
   m.impl("car_broadcast", &car_broadcast);
   m.impl("car_all_gather", &car_all_gather);
   m.impl("ep_dispatch", &ep_dispatch);

@@ -170,7 +170,9 @@ long car_create(int rank, int world, long max_bytes, int device);
 void car_ipc_handle(long h, void* out64);
 void car_open(long h, const void* handles);
 long car_max_bytes(long h);
-void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot = false);
+// add_out: out = bf16(out + bf16(sum)) (the residual stream; one-shot only, out != in)
+void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot = false,
+                    bool add_out = false);
 void car_broadcast(long h, void* out, const void* in, long nbytes, int root, hipStream_t st);
 void car_all_gather(long h, void* out, long out_bytes, const void* in, long nbytes, hipStream_t st);
 int car_error(long h);

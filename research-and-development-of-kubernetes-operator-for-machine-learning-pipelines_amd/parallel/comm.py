@@ -57,6 +57,15 @@ class Group:
             dist.all_reduce(x, group=self.handle)
         return x
 
+    def all_reduce_add(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """residual = bf16(residual + bf16(all_reduce(x))) in place (x may be overwritten): one
+        K15 launch when eligible, else the all-reduce and the add with the same rounding."""
+        if self.size > 1 and self.car is not None and self.car.can_all_reduce_add(x, residual):
+            return self.car.all_reduce_add(x, residual)
+        self.all_reduce(x)
+        residual.copy_((residual.float() + x.float()).to(residual.dtype))
+        return residual
+
     def all_gather(self, x: torch.Tensor, dim: int = -1) -> torch.Tensor:
         if self.size == 1:
             return x

@@ -64,6 +64,17 @@ class CustomAllReduce:
         torch.ops.mlop.car_all_reduce(self.h, out, x, bool(two_shot))
         return out
 
+    def can_all_reduce_add(self, x: torch.Tensor, residual: torch.Tensor) -> bool:
+        return (self.eligible(x) and 2 * x.numel() < TWO_SHOT_MIN_BYTES and residual.is_contiguous()
+                and residual.dtype == x.dtype and residual.numel() == x.numel()
+                and residual.data_ptr() != x.data_ptr())
+
+    def all_reduce_add(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """residual = bf16(residual + bf16(sum over ranks of x)) in ONE one-shot launch (the
+        tensor-parallel decode norm chain: the residual add rides in the all-reduce)."""
+        torch.ops.mlop.car_all_reduce_add(self.h, residual, x)
+        return residual
+
     def can_broadcast(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()
         return x.is_cuda and x.is_contiguous() and n % 16 == 0 and n <= self.max_bytes

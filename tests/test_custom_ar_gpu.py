@@ -128,6 +128,23 @@ def _worker(rank, world, port, out_dir):
             res["contention"].append(torch.equal(x.cpu(), _oracle(xs)) and torch.equal(buf.cpu(), src) and
                                      torch.equal(got.cpu(), torch.stack(pieces)))
         side.synchronize()
+        # all-reduce + residual add (the TP decode norm chain): residual = bf16(residual +
+        # bf16(sum)), interleaved with plain all-reduces on the same epochs, uneven arrival
+        res["add"] = []
+        for it, n in enumerate([8, 4096, 8192 * 4, 4 * 8192, 8000, 64 * 1024]):
+            xs = _inputs(500 + it, n, world)
+            r0 = torch.randn(n, generator=torch.Generator().manual_seed(550 + it)).to(torch.bfloat16)
+            x, r = xs[rank].cuda(), r0.cuda()
+            if rank == 1 and it % 2:
+                time.sleep(0.05)
+            car.all_reduce_add(x, r)
+            ys = _inputs(560 + it, 4096, world)
+            y = ys[rank].cuda()
+            car.all_reduce(y)
+            torch.cuda.synchronize()
+            exp = (r0.float() + _oracle(xs).float()).to(torch.bfloat16)
+            res["add"].append(torch.equal(r.cpu(), exp) and torch.equal(x.cpu(), xs[rank]) and
+                              torch.equal(y.cpu(), _oracle(ys)))
         # in place, back to back (parity reuse every second call)
         for it in range(6):
             xs = _inputs(50 + it, 4096, world)
@@ -142,19 +159,24 @@ def _worker(rank, world, port, out_dir):
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        resid = torch.zeros(8192, dtype=torch.bfloat16, device="cuda")
         with torch.cuda.graph(g, stream=s):
             car.all_reduce(static[0], outs[0])
             car.all_reduce(static[1], outs[1], two_shot=True)
+            car.all_reduce_add(static[0], resid)
         dist.barrier()
         for it in range(4):
             xs0, xs1 = _inputs(80 + it, 8192, world), _inputs(90 + it, 8192, world)
+            r0 = torch.randn(8192, generator=torch.Generator().manual_seed(95 + it)).to(torch.bfloat16)
             static[0].copy_(xs0[rank].cuda())
             static[1].copy_(xs1[rank].cuda())
+            resid.copy_(r0.cuda())
             torch.cuda.synchronize()
             g.replay()
             torch.cuda.synchronize()
             res["graph"].append(torch.equal(outs[0].cpu(), _oracle(xs0)) and
-                                torch.equal(outs[1].cpu(), _oracle(xs1)))
+                                torch.equal(outs[1].cpu(), _oracle(xs1)) and
+                                torch.equal(resid.cpu(), (r0.float() + _oracle(xs0).float()).to(torch.bfloat16)))
         res["error"] = car.error()
         res["uncached"] = car.uncached
     finally:
@@ -184,3 +206,4 @@ def test_custom_all_reduce_two_processes_one_gpu(world):
         assert all(res["bcast"]), (r, res["bcast"])
         assert all(res["gather"]), (r, res["gather"])
         assert all(res["contention"]), (r, res["contention"])
+        assert all(res["add"]), (r, res["add"])

@@ -57,6 +57,11 @@ def _worker(rank, world, port, out_dir, cfg_name):
             else:
                 eng.worker_loop()
                 res["worker_steps"] = eng.stats["worker_steps"]
+        from mlopamd import ops
+
+        # decode steps (<= 4 rows) ran the TP norm chain: row-scaled gate_up / QKV GEMVs, the
+        # residual adds inside the K15 all-reduces (Group.all_reduce_add)
+        res["tp_chain"] = any(k[0] <= 4 and k[3] & ops.EPI_RS for k in ops._GEMM_USED)
         res["car_error"] = ps.tp.car.error()
     finally:
         torch.cuda.synchronize()
@@ -132,6 +137,7 @@ def test_tp2_engine_on_gpu_with_custom_all_reduce(cfg_name):
     assert r0["car_error"] == 0 and r1["car_error"] == 0 and r1["worker_steps"] > 0
     assert r0["eager_steps_in_graphs"] == 0 and r0["graph_steps_in_graphs"] > 0
     assert r0["graph"] == r0["eager"]  # decode-graph replay (K15 inside) == eager TP
+    assert r0["tp_chain"] and r1["tp_chain"]
     from mlopamd.models import build_model
     from mlopamd.models.config import get_config
     from test_model_gpu import _check_greedy
