@@ -180,11 +180,11 @@ def test_gemv_chain_res_rs(gpu, w4, M):
     close(vc, vr)
 
 
-@pytest.mark.parametrize("batch", [1, 4])
+@pytest.mark.parametrize("batch", [1, 3, 4])
 def test_llama_decode_gemv_chain_on_off(gpu, w4, monkeypatch, batch):
-    """2-layer Llama-3-8B-wide engine, graphs on: decode steps of 1 / 4 sequences with the GEMV
-    chain (five launches per layer, no add + RMSNorm) and without it both follow the fp32
-    dense oracle."""
+    """2-layer Llama-3-8B-wide engine, graphs on: decode steps of 1 / 3 / 4 sequences with the
+    GEMV chain (five launches per layer, no add + RMSNorm; batch 3 replays the 4-row graph with
+    a padding row) and without it both follow the fp32 dense oracle."""
     from mlopamd.models import build_model
     from mlopamd.models.config import get_config
     from mlopamd.models.reference import dense_logits
