@@ -29,6 +29,10 @@
 //                 stores q to q_out and k / v straight into the paged cache
 //                 (rope_cache.hip's math and layouts, no [M, N] round trip, one
 //                 launch fewer per layer).
+//   EPI_RES       residual (C) += the outputs, in place (the decode norm chain's O / down).
+// Prologue RS (the decode norm chain's QKV / gate_up, norm weights folded into B): A is the
+// raw residual; each row's sum of squares accumulates from the chunks the dots stream (one
+// v_dot2 per chunk, no extra load) and rsqrt(mean + eps) scales the finished sums.
 // Prologue NORM (the decoder's residual add + RMSNorm feeding this projection, one
 // launch fewer per norm): instead of loading A, every activation chunk is formed from
 // the previous projection's output y and the residual stream, r = bf16(res + y), and
