@@ -49,14 +49,19 @@ class AttnMeta:
 # 128-token partitions: one 32-token page pair per wave at batch 1 (256: 312 tok/s, 128: 322,
 # 64: 246 - the reduce pass and partial traffic grow faster than the parallelism; run38/39)
 MIN_PART = int(os.environ.get("MLOP_ATTN_MIN_PART", 128))
+# workgroups a decode launch aims for before it splits contexts into partitions (2048 / 4096:
+# batch 64 11,361 / 11,221 vs 11,643 tok/s at 1024, batch 16 flat: scripts/history/r4_twgs.sh);
+# at most 2048, so tiles x kv heads x partitions stays within MetaBuffers.wp_capacity
+TARGET_WGS = min(2048, int(os.environ.get("MLOP_ATTN_TARGET_WGS", 1024)))
 
 
 def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int | None = None,
-                    target_wgs: int = 1024) -> tuple[int, int]:
+                    target_wgs: int | None = None) -> tuple[int, int]:
     """Split the KV range so a launch has >= ~target_wgs workgroups (256 CUs),
     partitions no shorter than ``min_part`` tokens; one partition when the batch
     already fills the chip (no reduce pass)."""
     min_part = MIN_PART if min_part is None else min_part
+    target_wgs = TARGET_WGS if target_wgs is None else target_wgs
     max_ctx = max(32, max_ctx)
     base = max(1, num_tiles * n_kv)
     if base >= target_wgs // 2:
