@@ -243,7 +243,7 @@ class MetaBuffers:
         ql_h[rows] = 1
         cl_h[rows] = ctx_lens
         self.ids_hn[:B] = last_tokens
-        self.lidx_hn[:B] = np.arange(B)
+        self.lidx_hn[:B] = np.arange(B)  # the identity: decode graphs skip the gather (Engine.capture_graphs)
         if pad_to > B:
             pad_rows = self.pad_rows(pad_to - B)
             pos_h[B:pad_to] = 0

@@ -1139,7 +1139,10 @@ class Engine:
             self._ids_gather = None
             B, toks_d = g
             self._src_d[:B].copy_(self._src_h[:B], non_blocking=True)
-            self.meta.ids_d[:B].copy_(toks_d.index_select(0, self._src_d[:B]))
+            if toks_d.dtype == self.meta.ids_d.dtype and toks_d.dim() == 1:  # one gather kernel, no copy
+                torch.index_select(toks_d, 0, self._src_d[:B], out=self.meta.ids_d[:B])
+            else:
+                self.meta.ids_d[:B].copy_(toks_d.index_select(0, self._src_d[:B]))
         if self.step_sync is not None:
             t0 = time.perf_counter()
             self.step_sync.send(self, kind, T, nt, nl, part, nparts, bucket, npt, int(greedy))
@@ -1257,15 +1260,17 @@ class Engine:
                 part, nparts = plan_partitions(b, m.n_kv, self.max_model_len)
                 meta = self.meta.meta(b, b, b, part, nparts)
                 ids = self.meta.ids_d[:b]
+                # decode fills (fill_decode) give every row, padding included, its own logits row
+                # in order: logits_idx is the identity, so the graph skips the row gather
                 for _ in range(2 if bi == 0 else 1):  # warm-up (allocator, autotune, lazy init)
-                    m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                    m.logits_local(m.forward(ids, meta, self.kv))
                 stream.synchronize()
                 if verbose:
                     print(f"[engine] capturing decode graph {bi + 1}/{len(self.buckets)} (batch {b}) "
                           f"at {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
-                    logits = m.logits_local(m.forward(ids, meta, self.kv)[meta.logits_idx])
+                    logits = m.logits_local(m.forward(ids, meta, self.kv))
                 self.graphs[b] = (g, logits)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
