@@ -480,7 +480,7 @@ NORM_CHAIN = os.environ.get("MLOP_NORM_CHAIN", "1")
 # add into the residual in place, QKV and gate_up take each row's factor from the residual
 # chunks they stream, so a layer has no add + RMSNorm launch.  "0" keeps the decode norms.
 GEMV_CHAIN = os.environ.get("MLOP_GEMV_CHAIN", "1") == "1"
-GEMV_CHAIN_MAX_M = 4
+GEMV_CHAIN_MAX_M = min(8, max(1, int(os.environ.get("MLOP_GEMV_CHAIN_MAX_M", 4))))  # = gemv.hip gemv_chain_max_m
 
 
 def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:

@@ -324,7 +324,7 @@ bool gemm_res_ss(Tensor residual, Tensor a, Tensor w, Tensor ss_out) {
                   residual.stride(0) % 8 == 0, "residual [M, N]");
   TORCH_CHECK(N % 128 == 0, "N % 128");
   check_ss(ss_out, M, N, "ss");
-  if (M <= 4) {  // decode sizes: the GEMV chain (gemv.hip EPI_RES); its consumers take their row
+  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: the GEMV chain (gemv.hip EPI_RES); its consumers take their row
                  // factors from the residual itself, so ss_out is not written
     if (residual.stride(0) != N || !mlop::gemv_chain_takes((int)M, (int)N, (int)K, 0)) return false;
     c10::DeviceGuard g(a.device());
@@ -353,7 +353,7 @@ bool gemm_rs(Tensor out, Tensor a, Tensor w, Tensor ss_in, double eps, int64_t e
                   out.stride(0) % 8 == 0, "out [M, N or N/2]");
   TORCH_CHECK(K % 128 == 0, "K % 128");
   check_ss(ss_in, M, K, "ss");
-  if (M <= 4) {  // decode sizes: gemv.hip PRO_RS, row factors from the streamed chunks (ss_in unused)
+  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: gemv.hip PRO_RS, row factors from the streamed chunks (ss_in unused)
     if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi)) return false;
     c10::DeviceGuard g(a.device());
     mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
@@ -391,7 +391,7 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
-  if (M <= 4) {  // decode sizes: gemv.hip PRO_RS + the RoPE / paged K/V epilogue (ss_in unused)
+  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: gemv.hip PRO_RS + the RoPE / paged K/V epilogue (ss_in unused)
     if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, 3)) return false;
     c10::DeviceGuard g(a.device());
     mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re,
@@ -477,7 +477,7 @@ bool gemm_norm_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor res_out
 }
 
 bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
-  return M <= 4 && mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
+  return mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
 }
 
 bool gemm_norm_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {

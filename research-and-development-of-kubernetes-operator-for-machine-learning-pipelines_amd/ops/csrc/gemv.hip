@@ -478,24 +478,24 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 template <int EPI, int PRO = PRO_NONE>
 void run_gemv(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
               int N, int K, const RopeEpi& re, hipStream_t st, const NormPro& np = NormPro{}) {
-  if constexpr (PRO != PRO_NONE || EPI == EPI_RES) {  // the norm-fused forms: decode sizes only (M <= 4)
+  if constexpr (PRO == PRO_NORM) {  // the fused-norm prologue: decode sizes only (M <= 4)
     switch (M) {
       case 1: run_gemv_m<1, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
       case 2: run_gemv_m<2, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
       case 3: run_gemv_m<3, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
       default: run_gemv_m<4, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
     }
-    return;
-  }
-  switch (M) {
-    case 1: run_gemv_m<1, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 2: run_gemv_m<2, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 3: run_gemv_m<3, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 4: run_gemv_m<4, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 5: run_gemv_m<5, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 6: run_gemv_m<6, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    case 7: run_gemv_m<7, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    default: run_gemv_m<8, EPI, PRO_NONE>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+  } else {
+    switch (M) {
+      case 1: run_gemv_m<1, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 2: run_gemv_m<2, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 3: run_gemv_m<3, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 4: run_gemv_m<4, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 5: run_gemv_m<5, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 6: run_gemv_m<6, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      case 7: run_gemv_m<7, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+      default: run_gemv_m<8, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
+    }
   }
 }
 
@@ -636,13 +636,22 @@ void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M,
   else run_gemv<EPI_NONE, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
 }
 
-// The decode norm chain (M <= 4, TP = 1, norm weights folded into the consuming projections:
+// The decode norm chain (M <= gemv_chain_max_m(), norm weights folded into the consuming projections:
 // LlamaModel.fold_norms): O and down add their output into the residual in place (EPI_RES),
 // QKV and gate_up read the raw residual and scale each row's sums by rsqrt(mean(a^2) + eps)
 // taken from the chunks they stream anyway (PRO_RS).  A decode layer is then five launches
 // and no add + RMSNorm pass: the GEMV form of gemm_w4.hip's large-M chain (W4_ADD_SS / W4_RS).
+// rows the chain's GEMV form takes (MLOP_GEMV_CHAIN_MAX_M, default 4, at most 8; above
+// gemv_max_m() the GEMV takes nothing anyway).  Measured (scripts/history/r4_chain8.sh): the
+// GEMV with the chain at 6 / 8 rows streams 1,419 / 1,612 tok/s against the MFMA path's
+// 1,522 / 1,936 (its split-K reduce already carries the add + RMSNorm), so 4 stays.
+int gemv_chain_max_m() {
+  static const int v = std::min(8, std::max(1, env_int("MLOP_GEMV_CHAIN_MAX_M", 4)));
+  return v;
+}
+
 bool gemv_chain_takes(int M, int N, int K, int epi) {
-  return M <= 4 && gemv_takes(M, N, K, epi);
+  return M <= gemv_chain_max_m() && gemv_takes(M, N, K, epi);
 }
 
 void launch_gemv_rs(const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K, int epi,

@@ -110,6 +110,7 @@ bool gemv_norm_takes(int M, int N, int K, int epi);
 // decode norm chain (gemv.hip PRO_RS / EPI_RES, M <= 4): C = epi(rowscale(A) . B^T) with
 // rowscale = rsqrt(mean(A_row^2) + eps) (norm weights folded into B); residual += A . B^T
 bool gemv_chain_takes(int M, int N, int K, int epi);
+int gemv_chain_max_m();
 void launch_gemv_rs(const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K, int epi,
                     const RopeEpi& re, float eps, hipStream_t st);
 void launch_gemv_res(const void* A, int lda, const void* B, void* residual, int M, int N, int K, hipStream_t st);
