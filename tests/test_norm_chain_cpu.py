@@ -72,3 +72,24 @@ def test_fold_norms_keeps_the_function():
     model.fold_norms()
     assert model.unit_norms
     torch.testing.assert_close(dense_logits(model, toks), before, rtol=1e-4, atol=1e-4)
+
+
+def test_ss_init_and_all_reduce_add_fallback():
+    """The decode chain's CPU pieces: ss_init fills the torch reference's row partials / totals
+    (the GPU GEMV form ignores them), and Group.all_reduce_add without the K15 buffers adds
+    the (here single-rank) sum into the residual with the kernel's rounding,
+    bf16(residual + bf16(sum))."""
+    from mlopamd.parallel.comm import Group
+
+    torch.manual_seed(0)
+    M, H = 3, 256
+    x = (3 * torch.randn(M, H)).to(torch.bfloat16)
+    ss = ops.ss_init(x, ops.ss_buffer(M, H, "cpu").fill_(float("nan")))
+    part, tot = ops.ss_parts(ss, M, H)
+    torch.testing.assert_close(part, x.float().pow(2).view(M, H // 128, 128).sum(-1))
+    torch.testing.assert_close(tot, x.float().pow(2).sum(-1))
+    res = torch.randn(M, H).to(torch.bfloat16)
+    y = torch.randn(M, H).to(torch.bfloat16)
+    exp = (res.float() + y.float()).to(torch.bfloat16)
+    out = Group().all_reduce_add(y.clone(), res)
+    assert out is res and torch.equal(res, exp)
