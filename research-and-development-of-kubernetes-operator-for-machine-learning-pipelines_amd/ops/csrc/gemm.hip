@@ -1038,9 +1038,19 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // the ping-pong kernel with its general stream-K tail
     static const int w4_min_tiles = env_int("MLOP_GEMM_W4_MIN_TILES", 192);
     const bool w4_fills = t256 >= w4_min_tiles || gemm_w4_split_ok((int)t256, K / kBK);
-    if (big == 5 && !(mrows >= big_min_m && !grouped && w4_fills && gemm_w4_ok(M, N, K, K, K))) {
-      if (mrows >= big_min_m && !grouped && pp_ok) { p.BN = 256; p.variant = 3; }
-    } else if (big && mrows >= big_min_m && !grouped && (big < 3 || pp_ok)) {
+    // Wide projections take the large-M kernels from 512 rows: gate_up / lm_head at M = 512 /
+    // 768 ran 127 -> 87 / 191 -> 153 us (8B) and 511 -> 404 us (70B gate_up), batch-512 serving
+    // +5.3 %; narrow ones lose there (o / down at M = 512: 31 -> 48 / 66 -> 124 us) and keep the
+    // 256 x 128 kernel (scripts/history/r4_bigminm.sh, r4_bigminm2.sh, r4_widemin.sh).
+    // Below ~72 tiles of 256 x 256 (o / down at M = 512 - 1024: 32 - 64 tiles) the 256 x 128
+    // kernel beats them at every M measured short of 2048 (o at M = 1024: 44.7 vs 48.6 us, down
+    // 114.7 vs 129.5); from 72 tiles (qkv at M = 768, 70B qkv at 512) the large-M kernels win.
+    static const int wide_min_m = env_int("MLOP_GEMM_BIG_WIDE_MIN_M", 512);
+    static const int mid_tiles = env_int("MLOP_GEMM_BIG_MID_TILES", 72);
+    const int big_from = t256 >= mid_tiles ? std::min(big_min_m, wide_min_m) : std::max(big_min_m, 2048);
+    if (big == 5 && !(mrows >= big_from && !grouped && w4_fills && gemm_w4_ok(M, N, K, K, K))) {
+      if (mrows >= big_from && !grouped && pp_ok) { p.BN = 256; p.variant = 3; }
+    } else if (big && mrows >= big_from && !grouped && (big < 3 || pp_ok)) {
       p.BN = 256;
       p.variant = big;
     }

@@ -1,4 +1,4 @@
-"""GEMM microbench on the Llama-3-8B projection shapes: the hand-written MFMA
+"""GEMM microbench on the Llama-3-8B (or BENCH_MODEL=70b: Llama-3-70B) projection shapes: the hand-written MFMA
 GEMM (forced, ``ops.GEMM_BACKEND = "mlop"``) vs torch.matmul (hipBLASLt).
 One process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), random data.
 Env knobs of the C++ planner are swept by re-running with MLOP_GEMM_* set."""
@@ -14,10 +14,13 @@ from mlopamd import ops  # noqa: E402
 ops.load()
 dev = torch.device("cuda")
 Ms = [int(m) for m in os.environ.get("BENCH_MS", "1,64,128,256,512,8192").split(",")]
+PROJ = {"8b": (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
+                ("down", 4096, 14336), ("lm_head", 128256, 4096)),
+        "70b": (("qkv", 10240, 8192), ("o", 8192, 8192), ("gate_up", 57344, 8192),
+                ("down", 8192, 28672), ("lm_head", 128256, 8192))}[os.environ.get("BENCH_MODEL", "8b")]
 shapes = []
 for M in Ms:
-    for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096),
-                       ("down", 4096, 14336), ("lm_head", 128256, 4096)):
+    for name, N, K in PROJ:
         if name == "lm_head" and M > 512:
             continue
         shapes.append((name, M, N, K))
