@@ -1028,7 +1028,11 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     static const int big_min_m = env_int("MLOP_GEMM_BIG_MIN_M", 1024);
     p.BM = 256;
     p.BN = 128;
-    static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 192);
+    // 128: o / down at 2049-2816 rows (the mixed steps of batch ~512: 144-176 tiles, no K-half
+    // tail for the four-wave kernel) ran on the 256 x 128 kernel at 0.55x hipBLASLt; the
+    // ping-pong kernel's stream-K tail takes them (o at M = 2560: 122 -> 88 us, down 394 -> 269;
+    // scripts/history/r4_m2560.sh)
+    static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 128);
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     // below pp_min_tiles the 256x256 grid leaves CUs idle, unless the stream-K tail can cut
     // every tile in two (T <= C / 2): o / down at M = 2040 (128 tiles)
