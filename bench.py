@@ -100,12 +100,12 @@ def parse(argv=None):
 
 
 def _gpu_count() -> int:
-    """Visible GPUs WITHOUT initialising HIP (``device_count`` does not on this image): the
-    launcher parent must never touch the GPU before its rank children exist."""
-    try:
-        return torch.cuda.device_count()
-    except Exception:  # noqa: BLE001
-        return 0
+    """Visible GPUs from the visible-devices env / the KFD topology in sysfs, never through HIP
+    or torch (runtime/rank_launcher.py ``visible_gpu_count``): the launcher parent must not
+    touch the GPU before its rank children exist, whatever torch's device count would do."""
+    from mlopamd.runtime.rank_launcher import visible_gpu_count
+
+    return visible_gpu_count()
 
 
 def _process_ready(a, device_index: int | None) -> dict:

@@ -121,19 +121,17 @@ class GpuPool:
 
     @classmethod
     def detect(cls, slots_per_gpu: int = 1) -> "GpuPool":
-        """Devices visible to this process: HIP_VISIBLE_DEVICES, else the driver's count
-        (``torch.cuda.device_count`` does not initialise HIP on this image)."""
+        """Devices visible to this process: HIP_VISIBLE_DEVICES, else the KFD topology in sysfs
+        (``rank_launcher.visible_gpu_count``: no HIP / torch call, the launcher of predictor
+        processes never touches a GPU itself)."""
         vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
         if vis:
             return cls([int(x) for x in vis.split(",") if x.strip()], slots_per_gpu)
         n = int(os.environ.get("MLOP_NODE_GPUS", "-1"))
         if n < 0:
-            try:
-                import torch
+            from ..runtime.rank_launcher import visible_gpu_count
 
-                n = torch.cuda.device_count()
-            except Exception:  # noqa: BLE001
-                n = 0
+            n = visible_gpu_count()
         return cls(n, slots_per_gpu)
 
     @property
@@ -164,13 +162,20 @@ class ProcessLauncher:
     ``command`` / ``args`` as the Seldon controller's pod would (``python`` resolved to this
     interpreter, ``--port`` rewritten to a free local port), with the container env and the
     GPUs the container requests (``amd.com/gpu`` -> ``HIP_VISIBLE_DEVICES`` from ``gpus``, a
-    ``GpuPool``).  A TP predictor's container (``--tp N``) launches its own N rank processes
-    (runtime/server.py ``launch_ranks``)."""
+    ``GpuPool``).  A TP / EP predictor's container (``--tp N`` / ``--ep N``) launches its own N
+    rank processes (runtime/rank_launcher.py).
+
+    ``share_gpu``: the one-GPU node rehearsal of multi-GPU pods.  A pod that asks for k > 1 GPUs
+    gets ONE device and ``MLOP_SHARE_GPU=1``, so its N ranks all run on that device over gloo
+    with the IPC all-reduce / expert-exchange kernels forced (what ``bench.py --share-gpu``
+    does): the operator -> SeldonDeployment -> pod -> launcher -> ranks -> HTTP path runs
+    end to end on a box with one MI355X."""
 
     def __init__(self, scraper=None, extra_env: dict | None = None, python: str = sys.executable,
                  ready_timeout_s: float = 600.0, per_predictor_env: dict | None = None,
-                 gpus: GpuPool | int | None = None, gpu_resource: str = "amd.com/gpu"):
+                 gpus: GpuPool | int | None = None, gpu_resource: str = "amd.com/gpu", share_gpu: bool = False):
         self.scraper, self.extra_env, self.python = scraper, extra_env or {}, python
+        self.share_gpu = share_gpu
         self.per_predictor_env = per_predictor_env or {}  # predictor name -> env (fault injection)
         self.ready_timeout_s = ready_timeout_s
         if gpus is None and self.extra_env.get("MLOP_DEVICE") == "cpu":
@@ -207,6 +212,10 @@ class ProcessLauncher:
         for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):  # the pod is its own rank group
             env.pop(k, None)
         need = seldon.gpus_of(pod.spec, self.gpu_resource)
+        if self.share_gpu and need > 1:  # rehearsal: the pod's ranks time-share one device
+            env["MLOP_SHARE_GPU"] = "1"
+            pod.extra["requested_gpus"] = need
+            need = 1
         devs = self.gpus.acquire(need)  # raises (unschedulable) when the node has no free GPUs
         pod.extra["gpus"] = devs
         if need:

@@ -33,6 +33,9 @@ from .crd import (EV_ALIAS_NOT_FOUND, EV_NEW_VERSION, EV_PREDICTOR_READY, EV_PRE
 from .kube import ApiError
 from .mlflow import NotFound, RegistryError, RegistryUnavailable
 from .placement import plan
+
+ANN = seldon.ANN_PREFIX
+SELDON_POD_LABEL = seldon.POD_LABEL
 from .prometheus import MetricsUnavailable, get_model_metrics, gpu_guard_queries, should_promote
 
 PH_DEPLOYING, PH_READY, PH_CANARY = "Deploying", "Ready", "Canary"
@@ -46,6 +49,7 @@ class MlflowModelReconciler:
         self.settings = settings or OperatorSettings()
         self.metrics = metrics  # optional OperatorMetrics (reconcile latency, CR->ready)
         self._kicks = {}
+        self.placement_notes: dict = {}  # (ns, name) -> {predictor: why it cannot be placed}
 
     # ------------------------------------------------------------- k8s --
     async def _get_cr(self, ns, name):
@@ -128,7 +132,7 @@ class MlflowModelReconciler:
         # per-node accounting from the pods bound to each node (GPU limits of pods that still
         # hold their devices); without pod access, the SeldonDeployments' total is charged to
         # the cluster and the roomiest node reports min(its GPUs, the cluster's free GPUs)
-        per_node = await self._gpus_used_per_node(res)
+        per_node = await self._gpus_used_per_node(res, exclude)
         if per_node is not None:
             for c in cands:
                 c["free"] = max(0, c["gpus"] - per_node.get(c["node"], 0))
@@ -154,9 +158,12 @@ class MlflowModelReconciler:
             out["hbm_gb"] = best["hbm_gb"]
         return out
 
-    async def _gpus_used_per_node(self, res: str) -> dict | None:
+    async def _gpus_used_per_node(self, res: str, exclude: tuple | None = None) -> dict | None:
         """{node: GPUs requested by the pods bound to it and not finished}, or None when pods
-        cannot be listed (no RBAC / no pod API in this cluster emulation)."""
+        cannot be listed (no RBAC / no pod API in this cluster emulation).  ``exclude`` =
+        (namespace, SeldonDeployment name): that deployment's OWN predictor pods (Seldon v1
+        labels every pod it creates ``seldon-deployment-id: <SD name>``) are not charged, so
+        the model's running predictors never count against its own re-planned placement."""
         try:
             pods = await self.kube.list("", "v1", None, "pods")
         except Exception:  # noqa: BLE001
@@ -168,6 +175,9 @@ class MlflowModelReconciler:
             spec, st = pod.get("spec") or {}, pod.get("status") or {}
             node = spec.get("nodeName")
             if not node or st.get("phase") in ("Succeeded", "Failed"):
+                continue
+            pmd = pod.get("metadata") or {}
+            if exclude and (pmd.get("namespace"), (pmd.get("labels") or {}).get(SELDON_POD_LABEL)) == exclude:
                 continue
             n = 0
             for c in spec.get("containers") or []:
@@ -188,7 +198,21 @@ class MlflowModelReconciler:
         rt = spec.runtime or tags.get("mlop.runtime") or (seldon.RUNTIME_LLM if arch else seldon.RUNTIME_STOCK)
         return rt, arch
 
+    @staticmethod
+    def _placement_key(spec: ModelSpec, arch: str) -> str:
+        """Everything a version's placement is planned from, besides the cluster's momentary
+        free capacity: a deployed predictor keeps its placement while this key is unchanged."""
+        return (f"{arch}|tp={spec.tensor_parallel or 0}|ep={spec.expert_parallel or 0}"
+                f"|len={spec.max_model_len or 4096}|seqs={spec.max_num_seqs or 256}"
+                f"|kvf={spec.kv_target_fraction or 0.5}|replicas={spec.replicas}")
+
     async def desired_sd(self, body: dict, spec: ModelSpec, status: dict) -> dict | None:
+        """The SeldonDeployment this CR wants now.  Placement is decided ONCE per version, like
+        a scheduled pod that does not move: a predictor already deployed with a placement that
+        fit, planned from the same inputs (``_placement_key``), keeps it — so level-triggered
+        reconciles never rewrite the SD spec because GPU counts moved (its own pods, a rollout).
+        Only the stable plan goes into the predictor annotations; the planner's reason text,
+        which quotes momentary free counts, goes to the CR status (``placement``)."""
         md = body["metadata"]
         cur, prev = status.get("currentModelVersion"), status.get("previousModelVersion")
         if cur is None:
@@ -201,29 +225,43 @@ class MlflowModelReconciler:
         ct = int(status.get("canaryTraffic") or 0)
         versions = [(prev, 100 - ct), (cur, ct)] if split else [(cur, 100)]
         node = None
+        existing = None
+        notes = {}
         for v, traffic in versions:
             uri, mv = await self._uri(spec, v)
             runtime, arch = self._runtime_of(spec, mv)
             placement = None
             if runtime == seldon.RUNTIME_LLM and arch:
-                if node is None:
-                    node = await self.node_capacity(exclude=(md["namespace"], md["name"]))
-                p = plan(arch, max_model_len=spec.max_model_len or 4096, max_num_seqs=spec.max_num_seqs or 256,
-                         hbm_gb=node.get("hbm_gb", self.settings.hbm_per_gpu_gb),
-                         gpus_per_node=node.get("gpus", self.settings.gpus_per_node),
-                         requested_tp=spec.tensor_parallel, requested_ep=spec.expert_parallel,
-                         kv_target_fraction=spec.kv_target_fraction or 0.5,
-                         free_gpus=node.get("free_gpus"))
-                placement = {"tensorParallel": p.tensorParallel, "expertParallel": p.expertParallel,
-                             "gpus": p.gpus, "weightGBPerGPU": p.weightGBPerGPU,
-                             "kvTokenCapacity": p.kvTokenCapacity, "fits": p.fits}
-                if not p.fits:
-                    placement["reason"] = p.reason + (f" [GPU accounting: {node['accounting']}]"
-                                                      if node.get("accounting") else "")
-                if node.get("node"):
-                    placement["node"] = node["node"]
-                if node.get("free_gpus") is not None:  # the canary's second predictor needs its own
-                    node = dict(node, free_gpus=max(0, node["free_gpus"] - p.gpus * spec.replicas))
+                if existing is None:
+                    existing = {p["name"]: p for p in ((await self._get_sd(md["namespace"], md["name"])) or {})
+                                .get("spec", {}).get("predictors", [])}
+                key = self._placement_key(spec, arch)
+                ann = (existing.get(seldon.predictor_name(v)) or {}).get("annotations") or {}
+                if ann.get(f"{ANN}placementKey") == key and ann.get(f"{ANN}fits") == "True":
+                    placement = {k[len(ANN):]: val for k, val in ann.items()
+                                 if k.startswith(ANN) and k != f"{ANN}runtime"}
+                    gpus_held = int(placement.get("gpus", 0))
+                else:
+                    if node is None:
+                        node = await self.node_capacity(exclude=(md["namespace"], md["name"]))
+                    p = plan(arch, max_model_len=spec.max_model_len or 4096, max_num_seqs=spec.max_num_seqs or 256,
+                             hbm_gb=node.get("hbm_gb", self.settings.hbm_per_gpu_gb),
+                             gpus_per_node=node.get("gpus", self.settings.gpus_per_node),
+                             requested_tp=spec.tensor_parallel, requested_ep=spec.expert_parallel,
+                             kv_target_fraction=spec.kv_target_fraction or 0.5,
+                             free_gpus=node.get("free_gpus"))
+                    placement = {"tensorParallel": p.tensorParallel, "expertParallel": p.expertParallel,
+                                 "gpus": p.gpus, "weightGBPerGPU": p.weightGBPerGPU,
+                                 "kvTokenCapacity": p.kvTokenCapacity, "fits": p.fits, "placementKey": key}
+                    if node.get("node"):
+                        placement["node"] = node["node"]
+                    if not p.fits:
+                        notes[seldon.predictor_name(v)] = p.reason + (
+                            f" [GPU accounting: {node['accounting']}]" if node.get("accounting") else "")
+                    gpus_held = p.gpus
+                if node is not None and node.get("free_gpus") is not None:
+                    # the canary's second predictor needs its own GPUs beside this one's
+                    node = dict(node, free_gpus=max(0, node["free_gpus"] - gpus_held * spec.replicas))
             elif runtime == seldon.RUNTIME_LLM and (spec.tensor_parallel or spec.expert_parallel):
                 # a checkpoint of unknown architecture (no preset): honour the requested degrees
                 tp = int(spec.tensor_parallel or 1)
@@ -239,6 +277,7 @@ class MlflowModelReconciler:
                 image=self.settings.runtime_image, gpu_resource=self.settings.gpu_resource,
                 model_name=spec.model_name, deployment=md["name"], namespace=md["namespace"],
                 architecture=arch, engine_args=engine_args))
+        self.placement_notes[(md["namespace"], md["name"])] = notes
         return seldon.build_seldon_deployment(md["name"], md["namespace"], body, preds)
 
     # -------------------------------------------------------------- run --
@@ -349,6 +388,10 @@ class MlflowModelReconciler:
 
         # ---- level-triggered apply of the desired deployment
         desired = await self.desired_sd(body, spec, status)
+        notes = self.placement_notes.get((ns, name)) or None
+        if desired is not None and status.get("placement") != notes:  # why a predictor cannot be placed
+            body = await self._patch_status(ns, name, {"placement": notes})
+            status["placement"] = notes
         if desired is not None:
             sd = await self.apply_sd(desired, logger)
         else:

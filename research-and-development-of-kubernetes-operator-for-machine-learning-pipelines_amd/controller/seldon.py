@@ -25,6 +25,8 @@ RUNTIME_STOCK = "MLFLOW_SERVER"
 RUNTIME_LLM = "mlop-llm"
 RUNTIME_SKLEARN = "mlop-sklearn"
 RUNTIMES = (RUNTIME_STOCK, RUNTIME_LLM, RUNTIME_SKLEARN)
+ANN_PREFIX = "mlop.amd.com/"  # predictor annotations: runtime + the HBM-aware placement
+POD_LABEL = "seldon-deployment-id"  # Seldon v1 labels every predictor pod with its SD's name
 
 
 def predictor_name(version) -> str:
@@ -92,9 +94,9 @@ def build_predictor(version, model_uri: str, secret: str | None, traffic: int, r
     if gpus:
         spec["volumes"] = [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]
     pred["componentSpecs"] = [{"spec": spec}]
-    ann = {"mlop.amd.com/runtime": runtime}
+    ann = {f"{ANN_PREFIX}runtime": runtime}
     for k, v in (placement or {}).items():
-        ann[f"mlop.amd.com/{k}"] = str(v)
+        ann[f"{ANN_PREFIX}{k}"] = str(v)
     pred["annotations"] = ann
     return pred
 

@@ -7,7 +7,7 @@
 //   [ChanHeader | nslots x 128-B slots]
 //   producer: wait until the slowest consumer is < nslots behind, copy the words into slot
 //             seq % nslots, then seq.store(seq + 1, release);
-//   consumer: spin (pause, then yield) until seq > its own count (acquire), copy the slot, then
+//   consumer: spin (pause, then yield, then sleep) until seq > its own count (acquire), copy the slot, then
 //             its ack.store(count + 1, release) -- every counter on its own cache line.
 // Both sides take a timeout (microseconds) and return false when it expires, so the Python
 // loop around them never blocks inside a C++ call indefinitely (and drops the GIL in between).
@@ -65,7 +65,11 @@ Chan* get(long hd) {
   return reinterpret_cast<Chan*>(hd);
 }
 
-// spin briefly (a step header is expected within microseconds), then yield the core
+// spin briefly (a step header is expected within microseconds), then yield the core, then
+// back off to short sleeps: a parked worker of an idle predictor must not hold a host core at
+// 100 % (7 cores at TP = 8).  Up to 2 ms of waiting: yield (sub-microsecond wake-up); up to
+// 50 ms: 20 us sleeps (the header of a step still arrives well ahead of its device work under
+// one-step-ahead scheduling); beyond: 500 us sleeps (an idle group).
 template <class F>
 bool wait_until(F ready, long timeout_us) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -75,11 +79,13 @@ bool wait_until(F ready, long timeout_us) {
       __builtin_ia32_pause();
       continue;
     }
-    if ((i & 63) == 0 &&
-        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >=
-            timeout_us)
-      return false;
-    std::this_thread::yield();
+    const long waited =
+        (long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (waited >= timeout_us) return false;
+    if (waited < 2000)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(waited < 50000 ? 20 : 500));
   }
 }
 

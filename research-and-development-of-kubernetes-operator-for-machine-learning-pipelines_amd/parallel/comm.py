@@ -175,27 +175,55 @@ class HostChannel:
 
     SLOTS = 64
 
+    class Unavailable(RuntimeError):
+        """Raised on EVERY rank of the group when any rank could not create or map the channel
+        (callers fall back to gloo together)."""
+
     def __init__(self, cpu_group, words: int = 16):
         import uuid
 
+        self.words = words
+        self.h = 0
+        self.rank = dist.get_rank(cpu_group)
+        self.size = dist.get_world_size(cpu_group)
+        name, err = None, ""
+        if self.rank == 0:
+            name = f"/mlop-chan-{uuid.uuid4().hex[:16]}"
+            try:
+                self.h = self._create(name)
+            except Exception as e:  # noqa: BLE001 - agreed on below, every rank falls back
+                err, name = f"{type(e).__name__}: {e}", None
+        box = [name]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(cpu_group, 0), group=cpu_group)
+        if self.rank != 0:
+            if box[0] is None:
+                err = "the leader could not create the channel"
+            else:
+                try:
+                    self.h = self._open(box[0])
+                except Exception as e:  # noqa: BLE001
+                    err = f"{type(e).__name__}: {e}"
+        # every rank's verdict (and a barrier: nobody unlinks before all have mapped)
+        ok = torch.tensor([0 if err else 1], dtype=torch.int64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group)
+        if self.rank == 0 and name is not None:
+            torch.ops.mlop.chan_unlink(name)
+        if not int(ok.item()):
+            self.close()
+            raise HostChannel.Unavailable(err or "another rank could not map the channel")
+        self._buf = torch.zeros(words, dtype=torch.int64)
+
+    def _create(self, name: str) -> int:
         from .. import ops
 
         ops.load()
-        self.words = words
-        self.rank = dist.get_rank(cpu_group)
-        self.size = dist.get_world_size(cpu_group)
-        box = [f"/mlop-chan-{uuid.uuid4().hex[:16]}" if self.rank == 0 else None]
-        name = None
-        if self.rank == 0:
-            name = box[0]
-            self.h = torch.ops.mlop.chan_create(name, self.SLOTS, self.size - 1)
-        dist.broadcast_object_list(box, src=dist.get_global_rank(cpu_group, 0), group=cpu_group)
-        if self.rank != 0:
-            self.h = torch.ops.mlop.chan_open(box[0])
-        dist.barrier(group=cpu_group)
-        if self.rank == 0:
-            torch.ops.mlop.chan_unlink(name)
-        self._buf = torch.zeros(words, dtype=torch.int64)
+        return torch.ops.mlop.chan_create(name, self.SLOTS, self.size - 1)
+
+    def _open(self, name: str) -> int:
+        from .. import ops
+
+        ops.load()
+        return torch.ops.mlop.chan_open(name)
 
     def send(self, vals: torch.Tensor, timeout_s: float = 600.0) -> None:
         import time
@@ -206,11 +234,13 @@ class HostChannel:
                 raise TimeoutError("host channel: consumers stopped reading")
 
     def recv(self, out: torch.Tensor, timeout_s: float = 3600.0) -> torch.Tensor:
-        """Blocks (20 ms slices, the GIL dropped in between) until the next message arrives."""
+        """Blocks (250 ms slices; the op runs without the GIL) until the next message arrives.
+        Inside a slice the native wait spins, yields, then sleeps (shm_channel.cc wait_until),
+        so a parked worker of an idle predictor costs ~1 % of a core, not a whole one."""
         import time
 
         t0 = time.monotonic()
-        while not torch.ops.mlop.chan_recv(self.h, self.rank - 1, out, 20000):
+        while not torch.ops.mlop.chan_recv(self.h, self.rank - 1, out, 250000):
             if time.monotonic() - t0 > timeout_s:
                 raise TimeoutError("host channel: no message from the producer")
         return out

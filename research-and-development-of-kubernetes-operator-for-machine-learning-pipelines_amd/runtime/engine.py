@@ -78,7 +78,11 @@ class StepSync:
         if cpu_group is not None and os.environ.get("MLOP_TP_HEADER", "shm") == "shm":
             from ..parallel.comm import HostChannel
 
-            self.chan = HostChannel(cpu_group, words=self.NHDR)
+            try:  # collective: every rank gets a channel, or every rank raises and uses gloo
+                self.chan = HostChannel(cpu_group, words=self.NHDR)
+            except HostChannel.Unavailable as e:
+                print(f"[engine] TP step-header channel unavailable ({e}): gloo broadcast", file=sys.stderr)
+                self.chan = None
 
     def _bcast_header(self):
         import torch.distributed as dist
@@ -381,6 +385,14 @@ class Engine:
         mc, m = self.model.cfg, self.model
         if self.cfg.kv_cache_bytes:
             budget = self.cfg.kv_cache_bytes
+        elif self.device.type == "cuda" and os.environ.get("MLOP_SHARE_GPU", "0") not in ("", "0", "false"):
+            # one-GPU rehearsal of a multi-rank pod: the ranks size their pools concurrently, so
+            # a "free HBM" reading races the others' allocations; split the card's usable
+            # capacity evenly instead (every rank holds a same-size weight shard)
+            _, total = torch.cuda.mem_get_info(self.device)
+            n = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", 1)))
+            usable = total * self.cfg.gpu_memory_utilization - 4 * 2**30 - n * m.weight_bytes()
+            budget = int(max(usable / max(1, n), 2**30))
         elif self.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.device)
             reserve = total * (1 - self.cfg.gpu_memory_utilization) + 4 * 2**30

@@ -12,6 +12,8 @@ import torch
 
 from .. import ops
 
+I32_MAX = 2**31 - 1
+
 
 @dataclass
 class SamplingParams:
@@ -31,18 +33,23 @@ class SamplingParams:
         """Raise ValueError for parameters no sampler can honour (a bad request fails alone)."""
         import math
 
-        if int(self.max_tokens) < 1:
-            raise ValueError(f"max_tokens must be >= 1, got {self.max_tokens}")
+        # every integer must survive the int32 / int64 tensors the sampler and the EP request
+        # broadcast build from it: an unbounded value would raise inside the engine step and
+        # take the whole serving loop down instead of this one request
+        if not isinstance(self.max_tokens, int) or not 1 <= self.max_tokens <= I32_MAX:
+            raise ValueError(f"max_tokens must be an int in [1, {I32_MAX}], got {self.max_tokens}")
         if not math.isfinite(float(self.temperature)) or self.temperature < 0:
             raise ValueError(f"temperature must be finite and >= 0, got {self.temperature}")
-        if int(self.top_k) < 0:
-            raise ValueError(f"top_k must be >= 0, got {self.top_k}")
+        if not isinstance(self.top_k, int) or self.top_k < 0:
+            raise ValueError(f"top_k must be an int >= 0, got {self.top_k}")
+        if self.top_k > I32_MAX:
+            self.top_k = 0  # beyond any vocabulary: the same as no top-k bound (full vocabulary)
         if not (0.0 < float(self.top_p) <= 1.0):
             raise ValueError(f"top_p must be in (0, 1], got {self.top_p}")
-        if any(not isinstance(t, int) or t < 0 for t in self.stop_token_ids):
-            raise ValueError("stop_token_ids must be non-negative ints")
-        if self.seed is not None and not isinstance(self.seed, int):
-            raise ValueError("seed must be an int")
+        if any(not isinstance(t, int) or not 0 <= t <= I32_MAX for t in self.stop_token_ids):
+            raise ValueError(f"stop_token_ids must be ints in [0, {I32_MAX}]")
+        if self.seed is not None and (not isinstance(self.seed, int) or not 0 <= self.seed < 2**63):
+            raise ValueError("seed must be an int in [0, 2**63)")
         return self
 
 

@@ -52,6 +52,23 @@ def _since_process_start() -> float:
 
 
 STARTUP["server_module_imported_s"] = _since_process_start()
+if os.environ.get("MLOP_LAUNCHER_INFO"):  # this rank's pod launcher (rank_launcher.py) about itself
+    STARTUP["launcher"] = json.loads(os.environ["MLOP_LAUNCHER_INFO"])
+
+if __name__ == "__main__":
+    import sys as _sys
+
+    # one module object whether reached as __main__ or as a package import (tp_worker /
+    # ep_serving import make_app from here): one STARTUP dict, one set of globals
+    _sys.modules.setdefault(f"{__package__}.server", _sys.modules[__name__])
+
+    # a multi-rank pod's container process is a LAUNCHER: decided from argv / env alone, before
+    # torch is imported and before any HIP call, and it never comes back here (rank_launcher.py)
+    from .rank_launcher import launch_ranks as _launch_ranks, launcher_degree as _launcher_degree
+
+    _n_ranks = _launcher_degree(_sys.argv[1:])
+    if _n_ranks > 1:
+        raise SystemExit(_launch_ranks(_n_ranks, _sys.argv[1:]))
 
 
 def _warm_hip() -> None:
@@ -77,10 +94,25 @@ def _warm_hip() -> None:
         pass
 
 
-if os.environ.get("MLOP_DEVICE", "cuda") != "cpu" and os.environ.get("MLOP_HIP_WARMUP", "1") != "0":
+def start_hip_warmup() -> bool:
+    """Start ``_warm_hip`` on a daemon thread in a process that will itself run a GPU engine:
+    the predictor's ``__main__`` once it is known not to be a multi-rank launcher (above), never
+    on import as a library.  Off for CPU / sklearn predictors and with MLOP_HIP_WARMUP=0."""
+    if (os.environ.get("MLOP_DEVICE", "cuda") == "cpu" or os.environ.get("MLOP_HIP_WARMUP", "1") == "0"
+            or os.environ.get("MLOP_RUNTIME", "mlop-llm") in ("mlop-sklearn", "sklearn")):
+        return False
     import threading
 
+    from . import rank_launcher
+
+    rank_launcher.WARMUP_STARTED = True
+    STARTUP["hip_warmup_started"] = True
     threading.Thread(target=_warm_hip, name="hip-warmup", daemon=True).start()
+    return True
+
+
+if __name__ == "__main__":
+    start_hip_warmup()
 
 from .sampler import SamplingParams  # noqa: E402 (imports torch: timed below)
 
@@ -307,58 +339,6 @@ def engine_kwargs_from_env() -> dict:
     return out
 
 
-def launch_ranks(tp: int, argv: list[str]) -> int:
-    """``--tp N`` (or ``--ep N``) in a container started WITHOUT a rank launcher (what the SeldonDeployment's
-    predictor command is): this process becomes the launcher of N fresh rank processes, one
-    per visible GPU (``LOCAL_RANK`` indexes ``HIP_VISIBLE_DEVICES``), and never touches the GPU
-    itself (no HIP call before the children exist).  Rank 0 serves HTTP on ``--port``, the
-    others park in the engine's worker loop (runtime/tp_worker.py).  The first rank to exit
-    ends the group: the rest are terminated and the launcher exits with that rank's status,
-    so the kubelet (or the local Seldon stand-in) sees one pod that failed, as it would for
-    ``torchrun``.  Reference contract: one predictor per model version
-    (mlflow_operator.py:194-222) — with TP it is one pod of N ranks."""
-    import signal
-    import socket
-    import subprocess
-    import sys
-
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    procs = []
-    for r in range(tp):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(tp),
-                   LOCAL_WORLD_SIZE=str(tp), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, "-m", "mlopamd.runtime.server", *argv], env=env))
-
-    def forward(sig, _frame):
-        for p in procs:
-            if p.poll() is None:
-                p.send_signal(sig)
-
-    signal.signal(signal.SIGTERM, forward)
-    signal.signal(signal.SIGINT, forward)
-    rc = 0
-    try:
-        while True:
-            done = [p for p in procs if p.poll() is not None]
-            if done:
-                rc = next((p.returncode for p in done if p.returncode), 0)
-                break
-            time.sleep(0.2)
-    finally:
-        # rank 0 first: its shutdown sends STOP to the parked workers (engine.shutdown)
-        for p in procs:
-            if p.poll() is None:
-                p.terminate()
-                try:
-                    p.wait(timeout=10 if p is procs[0] else 3)
-                except subprocess.TimeoutExpired:
-                    p.kill()
-    return rc
-
-
 def main(argv=None):
     import sys
 
@@ -376,11 +356,18 @@ def main(argv=None):
     ap.add_argument("--ep", type=int, default=1,
                     help="expert-parallel degree with data-parallel attention (MoE; --tp 1): one "
                          "engine per GPU behind this endpoint (runtime/ep_serving.py)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="one-GPU rehearsal of a --tp / --ep pod: every rank on device 0 over a gloo "
+                         "group with the IPC all-reduce / exchange kernels forced (also MLOP_SHARE_GPU=1)")
     a = ap.parse_args(argv)
     if a.tp > 1 and a.ep > 1:
         raise SystemExit("--tp and --ep > 1 together: TP shards experts itself (EP = TP); use one")
-    if max(a.tp, a.ep) > 1 and "WORLD_SIZE" not in os.environ:
-        raise SystemExit(launch_ranks(max(a.tp, a.ep), argv))
+    from .rank_launcher import launch_ranks, launcher_degree, share_gpu_requested
+
+    a.share_gpu = share_gpu_requested(argv)
+    n = launcher_degree(argv)
+    if n > 1:  # main() called in-process (the __main__ path decided this before importing torch)
+        raise SystemExit(launch_ranks(n, argv, a.share_gpu))
 
     from aiohttp import web
 

@@ -23,10 +23,18 @@ def build_tp_engine(architecture: str, tp: int, device=None, seed: int = 0, engi
     from ..parallel.comm import init_distributed, make_parallel_state
     from .engine import Engine, EngineConfig
 
+    from .rank_launcher import share_gpu_requested
+
+    # one-GPU rehearsal of a multi-rank pod (rank_launcher.py): every rank on device 0, gloo
+    # (RCCL refuses two ranks on one device), the IPC kernels forced by the launcher's env
+    share = share_gpu_requested([])
     if device is None:
-        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0))) if torch.cuda.is_available() else "cpu"
+        local = 0 if share else int(os.environ.get("LOCAL_RANK", 0))
+        device = torch.device("cuda", local) if torch.cuda.is_available() else "cpu"
     device = torch.device(device)
-    init_distributed(backend="gloo" if device.type == "cpu" else None)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    init_distributed(backend="gloo" if (device.type == "cpu" or share) else None)
     ps = make_parallel_state(tp_size=tp, ep_size=ep or tp)
     from ..models.loader import load_pretrained, resolve_model_dir
 

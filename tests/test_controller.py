@@ -476,7 +476,10 @@ def test_placement_reads_node_capacity():
         (p,) = (await env.sd())["spec"]["predictors"]
         ann = p["annotations"]
         assert ann["mlop.amd.com/fits"] == "False" and ann["mlop.amd.com/node"] == "mi355x-0"
-        assert "needs 8 GPUs" in ann["mlop.amd.com/reason"] and "4 of 8" in ann["mlop.amd.com/reason"]
+        # the reason quotes momentary free counts: CR status, never the SD spec
+        assert "mlop.amd.com/reason" not in ann
+        why = (await env.status())["placement"]["v1"]
+        assert "needs 8 GPUs" in why and "4 of 8" in why
         await env.stop()
 
         env2 = Env()
@@ -521,6 +524,41 @@ def test_placement_charges_gpus_per_node():
         (p,) = (await env.sd())["spec"]["predictors"]
         ann = p["annotations"]
         assert ann["mlop.amd.com/fits"] == "True" and ann["mlop.amd.com/node"] == "node-b", ann
+        await env.stop()
+    run(go())
+
+
+def test_own_predictor_pods_do_not_move_the_placement():
+    """after the first deploy, the model's OWN predictor pods (Seldon labels
+    them ``seldon-deployment-id: <SD>``) are bound to the node.  A later reconcile must not
+    charge them against the model: the SD is not replaced, the placement stays, and a canary's
+    new version is planned with the old version's GPUs subtracted once."""
+    async def go():
+        env = Env()
+        await env.kube.create("", "v1", None, "nodes", _gpu_node("mi355x-0", 8))
+        v1 = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v1)
+        await env.start()
+        await env.create_cr(tensorParallel=4, maxModelLen=8192, maxNumSeqs=64)
+        assert await env.run_until(lambda: _ready(env))
+        sd = await env.sd()
+        (p,) = sd["spec"]["predictors"]
+        assert p["annotations"]["mlop.amd.com/fits"] == "True"
+        rv = sd["metadata"]["resourceVersion"]
+        # the predictor's pod is now scheduled on the node and holds its 4 GPUs; another team's
+        # pod holds 2 more
+        own = _gpu_pod("m-v1-0", "mi355x-0", 4)
+        own["metadata"].update(namespace=NS, labels={"seldon-deployment-id": "m"})
+        await env.kube.create("", "v1", NS, "pods", own)
+        await env.kube.create("", "v1", "team", "pods", _gpu_pod("x", "mi355x-0", 2))
+        cap = await env.rec.node_capacity(exclude=(NS, "m"))
+        assert cap["free_gpus"] == 6, cap  # own pod not charged
+        assert (await env.rec.node_capacity())["free_gpus"] == 2
+        for _ in range(3):  # several level-triggered passes
+            env.rec.kick(NS, "m")
+            await env.clock.sleep(61.0)
+        sd2 = await env.sd()
+        assert sd2["metadata"]["resourceVersion"] == rv and sd2["spec"] == sd["spec"]
         await env.stop()
     run(go())
 

@@ -298,3 +298,47 @@ def test_host_channel_broadcast(fn, world):
     res = run_ranks(fn, world)
     assert all(r["ok"] for r in res) and all(r["n"] == 5000 for r in res[1:])
     assert not any(r["leftover"] for r in res)
+
+
+def _chan_fallback(rank, world, fail_rank):
+    """a HostChannel that one rank cannot create / map raises ``Unavailable`` on
+    EVERY rank (no rank left waiting in a broadcast or barrier), nothing is left in /dev/shm,
+    and the TP engine's StepSync falls back to the gloo header: TP still == TP=1."""
+    import glob
+
+    import torch.distributed as dist
+
+    from mlopamd.parallel.comm import HostChannel
+
+    def broken(self, name):
+        raise OSError("injected: no such shm namespace")
+
+    if rank == fail_rank:
+        HostChannel._open = broken
+        HostChannel._create = broken
+    cpu = dist.new_group(list(range(world)), backend="gloo")
+    try:
+        HostChannel(cpu, words=4)
+        raised = False
+    except HostChannel.Unavailable:
+        raised = True
+    dist.barrier(group=cpu)
+    leftover = glob.glob("/dev/shm/mlop-chan-*")
+    res = _tp_engine("tiny-llama")
+    res.update(raised=raised, leftover=leftover)
+    return res
+
+
+def chan_fail_worker(rank, world):
+    return _chan_fallback(rank, world, 1)
+
+
+def chan_fail_leader(rank, world):
+    return _chan_fallback(rank, world, 0)
+
+
+@pytest.mark.parametrize("fn", ["chan_fail_worker", "chan_fail_leader"])
+def test_host_channel_failure_falls_back_together(fn):
+    r0, r1 = run_ranks(fn, 2)
+    assert r0["raised"] and r1["raised"] and not r0["leftover"] and not r1["leftover"]
+    assert r0["tp"] == r0["ref"] and r1["worker_steps"] > 0

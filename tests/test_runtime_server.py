@@ -99,6 +99,27 @@ def test_llm_generate_infer_stream(llm_backend):
     asyncio.run(go())
 
 
+def test_out_of_range_sampling_params_fail_alone(llm_backend):
+    """A request whose integers cannot fit the sampler's int32 / int64 tensors (top_k 2**40,
+    seed 2**64, huge stop ids / max_tokens) gets a 400 and leaves the engine loop serving."""
+    async def go():
+        async with _client(make_app(llm_backend, llm_backend.metrics)) as c:
+            bad = [{"temperature": 1.0, "seed": 2**64}, {"max_tokens": 2**40}, {"stop_token_ids": [2**40]},
+                   {"seed": -1}, {"top_k": -3}]
+            for params in bad:
+                r = await c.post("/v2/models/tiny/generate", json={"input_ids": [5, 6, 7], "parameters": params})
+                assert r.status == 400, (params, r.status, await r.text())
+            # top_k beyond int32 means "no bound": served as full-vocabulary sampling
+            r = await c.post("/v2/models/tiny/generate", json={"input_ids": [5, 6, 7], "parameters": {
+                "temperature": 1.0, "top_k": 2**40, "seed": 3, "max_tokens": 3, "ignore_eos": True}})
+            assert r.status == 200 and len((await r.json())["output_ids"]) == 3
+            r = await c.post("/v2/models/tiny/generate", json={"input_ids": [5, 6, 7], "parameters": {
+                "max_tokens": 4, "ignore_eos": True}})
+            assert r.status == 200 and len((await r.json())["output_ids"]) == 4
+    asyncio.run(go())
+    assert llm_backend.failure is None if hasattr(llm_backend, "failure") else True
+
+
 def test_torch_profile_window(tmp_path):
     """MLOP_PROFILE_STEPS-style window: torch.profiler around engine steps a..b, Chrome trace written."""
     import torch
@@ -255,7 +276,8 @@ def test_hip_warmup_loads_torchs_own_runtime():
     import subprocess
     import sys
 
-    code = ("import time, mlopamd.runtime.server as s; time.sleep(0.5); from mlopamd import ops; ops.load(); "
+    code = ("import time, mlopamd.runtime.server as s; s.start_hip_warmup(); time.sleep(0.5); "
+            "from mlopamd import ops; ops.load(); "
             "print(sorted({l.split()[-1] for l in open('/proc/self/maps') if 'amdhip' in l}))")
     env = {k: v for k, v in os.environ.items() if k not in ("MLOP_DEVICE", "MLOP_HIP_WARMUP")}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
