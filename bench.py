@@ -92,7 +92,13 @@ def parse(argv=None):
                          "(a fresh predictor process: CR->ready includes its start-up) + V2 HTTP + Router "
                          "(runtime/http_bench.py); the value is the served rate over the predictor's own "
                          "engine steps")
-    ap.add_argument("--cr-ready-samples", type=int, default=1,
+    ap.add_argument("--http-check", type=int, default=-1,
+                    help="also measure the served rate over HTTP at this config (a fresh predictor process "
+                         "through operator + ProcessLauncher + V2 clients, runtime/http_bench.py) BEFORE the "
+                         "engine-direct run, and report it as served_tokens_per_sec_http; its window is "
+                         "max(--steps, 40) engine steps.  -1 (default): on for the 1-GPU operator bench, "
+                         "off otherwise; 0 / 1 force it")
+    ap.add_argument("--cr-ready-samples", type=int, default=3,
                     help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
                          "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
                          "their median is p50_cr_ready_s.  0: report the in-process deploy time instead")
@@ -108,9 +114,17 @@ def _gpu_count() -> int:
     return visible_gpu_count()
 
 
-def _process_ready(a, device_index: int | None) -> dict:
-    """p50 CR->ready over ``--cr-ready-samples`` fresh predictor processes (runtime/http_bench.py),
-    on one GPU, before this process touches HIP.  CPU: a float32 predictor without graphs."""
+def _http_check_on(a, world: int) -> bool:
+    if a.http_check >= 0:
+        return bool(a.http_check)
+    return world == 1 and not a.no_operator and a.tp == 1 and a.ep == 1
+
+
+def _process_ready(a, device_index: int | None, http: bool = False) -> dict:
+    """Fresh predictor PROCESSES on one GPU, before this process touches HIP: p50 CR->ready over
+    ``--cr-ready-samples`` of them, and with ``http`` the served rate of one more at this
+    config under ``--batch`` closed-loop V2 HTTP clients (runtime/http_bench.py).  CPU: a
+    float32 predictor without graphs (HTTP only when forced with ``--http-check 1``)."""
     import asyncio
 
     from mlopamd.runtime import http_bench
@@ -124,6 +138,14 @@ def _process_ready(a, device_index: int | None) -> dict:
     r = asyncio.run(http_bench.cr_ready_process(a.model, a.batch, env, samples=a.cr_ready_samples,
                                                 gpus=[device_index] if device_index is not None else 8))
     r["probe_wall_s"] = round(time.perf_counter() - t0, 2)
+    if http and (device_index is not None or a.http_check == 1):
+        t0 = time.perf_counter()
+        _progress(0, f"HTTP served-rate run: {a.batch} V2 clients against a fresh predictor process")
+        h = http_bench.main(a, steps=max(a.steps, 40), warmup=a.warmup,
+                            gpus=[device_index] if device_index is not None else 8,
+                            extra_env=env if device_index is None else None)
+        h["wall_s"] = round(time.perf_counter() - t0, 2)
+        r["http"] = h
     return r
 
 
@@ -142,7 +164,8 @@ def launch(a, argv) -> int:
         raise SystemExit(f"--gpus {n}: only {ngpu} GPUs visible")
     extra = {}
     if a.cr_ready_samples > 0 and not a.no_operator:
-        extra["MLOP_BENCH_PROCESS_READY"] = json.dumps(_process_ready(a, 0 if ngpu else None))
+        extra["MLOP_BENCH_PROCESS_READY"] = json.dumps(_process_ready(a, 0 if ngpu else None,
+                                                                      http=_http_check_on(a, n)))
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -200,7 +223,7 @@ def main(argv=None):
         if os.environ.get("MLOP_BENCH_PROCESS_READY"):  # measured by our launcher parent
             proc_ready = json.loads(os.environ["MLOP_BENCH_PROCESS_READY"])
         else:  # before this process makes its first HIP call (the probe's predictor uses this GPU)
-            proc_ready = _process_ready(a, local_rank if _gpu_count() else None)
+            proc_ready = _process_ready(a, local_rank if _gpu_count() else None, http=_http_check_on(a, world))
     if world > 1:
         init_distributed(backend="gloo" if a.share_gpu else None)
     dev = torch.device("cuda", 0 if a.share_gpu else local_rank) if torch.cuda.is_available() else torch.device("cpu")
@@ -402,6 +425,9 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
             "cr_ready_path": "fresh predictor process" if proc_ready else "in-process",
             "p50_cr_ready_in_process_s": round(p50_ready, 3),
             "cr_ready_process": proc_ready,
+            # the same config served over V2 HTTP by a fresh predictor process (operator ->
+            # ProcessLauncher -> Router -> aiohttp clients), measured before the engine-direct run
+            "served_tokens_per_sec_http": ((proc_ready or {}).get("http") or {}).get("served_tokens_per_sec_http"),
             "served_tokens_per_sec_per_gpu": round(value / world, 2),
             "per_rank_tokens_per_sec": [round(float(g[0]) / float(g[1]), 2) if float(g[1]) > 0 else 0.0
                                         for g in gathered],

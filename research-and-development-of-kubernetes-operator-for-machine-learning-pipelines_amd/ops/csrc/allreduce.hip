@@ -26,20 +26,30 @@
 //   * every poll is bounded: on timeout the block sets an error word (read by
 //     car_error) and finishes — a wedged peer never hangs the GPU.
 //
-// Memory: the IPC-exported buffer (flags AND data) is allocated UNCACHED
-// (hipExtMallocWithFlags(hipDeviceMallocUncached)).  Its lines are written by
-// REMOTE agents (peer flag stores and, under xGMI, peer reads of the data): in
-// coarse-grained hipMalloc memory this device's L2 may keep a stale copy of a
-// flag line a peer rewrote (the L2 is not coherent with other agents' stores),
-// and a poll served from that copy never sees the epoch.  Uncached memory keeps
-// every access at the memory side, as RCCL does for its flags; the messages are
-// decode-sized (<= 4 MiB), so bypassing L2 costs nothing measurable next to the
-// hop.  The release / acquire fences stay: they order this wave's own stores
-// and the flag.  If the driver refuses to IPC-export uncached memory the buffer
-// falls back to hipMalloc (car_mem_mode() reports which one is in use).
+// Memory (two layouts, car_create's `split`):
+//   * split = 0: ONE IPC-exported buffer, flags AND data, allocated UNCACHED
+//     (hipExtMallocWithFlags(hipDeviceMallocUncached));
+//   * split = 1: the flag banks alone in an uncached buffer, the data parities in a separate
+//     ordinary (cached, coarse-grained) hipMalloc buffer, each IPC-exported.
+// The flag lines are written by REMOTE agents: in coarse-grained memory this device's L2 may
+// keep a stale copy of a flag line a peer rewrote, and a poll served from it would never see
+// the epoch -- so flags are uncached in both layouts, as RCCL keeps its flags.  Data does not
+// need that: every data line is published before a system-scope release (L2 write-back) that
+// precedes its flag, and read after a system-scope acquire (L2 invalidate of non-local lines)
+// that follows the flag poll, so a cached data buffer sees the same values.  What the layouts
+// trade is bandwidth: uncached data keeps every publish / peer read at the memory side (no L2
+// write combining, no L2 hits on the local copy), which is free for decode-sized messages but
+// could be paid per byte on the two-shot kernel's 1-64 MiB prefill chunks.  Measured on one
+// GPU (scripts/bench_car.py, profiles/r05_car_memory.md): the layouts are within -5 / +9 % at
+// 1-64 MiB, and the uncached one is 11-23 % faster at 256 KiB-4 MiB one-shot messages, so
+// split = 0 is the default (parallel/custom_ar.py SPLIT_DATA).  What bounds large messages is
+// the fixed 64-workgroup grid (a 64 MiB two-shot call: 276 us vs 38 us for a plain copy on one
+// GPU), which on a node keeps pace with the ~400 GB/s of xGMI read bandwidth per GPU.  If the driver refuses to IPC-export uncached memory the flags fall
+// back to hipMalloc (car_mem_mode() reports which layout is in use).
 #include "common.h"
 #include "launch.h"
 
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -56,14 +66,17 @@ constexpr size_t kFlagsBytes = 2 * kFlagBank;  // bank 0: one-shot + two-shot ph
 constexpr long kMaxSpins = 1L << 26;
 
 struct Peers {
-  uint8_t* base[kMaxRanks];
+  uint8_t* base[kMaxRanks];  // flag banks (and, split = 0, the data parities after them)
+  uint8_t* data[kMaxRanks];  // data parity 0 | parity 1 of each rank
 };
 
 struct CarState {
   int rank = 0, world = 1, device = 0;
-  int uncached = 0;  // 1: the IPC buffer is hipDeviceMallocUncached memory
+  int uncached = 0;  // 1: the flag buffer is hipDeviceMallocUncached memory
+  int split = 0;     // 1: data in its own cached buffer (dbuf), else after the flags in buf
   size_t max_bytes = 0;  // per parity
   uint8_t* buf = nullptr;
+  uint8_t* dbuf = nullptr;
   uint32_t* epochs = nullptr;
   int* err = nullptr;       // device alias of err_host
   int* err_host = nullptr;
@@ -102,13 +115,13 @@ __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restr
   if (tid == 0) s_e = epochs[b] + 1;
   __syncthreads();
   const uint32_t e = s_e;
-  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const size_t doff = (size_t)(e & 1) * max_bytes;
   const long per = (n16 + kBlocks - 1) / kBlocks;
   const long lo = min(n16, (long)b * per), hi = min(n16, lo + per);
   const uint4* src = reinterpret_cast<const uint4*>(in);
 
   // 1. publish my slice
-  uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+  uint4* mine = reinterpret_cast<uint4*>(peers.data[rank] + doff);
   for (long i = lo + tid; i < hi; i += kThreads) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -146,7 +159,7 @@ __global__ void __launch_bounds__(kThreads) car_oneshot_kernel(uint16_t* __restr
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int p = 0; p < NR; ++p) {
-      const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.base[p] + doff)[i];
+      const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.data[p] + doff)[i];
       add_bf16x8(acc, v);
     }
     if (add_out) {
@@ -192,7 +205,7 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
   __syncthreads();
   const uint32_t e = s_e;
   const size_t half = max_bytes / 2;  // input copy | reduced, per parity
-  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const size_t doff = (size_t)(e & 1) * max_bytes;
   const uint4* src = reinterpret_cast<const uint4*>(in);
   uint4* o = reinterpret_cast<uint4*>(out);
   // slices: rank p owns [p * sl, min(n16, (p + 1) * sl)); block b its piece of every slice
@@ -229,7 +242,7 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
     }
   };
   // 1a. publish piece b of every slice of the input
-  uint4* mine_in = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+  uint4* mine_in = reinterpret_cast<uint4*>(peers.data[rank] + doff);
 #pragma unroll
   for (int p = 0; p < NR; ++p) {
     long lo, hi;
@@ -247,12 +260,12 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
   {
     long lo, hi;
     piece(rank, lo, hi);
-    uint4* red = reinterpret_cast<uint4*>(peers.base[rank] + doff + half);
+    uint4* red = reinterpret_cast<uint4*>(peers.data[rank] + doff + half);
     for (long i = lo + tid; i < hi; i += kThreads) {
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int p = 0; p < NR; ++p) {
-        const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.base[p] + doff)[i];
+        const uint4 v = p == rank ? src[i] : reinterpret_cast<const uint4*>(peers.data[p] + doff)[i];
         add_bf16x8(acc, v);
       }
       uint4 r;
@@ -277,7 +290,7 @@ __global__ void __launch_bounds__(kThreads) car_twoshot_kernel(uint16_t* __restr
     if (p == rank) continue;
     long lo, hi;
     piece(p, lo, hi);
-    const uint4* red = reinterpret_cast<const uint4*>(peers.base[p] + doff + half);
+    const uint4* red = reinterpret_cast<const uint4*>(peers.data[p] + doff + half);
     for (long i = lo + tid; i < hi; i += kThreads) o[i] = red[i];
   }
   if (tid == 0) epochs[b] = e;
@@ -298,7 +311,7 @@ __global__ void __launch_bounds__(kThreads) car_bcast_kernel(uint4* __restrict__
   if (tid == 0) s_e = epochs[b] + 1;
   __syncthreads();
   const uint32_t e = s_e;
-  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const size_t doff = (size_t)(e & 1) * max_bytes;
   const long per = (n16 + kBlocks - 1) / kBlocks;
   const long lo = min(n16, (long)b * per), hi = min(n16, lo + per);
   auto raise_flag = [&]() {
@@ -326,7 +339,7 @@ __global__ void __launch_bounds__(kThreads) car_bcast_kernel(uint4* __restrict__
     }
   };
   if (rank == root) {
-    uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + doff);
+    uint4* mine = reinterpret_cast<uint4*>(peers.data[rank] + doff);
     for (long i = lo + tid; i < hi; i += kThreads) {
       const uint4 v = in[i];
       mine[i] = v;
@@ -340,7 +353,7 @@ __global__ void __launch_bounds__(kThreads) car_bcast_kernel(uint4* __restrict__
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    const uint4* src = reinterpret_cast<const uint4*>(peers.base[root] + doff);
+    const uint4* src = reinterpret_cast<const uint4*>(peers.data[root] + doff);
     for (long i = lo + tid; i < hi; i += kThreads) out[i] = src[i];
     raise_flag();
   }
@@ -363,10 +376,10 @@ __global__ void __launch_bounds__(kThreads) car_allgather_kernel(uint32_t* __res
   if (tid == 0) s_e = epochs[b] + 1;
   __syncthreads();
   const uint32_t e = s_e;
-  const size_t doff = kFlagsBytes + (size_t)(e & 1) * max_bytes;
+  const size_t doff = (size_t)(e & 1) * max_bytes;
   const long per = (n4 + kBlocks - 1) / kBlocks;
   const long lo = min(n4, (long)b * per), hi = min(n4, lo + per);
-  uint32_t* mine = reinterpret_cast<uint32_t*>(peers.base[rank] + doff);
+  uint32_t* mine = reinterpret_cast<uint32_t*>(peers.data[rank] + doff);
   for (long i = lo + tid; i < hi; i += kThreads) {
     const uint32_t v = in[i];
     mine[i] = v;
@@ -402,7 +415,7 @@ __global__ void __launch_bounds__(kThreads) car_allgather_kernel(uint32_t* __res
 #pragma unroll
   for (int p = 0; p < NR; ++p) {
     if (p == rank) continue;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(peers.base[p] + doff);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(peers.data[p] + doff);
     for (long i = lo + tid; i < hi; i += kThreads) out[(long)p * n4 + i] = src[i];
   }
   if (tid == 0) epochs[b] = e;
@@ -415,14 +428,15 @@ CarState* get(long h) {
 
 }  // namespace
 
-long car_create(int rank, int world, long max_bytes, int device) {
+long car_create(int rank, int world, long max_bytes, int device, int split) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world)
     throw std::runtime_error("custom all-reduce: bad rank/world");
   if (max_bytes <= 0 || max_bytes % 16) throw std::runtime_error("custom all-reduce: max_bytes % 16");
   auto* s = new CarState;
-  s->rank = rank, s->world = world, s->device = device, s->max_bytes = (size_t)max_bytes;
+  s->rank = rank, s->world = world, s->device = device, s->max_bytes = (size_t)max_bytes, s->split = split ? 1 : 0;
   CAR_CHECK(hipSetDevice(device));
-  const size_t bytes = kFlagsBytes + 2 * (size_t)max_bytes;
+  const size_t data_bytes = 2 * (size_t)max_bytes;
+  const size_t bytes = kFlagsBytes + (s->split ? 0 : data_bytes);
   if (hipExtMallocWithFlags((void**)&s->buf, bytes, hipDeviceMallocUncached) == hipSuccess) {
     hipIpcMemHandle_t probe;
     if (hipIpcGetMemHandle(&probe, s->buf) == hipSuccess) {
@@ -435,6 +449,7 @@ long car_create(int rank, int world, long max_bytes, int device) {
   (void)hipGetLastError();  // clear a refused uncached allocation / export
   if (!s->buf) CAR_CHECK(hipMalloc(&s->buf, bytes));
   CAR_CHECK(hipMemset(s->buf, 0, kFlagsBytes));
+  if (s->split) CAR_CHECK(hipMalloc(&s->dbuf, data_bytes));
   CAR_CHECK(hipMalloc(&s->epochs, kBlocks * sizeof(uint32_t)));
   CAR_CHECK(hipMemset(s->epochs, 0, kBlocks * sizeof(uint32_t)));
   // error word in host-mapped (coherent) memory: the host polls it every engine step with a
@@ -444,14 +459,21 @@ long car_create(int rank, int world, long max_bytes, int device) {
   CAR_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&s->err), s->err_host, 0));
   CAR_CHECK(hipDeviceSynchronize());
   s->peers.base[rank] = s->buf;
+  s->peers.data[rank] = s->split ? s->dbuf : s->buf + kFlagsBytes;
   return reinterpret_cast<long>(s);
 }
 
-void car_ipc_handle(long h, void* out64) {
+// two 64-B handles per rank: the flag buffer, then the data buffer (zeros when not split)
+void car_ipc_handle(long h, void* out128) {
   CarState* s = get(h);
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
   CAR_CHECK(hipSetDevice(s->device));
-  CAR_CHECK(hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(out64), s->buf));
+  auto* hs = reinterpret_cast<hipIpcMemHandle_t*>(out128);
+  CAR_CHECK(hipIpcGetMemHandle(&hs[0], s->buf));
+  if (s->split)
+    CAR_CHECK(hipIpcGetMemHandle(&hs[1], s->dbuf));
+  else
+    std::memset(&hs[1], 0, sizeof(hipIpcMemHandle_t));
 }
 
 void car_open(long h, const void* handles) {
@@ -461,14 +483,22 @@ void car_open(long h, const void* handles) {
   for (int p = 0; p < s->world; ++p) {
     if (p == s->rank || s->peers.base[p]) continue;
     void* ptr = nullptr;
-    CAR_CHECK(hipIpcOpenMemHandle(&ptr, hs[p], hipIpcMemLazyEnablePeerAccess));
+    CAR_CHECK(hipIpcOpenMemHandle(&ptr, hs[2 * p], hipIpcMemLazyEnablePeerAccess));
     s->peers.base[p] = reinterpret_cast<uint8_t*>(ptr);
+    if (s->split) {
+      void* dptr = nullptr;
+      CAR_CHECK(hipIpcOpenMemHandle(&dptr, hs[2 * p + 1], hipIpcMemLazyEnablePeerAccess));
+      s->peers.data[p] = reinterpret_cast<uint8_t*>(dptr);
+    } else {
+      s->peers.data[p] = s->peers.base[p] + kFlagsBytes;
+    }
   }
 }
 
 long car_max_bytes(long h) { return (long)get(h)->max_bytes; }
 
-int car_mem_mode(long h) { return get(h)->uncached; }
+// bit 0: flags uncached; bit 1: data in its own cached buffer
+int car_mem_mode(long h) { return get(h)->uncached | (get(h)->split << 1); }
 
 void car_all_reduce(long h, void* out, const void* in, long numel, hipStream_t st, bool two_shot, bool add_out) {
   CarState* s = get(h);
@@ -555,8 +585,12 @@ void car_destroy(long h) {
   hipSetDevice(s->device);
   hipDeviceSynchronize();
   for (int p = 0; p < s->world; ++p)
-    if (p != s->rank && s->peers.base[p]) hipIpcCloseMemHandle(s->peers.base[p]);
+    if (p != s->rank && s->peers.base[p]) {
+      hipIpcCloseMemHandle(s->peers.base[p]);
+      if (s->split && s->peers.data[p]) hipIpcCloseMemHandle(s->peers.data[p]);
+    }
   hipFree(s->buf);
+  if (s->dbuf) hipFree(s->dbuf);
   hipFree(s->epochs);
   hipHostFree(s->err_host);
   delete s;

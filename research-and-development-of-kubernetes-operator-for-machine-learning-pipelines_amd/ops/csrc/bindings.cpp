@@ -629,17 +629,17 @@ void sample(Tensor out, Tensor logits, Tensor temps, Tensor top_ks, Tensor top_p
 
 
 // ---- K15 custom all-reduce: host-side state, int handles -------------------
-int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes, int64_t device) {
-  return mlop::car_create((int)rank, (int)world, (long)max_bytes, (int)device);
+int64_t car_create(int64_t rank, int64_t world, int64_t max_bytes, int64_t device, bool split) {
+  return mlop::car_create((int)rank, (int)world, (long)max_bytes, (int)device, split ? 1 : 0);
 }
 Tensor car_ipc_handle(int64_t h) {
-  Tensor t = at::empty({64}, at::TensorOptions().dtype(at::kByte));
+  Tensor t = at::empty({128}, at::TensorOptions().dtype(at::kByte));
   mlop::car_ipc_handle((long)h, t.data_ptr());
   return t;
 }
 void car_open(int64_t h, Tensor handles) {
   TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
-              handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
+              handles.dim() == 2 && handles.size(1) == 128, "handles: CPU uint8 [world, 128]");
   mlop::car_open((long)h, handles.data_ptr());
 }
 void car_all_reduce(int64_t h, Tensor out, Tensor inp, bool two_shot) {
@@ -710,7 +710,7 @@ Tensor ep_ipc_handle(int64_t h) {
 }
 void ep_open(int64_t h, Tensor handles) {
   TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
-              handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
+              handles.dim() == 2 && handles.size(1) == 128, "handles: CPU uint8 [world, 128]");
   mlop::ep_open((long)h, handles.data_ptr());
 }
 // xp [rows, H] bf16 <- this rank's received rows grouped by local expert; offsets int32 [n_local + 1]
@@ -748,7 +748,7 @@ std::string src_hash() { return std::string(mlop_src_hash()); }
 
 TORCH_LIBRARY(mlop, m) {
   m.def("src_hash() -> str", &src_hash);
-  m.def("car_create(int rank, int world, int max_bytes, int device) -> int", &car_create);
+  m.def("car_create(int rank, int world, int max_bytes, int device, bool split=False) -> int", &car_create);
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);
   m.def("car_all_reduce(int h, Tensor(a!) out, Tensor inp, bool two_shot=False) -> ()");

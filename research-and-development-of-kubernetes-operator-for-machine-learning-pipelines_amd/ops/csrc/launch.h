@@ -167,8 +167,8 @@ long vmm_chunks_ready(void* base);
 int vmm_error(void* base);
 
 // K15 custom one-shot all-reduce (allreduce.hip); handles are opaque state pointers
-long car_create(int rank, int world, long max_bytes, int device);
-void car_ipc_handle(long h, void* out64);
+long car_create(int rank, int world, long max_bytes, int device, int split);
+void car_ipc_handle(long h, void* out128);
 void car_open(long h, const void* handles);
 long car_max_bytes(long h);
 // add_out: out = bf16(out + bf16(sum)) (the residual stream; one-shot only, out != in)

@@ -28,22 +28,31 @@ DEFAULT_MAX_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_MAX_BYTES", 64 << 20))
 TWO_SHOT_MIN_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_TWO_SHOT_MIN", 512 << 10))
 
 
+# data parities in their own cached buffer, flags alone uncached (allreduce.hip "Memory").  Off
+# by default: one uncached buffer measured the same at the two-shot sizes (1-64 MiB, -5..+9 %)
+# and 11-23 % faster at 256 KiB-4 MiB one-shot messages (scripts/bench_car.py,
+# profiles/r05_car_memory.md)
+SPLIT_DATA = False
+
+
 class CustomAllReduce:
-    def __init__(self, rank: int, world: int, device, group=None, max_bytes: int = DEFAULT_MAX_BYTES):
+    def __init__(self, rank: int, world: int, device, group=None, max_bytes: int = DEFAULT_MAX_BYTES,
+                 split_data: bool | None = None):
         from .. import ops
 
         ops.load()
         self.rank, self.world, self.group = rank, world, group
         self.device = torch.device(device)
         self.max_bytes = int(max_bytes)
-        self.h = torch.ops.mlop.car_create(rank, world, self.max_bytes, self.device.index or 0)
+        self.split_data = SPLIT_DATA if split_data is None else bool(split_data)
+        self.h = torch.ops.mlop.car_create(rank, world, self.max_bytes, self.device.index or 0, self.split_data)
         mine = torch.ops.mlop.car_ipc_handle(self.h)
         if world > 1:
             allh = [None] * world
             dist.all_gather_object(allh, bytes(mine.numpy().tobytes()), group=group)
         else:
             allh = [bytes(mine.numpy().tobytes())]
-        table = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(world, 64).clone()
+        table = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(world, 128).clone()
         torch.ops.mlop.car_open(self.h, table)
         if world > 1:
             dist.barrier(group=group)
@@ -99,8 +108,13 @@ class CustomAllReduce:
 
     @property
     def uncached(self) -> bool:
-        """True when the IPC buffer (flags + data) is uncached device memory (allreduce.hip)."""
-        return bool(torch.ops.mlop.car_mem_mode(self.h))
+        """True when the flag buffer is uncached device memory (allreduce.hip)."""
+        return bool(torch.ops.mlop.car_mem_mode(self.h) & 1)
+
+    @property
+    def data_cached(self) -> bool:
+        """True when the data parities live in their own ordinary (cached) buffer."""
+        return bool(torch.ops.mlop.car_mem_mode(self.h) & 2)
 
     def error(self) -> int:
         """Non-zero if any call timed out waiting for a peer (the result is then invalid)."""

@@ -124,13 +124,13 @@ async def cr_ready_process(model: str = "llama3-8b", batch: int = 2048, engine_e
 
 async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256, output_len: int = 256,
               steps: int = 20, warmup: int = 5, engine_env: dict | None = None, ready_timeout_s: float = 900.0,
-              ramp_timeout_s: float = 600.0) -> dict:
+              ramp_timeout_s: float = 600.0, gpus=None) -> dict:
     import aiohttp
 
     from ..models.config import get_config
 
     ns, name = _NS, _NAME
-    kube, op, ctl, router = await _start_stack(model, batch, engine_env, ready_timeout_s)
+    kube, op, ctl, router = await _start_stack(model, batch, engine_env, ready_timeout_s, gpus)
     out: dict = {"mode": "http", "path": "operator + ProcessLauncher + V2 HTTP + Router"}
     try:
         r = await _create_and_wait_ready(kube, ctl, batch, ready_timeout_s)
@@ -207,9 +207,11 @@ async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256
     return out
 
 
-def main(a) -> dict:
-    return asyncio.run(run(a.model, a.batch, a.prompt_len, a.output_len, a.steps, a.warmup,
-                           engine_env={"MLOP_ENGINE_MAX_NUM_BATCHED_TOKENS": str(a.max_batched_tokens),
-                                       "MLOP_ENGINE_MAX_MODEL_LEN": str(a.max_model_len),
-                                       "MLOP_ENGINE_PREFILL_MIN_BATCH": str(a.prefill_min_batch),
-                                       "MLOP_ENGINE_MAX_DECODE_GAP": str(a.max_decode_gap)}))
+def main(a, steps: int | None = None, warmup: int | None = None, gpus=None, extra_env: dict | None = None) -> dict:
+    env = {"MLOP_ENGINE_MAX_NUM_BATCHED_TOKENS": str(a.max_batched_tokens),
+           "MLOP_ENGINE_MAX_MODEL_LEN": str(a.max_model_len),
+           "MLOP_ENGINE_PREFILL_MIN_BATCH": str(a.prefill_min_batch),
+           "MLOP_ENGINE_MAX_DECODE_GAP": str(a.max_decode_gap)}
+    env.update(extra_env or {})
+    return asyncio.run(run(a.model, a.batch, a.prompt_len, a.output_len, a.steps if steps is None else steps,
+                           a.warmup if warmup is None else warmup, gpus=gpus, engine_env=env))

@@ -39,7 +39,22 @@ def test_bench_single_process_json():
     # CR -> ready measured with the predictor as a fresh OS process
     assert d["cr_ready_path"] == "fresh predictor process"
     assert d["p50_cr_ready_s"] == d["cr_ready_process"]["p50_cr_ready_process_s"]
-    assert d["p50_cr_ready_s"] >= d["cr_ready_process"]["predictor_process_ready_s"] > 0
+    assert max(d["cr_ready_process"]["cr_ready_process_samples_s"]) >= \
+        d["cr_ready_process"]["predictor_process_ready_s"] > 0
+    # a median of three fresh processes
+    samples = d["cr_ready_process"]["cr_ready_process_samples_s"]
+    assert len(samples) == 3 and d["p50_cr_ready_s"] == sorted(samples)[1]
+    assert "served_tokens_per_sec_http" in d  # None on CPU unless forced (below)
+
+
+def test_bench_reports_http_served_rate():
+    """``--http-check 1``: the default line also carries the HTTP-served rate of the same config
+    (fresh predictor process, operator + Router + V2 clients) measured before the engine run."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--http-check", "1", "--cr-ready-samples", "1",
+              *ARGS])
+    h = d["cr_ready_process"]["http"]
+    assert d["served_tokens_per_sec_http"] == h["served_tokens_per_sec_http"] > 0
+    assert h["http_errors"] == 0 and h["http_window_steps"] >= 40 and d["value"] > 0
 
 
 def test_bench_two_ranks_gloo():

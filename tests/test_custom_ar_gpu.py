@@ -40,7 +40,7 @@ def _oracle(xs):
     return acc.to(torch.bfloat16)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, split):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -48,7 +48,7 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     from mlopamd.parallel.custom_ar import CustomAllReduce
 
-    car = CustomAllReduce(rank, world, torch.device("cuda", 0), group=None, max_bytes=8 << 20)
+    car = CustomAllReduce(rank, world, torch.device("cuda", 0), group=None, max_bytes=8 << 20, split_data=split)
     res = {"eager": [], "inplace": [], "graph": [], "two_shot": []}
     try:
         for it, n in enumerate(SIZES):
@@ -179,6 +179,7 @@ def _worker(rank, world, port, out_dir):
                                 torch.equal(resid.cpu(), (r0.float() + _oracle(xs0).float()).to(torch.bfloat16)))
         res["error"] = car.error()
         res["uncached"] = car.uncached
+        res["data_cached"] = car.data_cached
     finally:
         torch.cuda.synchronize()
         dist.barrier()
@@ -187,18 +188,21 @@ def _worker(rank, world, port, out_dir):
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_custom_all_reduce_two_processes_one_gpu(world):
-    """world = 8: the NR = 8 kernels (Llama-3-70B TP = 8) with 8 processes sharing the GPU."""
+@pytest.mark.parametrize("world,split", [(2, True), (2, False), (8, True), (8, False)])
+def test_custom_all_reduce_two_processes_one_gpu(world, split):
+    """world = 8: the NR = 8 kernels (Llama-3-70B TP = 8) with 8 processes sharing the GPU.
+    ``split``: the data parities in their own cached buffer (flags alone uncached) vs one
+    uncached buffer for both -- every kernel bit-exact either way."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     d = tempfile.mkdtemp()
-    mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), d, split), nprocs=world, join=True, start_method="spawn")
     for r in range(world):
         res = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
         assert res["error"] == 0, f"rank {r}: a flag wait timed out"
         # the flags a peer rewrites live in uncached memory (no stale L2 copy can be polled)
-        assert res["uncached"], f"rank {r}: IPC buffer fell back to cached hipMalloc memory"
+        assert res["uncached"], f"rank {r}: IPC flag buffer fell back to cached hipMalloc memory"
+        assert res["data_cached"] == split
         assert all(res["eager"]), (r, res["eager"])
         assert all(res["inplace"]), (r, res["inplace"])
         assert all(res["graph"]), (r, res["graph"])
