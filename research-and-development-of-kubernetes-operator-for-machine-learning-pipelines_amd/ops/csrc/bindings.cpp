@@ -698,6 +698,22 @@ bool chan_recv(int64_t h, int64_t consumer, Tensor out, int64_t timeout_us) {
 }
 void chan_unlink(std::string name) { mlop::chan_unlink(name); }
 void chan_close(int64_t h, bool unlink) { mlop::chan_close((long)h, unlink); }
+int64_t xg_create(std::string name, int64_t world, int64_t slots, int64_t max_words) {
+  return mlop::xg_create(name, (int)world, (int)slots, (long)max_words);
+}
+int64_t xg_open(std::string name, int64_t rank) { return mlop::xg_open(name, (int)rank); }
+bool xg_exchange(int64_t h, Tensor vals, Tensor out, Tensor counts, int64_t timeout_us) {
+  const long mw = mlop::xg_max_words((long)h);
+  TORCH_CHECK(!vals.is_cuda() && vals.scalar_type() == at::kLong && vals.is_contiguous() && vals.dim() == 1,
+              "xg_exchange: vals must be a contiguous CPU int64 vector");
+  TORCH_CHECK(!out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.dim() == 2 &&
+              out.size(1) == mw, "xg_exchange: out must be CPU int64 [world, max_words]");
+  TORCH_CHECK(!counts.is_cuda() && counts.scalar_type() == at::kLong && counts.is_contiguous() &&
+              counts.numel() == out.size(0), "xg_exchange: counts must be CPU int64 [world]");
+  return mlop::xg_exchange((long)h, vals.data_ptr<int64_t>(), (long)vals.numel(), out.data_ptr<int64_t>(),
+                           counts.data_ptr<int64_t>(), (long)timeout_us);
+}
+void xg_close(int64_t h) { mlop::xg_close((long)h); }
 
 // ---- expert-parallel exchange over IPC peer memory (ep_exchange.hip) -------------
 int64_t ep_create(int64_t rank, int64_t world, int64_t E, int64_t k, int64_t H, int64_t tcap, int64_t device) {
@@ -766,6 +782,10 @@ TORCH_LIBRARY(mlop, m) {
   m.def("chan_recv(int h, int consumer, Tensor(a!) out, int timeout_us) -> bool", &chan_recv);
   m.def("chan_unlink(str name) -> ()", &chan_unlink);
   m.def("chan_close(int h, bool unlink) -> ()", &chan_close);
+  m.def("xg_create(str name, int world, int slots, int max_words) -> int", &xg_create);
+  m.def("xg_open(str name, int rank) -> int", &xg_open);
+  m.def("xg_exchange(int h, Tensor vals, Tensor(a!) out, Tensor(b!) counts, int timeout_us) -> bool", &xg_exchange);
+  m.def("xg_close(int h) -> ()", &xg_close);
   m.def("ep_create(int rank, int world, int E, int k, int H, int tcap, int device) -> int", &ep_create);
   m.def("ep_ipc_handle(int h) -> Tensor", &ep_ipc_handle);
   m.def("ep_open(int h, Tensor handles) -> ()", &ep_open);

@@ -187,6 +187,11 @@ bool chan_send(long h, const int64_t* w, int n, long timeout_us);
 bool chan_recv(long h, int consumer, int64_t* w, int n, long timeout_us);
 void chan_unlink(const std::string& name);
 void chan_close(long h, bool unlink);
+long xg_create(const std::string& name, int world, int nslots, long max_words);
+long xg_open(const std::string& name, int rank);
+long xg_max_words(long h);
+bool xg_exchange(long h, const int64_t* in, long n, int64_t* out, int64_t* counts, long timeout_us);
+void xg_close(long h);
 
 // expert-parallel dispatch / combine over IPC peer memory (ep_exchange.hip)
 long ep_create(int rank, int world, int E, int k, int H, int tcap, int device);

@@ -249,3 +249,120 @@ class HostChannel:
         if getattr(self, "h", 0):
             torch.ops.mlop.chan_close(self.h, False)
             self.h = 0
+
+
+class HostAllGather:
+    """Lock-step all-gather of small int64 messages between the processes of a group on ONE node,
+    over POSIX shared memory (``ops/csrc/shm_allgather.cc``): the expert-parallel serving loop's
+    per-iteration control (request broadcast, output gather, the step agreement) in one
+    shared-memory hop each instead of gloo TCP round trips.  Every rank calls ``exchange`` the
+    same number of times in the same order; each contributes up to ``max_words`` words and gets
+    every rank's words back.  Collective construction over ``cpu_group`` with the same agreement
+    as ``HostChannel``: every rank gets the segment, or every rank raises ``Unavailable``
+    (``make_host_allgather`` then falls back to gloo on all of them)."""
+
+    SLOTS = 2
+    Unavailable = HostChannel.Unavailable
+
+    def __init__(self, cpu_group, max_words: int):
+        import uuid
+
+        self.max_words = int(max_words)
+        self.h = 0
+        self.rank = dist.get_rank(cpu_group)
+        self.size = dist.get_world_size(cpu_group)
+        name, err = None, ""
+        if self.rank == 0:
+            name = f"/mlop-xg-{uuid.uuid4().hex[:16]}"
+            try:
+                self.h = self._create(name)
+            except Exception as e:  # noqa: BLE001 - agreed on below
+                err, name = f"{type(e).__name__}: {e}", None
+        box = [name]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(cpu_group, 0), group=cpu_group)
+        if self.rank != 0:
+            if box[0] is None:
+                err = "the leader could not create the segment"
+            else:
+                try:
+                    self.h = self._open(box[0])
+                except Exception as e:  # noqa: BLE001
+                    err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if err else 1], dtype=torch.int64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group)
+        if self.rank == 0 and name is not None:
+            torch.ops.mlop.chan_unlink(name)
+        if not int(ok.item()):
+            self.close()
+            raise HostAllGather.Unavailable(err or "another rank could not map the segment")
+        self._out = torch.zeros(self.size, self.max_words, dtype=torch.int64)
+        self._counts = torch.zeros(self.size, dtype=torch.int64)
+
+    def _create(self, name: str) -> int:
+        from .. import ops
+
+        ops.load()
+        return torch.ops.mlop.xg_create(name, self.size, self.SLOTS, self.max_words)
+
+    def _open(self, name: str) -> int:
+        from .. import ops
+
+        ops.load()
+        return torch.ops.mlop.xg_open(name, self.rank)
+
+    def exchange(self, vals: torch.Tensor, timeout_s: float = 600.0) -> list:
+        """Every rank's int64 words, in rank order (views into a reused buffer: copy what must
+        outlive the next exchange).  Waits in 250 ms slices (the op runs without the GIL and
+        resumes where it stopped); a peer silent for ``timeout_s`` raises TimeoutError."""
+        import time
+
+        vals = vals.contiguous()
+        t0 = time.monotonic()
+        while not torch.ops.mlop.xg_exchange(self.h, vals, self._out, self._counts, 250000):
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError("host all-gather: a peer stopped exchanging (dead rank?)")
+        return [self._out[q, :int(self._counts[q])] for q in range(self.size)]
+
+    def close(self):
+        if getattr(self, "h", 0):
+            torch.ops.mlop.xg_close(self.h)
+            self.h = 0
+
+
+class GlooAllGather:
+    """``HostAllGather``'s API over the gloo group (two collectives: the counts, then the words
+    padded to the longest): the fallback when shared memory is unavailable (ranks on different
+    hosts, no /dev/shm)."""
+
+    def __init__(self, cpu_group, max_words: int):
+        self.group, self.max_words = cpu_group, int(max_words)
+        self.size = dist.get_world_size(cpu_group)
+
+    def exchange(self, vals: torch.Tensor, timeout_s: float = 600.0) -> list:
+        n = torch.tensor([vals.numel()], dtype=torch.int64)
+        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(self.size)]
+        dist.all_gather(ns, n, group=self.group)
+        m = max(int(x) for x in ns)
+        if m == 0:
+            return [torch.zeros(0, dtype=torch.int64) for _ in range(self.size)]
+        buf = torch.zeros(m, dtype=torch.int64)
+        buf[:vals.numel()] = vals
+        parts = [torch.zeros(m, dtype=torch.int64) for _ in range(self.size)]
+        dist.all_gather(parts, buf, group=self.group)
+        return [p[:int(c)] for p, c in zip(parts, ns)]
+
+    def close(self):
+        pass
+
+
+def make_host_allgather(cpu_group, max_words: int):
+    """The shared-memory all-gather when every rank can map it (``MLOP_EP_CONTROL=gloo`` forces
+    the gloo fallback), else ``GlooAllGather``; decided collectively."""
+    import sys
+
+    if os.environ.get("MLOP_EP_CONTROL", "shm") == "shm":
+        try:
+            return HostAllGather(cpu_group, max_words)
+        except HostAllGather.Unavailable as e:
+            print(f"[comm] shared-memory all-gather unavailable ({e}): gloo", file=sys.stderr)
+    return GlooAllGather(cpu_group, max_words)

@@ -130,23 +130,27 @@ class EPSync:
     Every rank schedules its OWN requests, but each MoE layer is an all-to-all over the whole
     group, so every rank must run a forward in the same step, with the same MoE capacity, and
     either all replay a decode graph of the same bucket or all run eager.  Once per step every
-    rank calls ``agree`` (a 4-int MAX all-reduce on a CPU gloo group: no GPU sync):
-    [has_work, wants_eager, tokens, bucket] -> what the whole group does this step.  A rank with
-    nothing to do joins with a padding-only forward."""
+    rank calls ``agree``: [has_work, wants_eager, tokens, bucket, busy] from every rank over the
+    group's shared-memory all-gather (parallel/comm.py ``HostAllGather``: one host hop, no GPU
+    sync; gloo when shared memory is unavailable), reduced by MAX on each rank -> what the whole
+    group does this step.  A rank with nothing to do joins with a padding-only forward."""
 
     def __init__(self, group, cpu_group):
+        from ..parallel.comm import make_host_allgather
+
         self.g, self.cpu = group, cpu_group
         self.last_any = 1
         self.last_busy = 1
+        self.xg = make_host_allgather(cpu_group, 8)
+        self._v = torch.zeros(5, dtype=torch.int64)
 
     def agree(self, has_work: int, eager: int, tokens: int, bucket: int, busy: int = 1):
         """``busy``: this rank still holds requests (queued, running or in flight) even if it
         launches nothing this step; the group is done only when no rank is busy."""
-        import torch.distributed as dist
-
-        t = torch.tensor([has_work, eager, tokens, bucket, busy], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.cpu)
-        any_work, any_eager, t_max, b_max, any_busy = t.tolist()
+        v = self._v
+        v[0], v[1], v[2], v[3], v[4] = has_work, eager, tokens, bucket, busy
+        rows = self.xg.exchange(v)
+        any_work, any_eager, t_max, b_max, any_busy = torch.stack(rows).max(dim=0).values.tolist()
         self.last_any, self.last_busy = any_work, any_busy
         return any_work, any_eager, t_max, b_max
 

@@ -7,25 +7,27 @@ puts that group behind ONE predictor endpoint, the way the operator deploys it: 
 GPUs, ``python -m mlopamd.runtime.server --ep N`` (``server.launch_ranks`` starts one process
 per GPU; rank 0 serves HTTP).
 
-Per serving iteration, over the group's CPU (gloo) process group, with fixed-layout int64
-tensors (no pickles: a peer's message can only ever be numbers):
+Per serving iteration, over the group's host all-gather (parallel/comm.py ``HostAllGather``: one
+POSIX shared-memory hop per exchange, ops/csrc/shm_allgather.cc; gloo only when shared memory is
+unavailable), with fixed-layout int64 words (no pickles: a peer's message can only ever be
+numbers):
 
-  1. rank 0 broadcasts a 3-int header [stop, n_new, payload_len] and, when requests arrived over
-     HTTP since the last iteration, one payload tensor of request records (``_pack``): request
-     id, assigned rank (the least-loaded), prompt, sampling parameters (floats as their bit
-     patterns).  Requests are validated on rank 0 BEFORE they are broadcast (``Engine.
-     check_request``): a bad one fails its own HTTP future and never reaches a rank;
+  1. exchange 1 (a broadcast: only rank 0's words are read): [stop, n_new, request records]
+     (``_pack``): request id, assigned rank (the least-loaded), prompt, sampling parameters
+     (floats as their bit patterns).  Requests are validated on rank 0 BEFORE they are sent
+     (``Engine.check_request``): a bad one fails its own HTTP future and never reaches a rank.
+     At most one slot of records travels per iteration; the rest wait for the next one;
   2. every rank admits its share (an admission that still fails is reported back, below) and
-     runs ONE ``engine.step()`` (the EP agreement inside lets a rank with nothing scheduled join
-     the step's expert exchange with a padding-only forward);
-  3. every rank's outputs go to rank 0 as two all_gathers: [n_out, running, n_failed] counts,
-     then the rows [request id, token, finished, reason code] padded to the largest count; rank
-     0 completes the HTTP futures / stream queues, fails the requests a rank could not admit,
-     and keeps the load table.
+     runs ONE ``engine.step()`` (the EP agreement inside -- ``EPSync``, the same kind of
+     exchange -- lets a rank with nothing scheduled join the step's expert exchange with a
+     padding-only forward);
+  3. exchange 2 (an all-gather): [n_out, running, rows of (request id, token, finished, reason
+     code)] from every rank; rank 0 completes the HTTP futures / stream queues, fails the
+     requests a rank could not admit, and keeps the load table.
 
 All ranks therefore call ``engine.step()`` the same number of times, in lock-step, which the
-EP exchange requires.  An idle group keeps a heartbeat (one empty iteration per second) so
-the gloo collectives never sit past their timeout.  Reference contract: one predictor per
+EP exchange requires.  An idle group keeps a heartbeat (one empty iteration per second) so a
+dead rank is noticed (every exchange has a deadline).  Reference contract: one predictor per
 model version behind the SeldonDeployment's endpoint (mlflow_operator.py:194-238).
 """
 from __future__ import annotations
@@ -61,6 +63,11 @@ def _i2f(i: int) -> float:
     return float(np.array([i], dtype=np.int64).view(np.float64)[0])
 
 
+def packed_words(prompt, params) -> int:
+    """int64 words one request record takes in ``_pack``."""
+    return 11 + len(params.stop_token_ids) + len(prompt)
+
+
 def _pack(new) -> torch.Tensor:
     """[(rid, rank, prompt, SamplingParams)] -> one int64 tensor of records:
     rid, rank, len(prompt), max_tokens, top_k, ignore_eos, len(stop), has_seed, seed,
@@ -93,35 +100,32 @@ class EPGroupLoop:
     """The per-iteration protocol, shared by rank 0 (inside ``EPBackend``) and the other ranks."""
 
     def __init__(self, engine, ps):
+        from ..parallel.comm import make_host_allgather
+
         self.engine, self.ps = engine, ps
         self.group = ps.ep_cpu
         self.rank, self.world = ps.ep.rank, ps.ep.size
         self.local: dict[int, int] = {}  # local seq_id -> global request id
         self.iterations = 0
-        self.hdr = torch.zeros(3, dtype=torch.int64)
-
-    def _src(self):
-        import torch.distributed as dist
-
-        return dist.get_global_rank(self.group, 0)
+        # one slot holds a longest prompt's record, and every output row of a full engine
+        self.max_words = max(32768, engine.max_model_len + 64, 8 * engine.cfg.max_num_seqs + 64)
+        self.xg = make_host_allgather(self.group, self.max_words)
+        self._none = torch.zeros(0, dtype=torch.int64)
 
     def iterate(self, stop: bool = False, new=()) -> tuple[bool, list]:
         """One lock-step iteration.  ``stop`` / ``new`` [(rid, rank, prompt, params)]: rank 0's
-        (ignored elsewhere).  Returns (stop, every rank's (outputs [n, 4] int64, running))."""
-        import torch.distributed as dist
-
+        (ignored elsewhere; their packed records must fit one slot).  Returns (stop, every
+        rank's (outputs [n, 4] int64, running))."""
         if self.rank == 0:
-            payload = _pack(new) if new else None
-            self.hdr.copy_(torch.tensor([int(stop), len(new), 0 if payload is None else payload.numel()]))
-        dist.broadcast(self.hdr, src=self._src(), group=self.group)
-        stop, n_new, plen = (int(x) for x in self.hdr.tolist())
-        if n_new:
-            if self.rank != 0:
-                payload = torch.empty(plen, dtype=torch.int64)
-            dist.broadcast(payload, src=self._src(), group=self.group)
-            new = _unpack(payload, n_new)
+            head = torch.tensor([int(stop), len(new)], dtype=torch.int64)
+            msg = torch.cat([head, _pack(new)]) if new else head
+        else:
+            msg = self._none
+        w = self.xg.exchange(msg)[0]  # rank 0's words
+        stop, n_new = int(w[0]), int(w[1])
+        new = _unpack(w[2:], n_new) if n_new else ()
         rows, failed = [], []
-        for rid, r, prompt, params in (new if n_new else ()):
+        for rid, r, prompt, params in new:
             if r != self.rank:
                 continue
             try:
@@ -139,25 +143,15 @@ class EPGroupLoop:
                     self.local.pop(o.seq_id, None)
         rows += [(rid, 0, 1, FAILED) for rid in failed]
         running = self.engine.num_running + len(self.engine.waiting)
-        cnt = torch.tensor([len(rows), running], dtype=torch.int64)
-        cnts = [torch.zeros(2, dtype=torch.int64) for _ in range(self.world)]
-        dist.all_gather(cnts, cnt, group=self.group)
-        m = max(int(c[0]) for c in cnts)
-        gathered = []
-        if m:
-            mine = torch.zeros(m, 4, dtype=torch.int64)
-            if rows:
-                mine[:len(rows)] = torch.tensor(rows, dtype=torch.int64)
-            allr = [torch.zeros(m, 4, dtype=torch.int64) for _ in range(self.world)]
-            dist.all_gather(allr, mine, group=self.group)
-            gathered = [(allr[r][:int(cnts[r][0])], int(cnts[r][1])) for r in range(self.world)]
-        else:
-            gathered = [(torch.zeros(0, 4, dtype=torch.int64), int(cnts[r][1])) for r in range(self.world)]
+        msg = torch.tensor([len(rows), running] + [v for row in rows for v in row], dtype=torch.int64)
+        parts = self.xg.exchange(msg)
+        # copies: the exchange's buffer is reused by the next iteration
+        gathered = [(p[2:2 + 4 * int(p[0])].reshape(-1, 4).clone(), int(p[1])) for p in parts]
         self.iterations += 1
         return bool(stop), gathered
 
     def worker(self):
-        """Ranks > 0: follow rank 0's iterations until it broadcasts stop."""
+        """Ranks > 0: follow rank 0's iterations until it sends stop."""
         while True:
             stop, _ = self.iterate()
             if stop:
@@ -198,13 +192,21 @@ class EPBackend(LLMBackend):
                 with self._lock:
                     pend, self._pending = self._pending, []
                 stop = self._stop
-            new = []
-            for r in pend:
+            new, room = [], self.group_loop.max_words - 2
+            for i, r in enumerate(pend):
                 try:  # validated HERE, before any rank sees it: a bad request fails alone
                     self.engine.check_request(list(r.prompt), r.params)
+                    if packed_words(r.prompt, r.params) > self.group_loop.max_words - 2:
+                        raise ValueError("request too large for the expert-parallel group's control slot")
                 except Exception as e:  # noqa: BLE001
                     r.loop.call_soon_threadsafe(_set_exc, r.future, e)
                     continue
+                need = packed_words(r.prompt, r.params)
+                if need > room:  # one slot per iteration: the rest go next iteration, in order
+                    with self._lock:
+                        self._pending[:0] = pend[i:]
+                    break
+                room -= need
                 rid = next(self._rid)
                 self._by_rid[rid] = r
                 new.append((rid, self._assign(), list(r.prompt), r.params))

@@ -342,3 +342,52 @@ def test_host_channel_failure_falls_back_together(fn):
     r0, r1 = run_ranks(fn, 2)
     assert r0["raised"] and r1["raised"] and not r0["leftover"] and not r1["leftover"]
     assert r0["tp"] == r0["ref"] and r1["worker_steps"] > 0
+
+
+def _xg_stress(rank, world):
+    """parallel/comm.HostAllGather (ops/csrc/shm_allgather.cc): lock-step exchanges of
+    variable-length messages (0 .. max_words words, the ring of 2 slots reused 2000 times), a
+    rank that arrives late (the others' waits time out in their 250 ms slices and RESUME the same
+    exchange), every rank sees every rank's words in order; nothing is left in /dev/shm; the
+    gloo fallback gives the same answers."""
+    import glob
+    import time
+
+    import torch.distributed as dist
+
+    from mlopamd.parallel.comm import GlooAllGather, HostAllGather
+
+    cpu = dist.new_group(list(range(world)), backend="gloo")
+    xg = HostAllGather(cpu, max_words=64)
+    dist.barrier(group=cpu)
+    leftover = glob.glob("/dev/shm/mlop-xg-*")
+    ok = True
+    for it in range(2000):
+        n = (it * 7 + rank * 13) % 65
+        v = torch.arange(n, dtype=torch.int64) + 1000 * rank + it
+        if it in (5, 1200) and rank == world - 1:
+            time.sleep(0.6)  # the others' first slices expire mid-exchange
+        got = xg.exchange(v)
+        for q in range(world):
+            m = (it * 7 + q * 13) % 65
+            ok &= got[q].numel() == m and (m == 0 or (int(got[q][0]) == 1000 * q + it and
+                                                      int(got[q][-1]) == 1000 * q + it + m - 1))
+    xg.close()
+    gl = GlooAllGather(cpu, 64)
+    g2 = gl.exchange(torch.arange(rank + 1, dtype=torch.int64))
+    ok &= [x.tolist() for x in g2] == [list(range(q + 1)) for q in range(world)]
+    return {"ok": bool(ok), "leftover": leftover}
+
+
+def xg2(rank, world):
+    return _xg_stress(rank, world)
+
+
+def xg4(rank, world):
+    return _xg_stress(rank, world)
+
+
+@pytest.mark.parametrize("fn,world", [("xg2", 2), ("xg4", 4)])
+def test_host_allgather(fn, world):
+    res = run_ranks(fn, world)
+    assert all(r["ok"] for r in res) and not any(r["leftover"] for r in res)
