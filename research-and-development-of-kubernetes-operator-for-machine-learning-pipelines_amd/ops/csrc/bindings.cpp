@@ -229,6 +229,12 @@ int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_
 int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
+void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits) {
+  mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits);
+}
+void gemm_grouped_plan(int64_t bm, int64_t bn, int64_t stages, int64_t splits) {
+  mlop::gemm_grouped_plan((int)bm, (int)bn, (int)stages, (int)splits);
+}
 int64_t gemm_small_stages(int64_t set) { return mlop::gemm_small_stages((int)set); }
 int64_t gemm_small_tile(int64_t set) { return mlop::gemm_small_tile((int)set); }
 int64_t gemm_sk_mode(int64_t set) { return mlop::gemm_sk_mode((int)set); }
@@ -726,7 +732,7 @@ Tensor ep_ipc_handle(int64_t h) {
 }
 void ep_open(int64_t h, Tensor handles) {
   TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.is_contiguous() &&
-              handles.dim() == 2 && handles.size(1) == 128, "handles: CPU uint8 [world, 128]");
+              handles.dim() == 2 && handles.size(1) == 64, "handles: CPU uint8 [world, 64]");
   mlop::ep_open((long)h, handles.data_ptr());
 }
 // xp [rows, H] bf16 <- this rank's received rows grouped by local expert; offsets int32 [n_local + 1]
@@ -796,6 +802,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("ep_destroy(int h) -> ()", &ep_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
+  m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
+  m.def("gemm_dense_plan(int variant, int bm, int bn, int splits) -> ()", &gemm_dense_plan);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
   m.def("gemm_small_tile(int set=-1) -> int", &gemm_small_tile);
   m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);

@@ -389,6 +389,40 @@ int gemm_small_tile(int set) {
   return g_small_tile;
 }
 
+// round-4 planner rules (MLOP_GEMM_PLAN_R4=1): the same-box A/B of the round-5 tile choices
+static const int g_plan_r4 = env_int("MLOP_GEMM_PLAN_R4", 0);
+
+// grouped-plan override (scripts/bench_moe_decode.py compares MoE decode tilings in one process):
+// BM, BN, ring stages, K splits; -1 = the planner's own choice.  Only tile shapes launch_plan has
+// a grouped config for are accepted.
+static int g_gp[4] = {-1, -1, -1, -1};
+void gemm_grouped_plan(int bm, int bn, int stages, int splits) {
+  if (bm > 0) {
+    static const int ok[][2] = {{16, 32}, {16, 64}, {32, 32}, {32, 64}, {64, 32}, {64, 64},
+                                {128, 64}, {256, 64}, {256, 128}, {256, 256}};
+    bool found = false;
+    for (const auto& t : ok) found = found || (t[0] == bm && t[1] == bn);
+    if (!found) throw std::runtime_error("gemm_grouped_plan: no grouped config for this tile");
+  }
+  g_gp[0] = bm, g_gp[1] = bn, g_gp[2] = stages, g_gp[3] = splits;
+}
+
+// dense-plan override (scripts/bench_mid_m.py sweeps the mid-M projection tilings in one
+// process): variant (0 = gemm_kernel BM x BN, 1 = 256x256 two-stage, 3 = ping-pong, 5 =
+// four-wave), BM, BN, K splits (plain gemm_kernel only); -1 = the planner's own choice
+static int g_dp[4] = {-1, -1, -1, -1};
+void gemm_dense_plan(int variant, int bm, int bn, int splits) {
+  if (variant >= 0 && variant != 0 && variant != 1 && variant != 3 && variant != 5)
+    throw std::runtime_error("gemm_dense_plan: variant must be 0, 1, 3 or 5");
+  if (variant == 0) {
+    static const int ok[][2] = {{64, 64}, {128, 64}, {256, 64}, {256, 128}};
+    bool found = false;
+    for (const auto& t : ok) found = found || (t[0] == bm && t[1] == bn);
+    if (!found) throw std::runtime_error("gemm_dense_plan: no dense config for this tile");
+  }
+  g_dp[0] = variant, g_dp[1] = bm, g_dp[2] = bn, g_dp[3] = splits;
+}
+
 // large-M kernel choice (plan() variants below); MLOP_GEMM_BIG_VARIANT at load, and
 // settable at run time (gemm_big_variant op) so A/B microbenches run in one process
 static int g_big_variant = env_int("MLOP_GEMM_BIG_VARIANT", 5);
@@ -590,7 +624,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       for (int i = 0; i < 2; ++i) {
         const int r = h < 2 ? i * 128 + h * 64 + wid * 8 + prow : (h & 1) * 128 + (wid + 8 * i) * 8 + prow;
         const int ch = (lane & 7) ^ swz(r);
-        voff[h][i] = h < 2 ? (uint32_t)((size_t)min(m0 + r, m_end - 1) * lda * 2) + ch * 16
+        // A rows past the tile's last row (the ragged / grouped tail: a spill m-tile of an expert
+        // with 256 + a few rows is almost all such rows) load nothing: an offset past the
+        // resource's num_records makes the LDS-DMA a dropped out-of-range access, still counted
+        // by vmcnt (the counted waits stay exact) but fetching no line.  Their LDS rows hold
+        // don't-care values that only ever reach accumulator rows that are never stored.
+        voff[h][i] = h < 2 ? (m0 + r < m_end ? (uint32_t)((size_t)(m0 + r) * lda * 2) + ch * 16 : 0x80000000u)
                            : (uint32_t)((size_t)min(n0 + r, N - 1) * ldb * 2) + ch * 16;
       }
     auto issue_half = [&](int buf, int h, int kt) {
@@ -991,7 +1030,13 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   Plan p{};
   p.variant = 0;
   const int mrows = grouped ? rows_per_group : M;
-  static const int pp_group_min_rows = env_int("MLOP_GEMM_PP_GROUP_MIN_ROWS", 256);
+  // grouped (MoE): the ping-pong kernel from ~56 routed rows per expert.  Its 256 x 256 tile
+  // streams each expert's weight panel once per n-tile and skips the MFMAs of empty 64-row
+  // quadrants, so a half-empty expert tile costs less than the extra m-tiles (each a second walk
+  // of the expert's weights) of the narrower kernels: Mixtral gate_up / down at 512 routed rows
+  // 474 -> 370 / 266 -> 200 us, 1024 rows 692 -> 389 / 375 -> 208 us; 48 rows per expert equal
+  // (scripts/bench_moe_decode.py, profiles/r05_moe_decode.md)
+  static const int pp_group_min_rows = g_plan_r4 ? 256 : 56;
   if (grouped && mrows >= pp_group_min_rows && K % kBK == 0 && N % 256 == 0) {
     p.BM = 256; p.BN = 256; p.variant = 3;  // grouped ping-pong
   } else if (mrows <= 64 && !grouped && g_small_tile == 1) {
@@ -1058,6 +1103,41 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
       p.BN = 256;
       p.variant = big;
     }
+    if (!g_plan_r4 && !grouped && big == 5) {
+      // long-K narrow projections (down, K = 14336) at 40-71 tiles of 256 x 256 (M 640-1279):
+      // the ping-pong kernel's stream-K tail spreads the few tiles' K over every CU (down at
+      // M = 768: 105 -> 90 us, 1024: 118 -> 108; hipBLASLt 90 / 111)
+      if (p.variant == 0 && K >= 8192 && t256 >= 40 && t256 < mid_tiles && K % kBK == 0 &&
+          sk_halves_ok(t256, K / kBK)) {
+        p.BN = 256;
+        p.variant = 3;
+      }
+      // four-wave vs ping-pong past one full round: the four-wave kernel runs whole rounds of
+      // 256 x 256 tiles (a tail of r <= CUs / 2 tiles in K-halves), the ping-pong kernel ~7 %
+      // slower per tile but with a stream-K tail that balances ANY remainder.  Estimated time in
+      // four-wave tile rounds: w4 = q + (r ? (2r <= C ? 0.55 : 1) : 0), pp = 1.08 T / C + 0.05.
+      // (M = 4608: o 147 -> 134 us, down 476 -> 403, qkv 181 -> 172; the headline's M ~ 4088 is
+      // whole rounds for every projection and stays on the four-wave kernel; bench_mid_m.py)
+      const SkBuf* b = sk_buf();
+      if (p.variant == 5 && b && t256 > b->cus && pp_ok) {
+        const long C = b->cus, q = t256 / C, r = t256 % C;
+        const float w4_est = (float)q + (r == 0 ? 0.f : (2 * r <= C ? 0.55f : 1.f));
+        const float pp_est = 1.08f * (float)t256 / (float)C + 0.05f;
+        if (pp_est < w4_est - 0.03f) p.variant = 3;
+      }
+    }
+  }
+  if (!grouped && g_dp[0] >= 0) {  // bench override (gemm_dense_plan)
+    p.variant = g_dp[0];
+    p.BM = p.variant == 0 ? g_dp[1] : 256;
+    p.BN = p.variant == 0 ? g_dp[2] : 256;
+    p.stages = 0;
+  }
+  if (grouped && g_gp[0] > 0) {  // bench override (gemm_grouped_plan)
+    p.BM = g_gp[0];
+    p.BN = g_gp[1];
+    p.variant = (p.BM == 256 && p.BN == 256) ? 3 : 0;
+    p.stages = g_gp[2] > 0 ? g_gp[2] : 0;
   }
   const int n_tiles = (N + p.BN - 1) / p.BN;
   const int real_m_tiles = (M + p.BM - 1) / p.BM;
@@ -1070,6 +1150,11 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3 && p.variant != 5) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
+    p.splits = (K + kc - 1) / kc;
+    p.k_chunk = kc;
+  }
+  if (!grouped && g_dp[0] == 0 && g_dp[3] >= 1) {
+    const int kc = ((K / g_dp[3] + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
     p.k_chunk = kc;
   }
@@ -1273,11 +1358,12 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
   // stream-K slab buffer (same stream, so never in use by another launch), then the reduce
   // kernel applies the epilogue.  Routed tiles are estimated as one m-tile per expert.
   float* ws = nullptr;
-  if (p.variant != 3 && K >= 2048) {
+  if (p.variant != 3 && K >= 2048 && g_gp[3] != 1) {
     const SkBuf* b = sk_buf();
     const long t_est = (long)((N + p.BN - 1) / p.BN) * std::max(1, std::min(n_groups, (M + p.BM - 1) / p.BM + n_groups));
     static const int target = env_int("MLOP_GROUPED_SPLIT_TARGET", 1024);
     int s = (int)std::min<long>(8, std::max<long>(1, target / std::max<long>(1, t_est)));
+    if (g_gp[3] > 1) s = g_gp[3];
     while (s > 1 && (K / s) % kBK) --s;
     if (b && s > 1 && (size_t)s * M * N * 4 <= (size_t)2 * kSkMaxWg * 256 * 256 * 4) {
       p.splits = s;

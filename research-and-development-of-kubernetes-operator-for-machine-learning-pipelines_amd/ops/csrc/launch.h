@@ -62,6 +62,8 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong, 5 four-wave asm K-loop); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
+void gemm_grouped_plan(int bm, int bn, int stages, int splits);
+void gemm_dense_plan(int variant, int bm, int bn, int splits);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip); epi 0 / 1 / 3
 bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
 // the four-wave kernel cuts its r = T % CUs tail tiles into K-halves (2r <= CUs, nk even)

@@ -665,6 +665,9 @@ def test_grouped_gemm_large_groups(gpu, rows, epi):
     ([2000, 0, 0, 7, 0, 1500, 300, 281], 0, 4096, 14336),        # empty / tiny experts
     ([16, 17, 15, 16, 16, 18, 14, 16], 0, 4096, 14336),           # mid-size batch: split-K grouped (reduce)
     ([16, 16, 0, 30, 16, 10, 16, 24], 1, 28672, 4096),            # ... with the SiLU-mul epilogue in the reduce
+    ([58, 54, 67, 83, 56, 59, 67, 68], 1, 28672, 4096),           # ~64 rows per expert: ping-pong from 56 (r5)
+    ([120, 135, 160, 98, 140, 111, 130, 130], 0, 4096, 14336),    # ~128 rows: half-empty 256-row tiles
+    ([257, 257, 257, 257, 257, 257, 257, 257], 1, 28672, 4096),   # decode-only spill: 1-row second tiles
 ])
 def test_grouped_gemm_stream_k(gpu, counts, epi, N, K):
     """Mixtral-size grouped GEMM with the stream-K tail planned ON DEVICE from the routed
