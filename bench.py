@@ -98,6 +98,9 @@ def parse(argv=None):
                          "engine-direct run, and report it as served_tokens_per_sec_http; its window is "
                          "max(--steps, 40) engine steps.  -1 (default): on for the 1-GPU operator bench, "
                          "off otherwise; 0 / 1 force it")
+    ap.add_argument("--ab-ops", default="",
+                    help="A/B runs: comma list of op=value set through torch.ops.mlop before the engine "
+                         "is built, e.g. gemm_half_tile=0 (in-process switches, scripts/ab.sh)")
     ap.add_argument("--cr-ready-samples", type=int, default=3,
                     help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
                          "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
@@ -204,6 +207,19 @@ def launch(a, argv) -> int:
     return rc
 
 
+def _apply_ab_ops(spec: str) -> dict:
+    """``op=value,...`` -> torch.ops.mlop.<op>(value) for the in-process A/B switches
+    (gemm_half_tile, gemm_big_variant, ...); returns each op's previous value."""
+    from mlopamd import ops
+
+    ops.load()
+    prev = {}
+    for item in filter(None, (t.strip() for t in spec.split(","))):
+        name, _, val = item.partition("=")
+        prev[name] = getattr(torch.ops.mlop, name)(int(val))
+    return prev
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
@@ -229,6 +245,8 @@ def main(argv=None):
     dev = torch.device("cuda", 0 if a.share_gpu else local_rank) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+    if a.ab_ops:
+        _apply_ab_ops(a.ab_ops)
 
     from mlopamd.runtime.deploy import deploy_for_bench
 
@@ -258,7 +276,6 @@ def main(argv=None):
                        "exchange": "ipc" if getattr(ps.ep, "ex", None) is not None else "all_to_all"}
     elif a.tp > 1:
         assert world % a.tp == 0, f"world {world} not divisible by --tp {a.tp}"
-        os.environ.setdefault("MLOP_TP_GRAPHS", "1")  # the one-shot all-reduce is graph-capturable
         from mlopamd.runtime.tp_worker import build_tp_engine
 
         engine, ps = build_tp_engine(a.model, a.tp, device=dev, seed=a.seed + rank // a.tp, engine_kwargs=ekw)

@@ -23,7 +23,6 @@ from .config import ModelConfig
 from .layers import init_norm, init_weight, linear, rope_table
 
 
-DECODE_FUSED_MAX_T = 4  # gemv.hip's NORM prologue sizes (M <= 4)
 
 
 class LlamaModel:
@@ -152,47 +151,11 @@ class LlamaModel:
     def weight_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.weight_tensors())
 
-    def post_attention(self, i: int, o: torch.Tensor, residual: torch.Tensor, eps: float):
-        """Decode form of the MLP block: (MLP output before any TP all-reduce, new
-        residual); the post-attention residual add + RMSNorm rides in the gate_up
-        projection's prologue (ops.norm_gemm)."""
-        L = self.layers[i]
-        act, residual = ops.norm_gemm(o, residual, L["post_norm"], L["gate_up"], eps, ops.EPI_SILU_MUL)
-        return linear(act, L["down"]), residual
-
-    def forward_decode(self, ids: torch.Tensor, meta, kv) -> torch.Tensor:
-        """Small-batch decode (T <= 4, the GEMV sizes): every residual add + RMSNorm is
-        the prologue of the projection that consumes it (QKV of the next layer, gate_up),
-        so a layer is QKV+RoPE+KV-store, attention, O, gate_up+SiLU, down: five weight
-        streams and no norm launches (SURVEY.md §3.5 call stack, fused)."""
-        cfg, tp = self.cfg, self.ps.tp
-        eps = cfg.rms_eps
-        h = ops.embedding(ids, self.embed, self.vocab_start)
-        tp.all_reduce(h)
-        residual = h
-        y = None
-        for i, L in enumerate(self.layers):
-            if y is None:
-                x = ops.rmsnorm(h, L["in_norm"], eps)
-                q = ops.qkv_rope_cache(x, L["qkv"], meta.positions, self.cos_sin, meta.slots, kv.k[i], kv.v[i],
-                                       self.n_q)
-            else:
-                q, residual = ops.norm_qkv_rope_cache(y, residual, L["in_norm"], L["qkv"], meta.positions,
-                                                      self.cos_sin, meta.slots, kv.k[i], kv.v[i], self.n_q, eps)
-            a = ops.paged_attention(q, kv.k[i], kv.v[i], meta)
-            o = linear(a.view(a.shape[0], -1), L["o"])
-            tp.all_reduce(o)
-            y, residual = self.post_attention(i, o, residual, eps)
-            tp.all_reduce(y)
-        return ops.add_rmsnorm(y, residual, self.final_norm, eps)
-
     def forward(self, ids: torch.Tensor, meta, kv) -> torch.Tensor:
         """ids [T] int64; meta: AttnMeta (positions/slots/tables); kv: KVCache.
         Returns the final-normed hidden states of every token [T, H]."""
         cfg, tp = self.cfg, self.ps.tp
         eps = cfg.rms_eps
-        if ids.shape[0] <= DECODE_FUSED_MAX_T and ops.NORM_FUSION:
-            return self.forward_decode(ids, meta, kv)
         h = ops.embedding(ids, self.embed, self.vocab_start)
         tp.all_reduce(h)
         residual = h

@@ -178,7 +178,7 @@ class HFWeights:
 
 
 def load_pretrained(path: str | os.PathLike, device="cuda", dtype=torch.bfloat16, pstate=None,
-                    name: str | None = None):
+                    name: str | None = None, fold_norms: bool = True):
     """Build our model for the checkpoint in ``path`` and copy its (TP-sharded) weights in."""
     from . import build_model
 
@@ -189,8 +189,8 @@ def load_pretrained(path: str | os.PathLike, device="cuda", dtype=torch.bfloat16
         model.load_shard_from(HFWeights(path, cfg))
     # checkpoints carry trained (non-unit) RMSNorm weights: fold them into the projections that
     # consume them so the large-M forward can run the norm chain (LlamaModel._chain_ok needs unit
-    # norms).  The same function up to the bf16 rounding of g * W; MLOP_FOLD_NORMS=0 keeps them.
-    if os.environ.get("MLOP_FOLD_NORMS", "1") != "0":
+    # norms).  The same function up to the bf16 rounding of g * W; fold_norms=False keeps them.
+    if fold_norms:
         model.fold_norms()
     return model
 

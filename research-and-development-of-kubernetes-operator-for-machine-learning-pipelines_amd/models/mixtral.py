@@ -64,11 +64,6 @@ class MixtralModel(LlamaModel):
         self.ps.tp.all_reduce(m)
         return ops.add_rmsnorm(m, residual, next_norm, eps)
 
-    def post_attention(self, i, o, residual, eps):
-        """MoE block in the decode forward: the router / grouped GEMM take a normed x."""
-        x = ops.add_rmsnorm(o, residual, self.layers[i]["post_norm"], eps)
-        return self.mlp(i, x), residual
-
     def mlp_add_norm(self, i, x, residual, next_norm, eps):
         """TP = EP = 1: MoE block + the next residual add / norm (decode-size dispatch in one
         launch, combine fused into the norm: parallel.moe.moe_forward_add_norm)."""

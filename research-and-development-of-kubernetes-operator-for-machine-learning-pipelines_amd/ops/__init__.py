@@ -248,16 +248,13 @@ def reset_gemm_used() -> None:
     _GEMM_USED.clear()
 
 
-_POW2_BUCKETS = os.environ.get("MLOP_GEMM_MBUCKET") == "pow2"  # A/B against the old keys
-
-
 def _mbucket(M: int) -> int:
     """Autotune key for the row count: powers of two up to 256 (GEMV / narrow-tile
     regimes), then every 256 rows: above one tile row the winner flips with how the
     256-row tiles fill the 256 CUs (e.g. QKV at M=2040 is 192 tiles = 3/4 of the chip
     for the fused RoPE kernel, while hipBLASLt's stream-K does not care), so
     power-of-two buckets let the first M seen in [1025, 2048] decide for all of them."""
-    if M > 256 and not _POW2_BUCKETS:
+    if M > 256:
         return (M + 255) // 256 * 256
     b = 1
     while b < M:
@@ -472,15 +469,16 @@ def qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads:
 # by rsqrt(total / K + eps) =
 # RMSNorm after the GEMM, with the norm weight folded into their weights (LlamaModel.fold_norms).
 # "1" (default): on where every GEMM of the chain runs on the four-wave kernel; "0" off;
-# "force": also on CPU / any shape through the torch reference below (plumbing tests).
-NORM_CHAIN = os.environ.get("MLOP_NORM_CHAIN", "1")
+# "force": also on CPU / any shape through the torch reference below (plumbing tests set it).
+NORM_CHAIN = "1"
 
 
 # The decode (M <= 4) form of the chain runs on the GEMV (gemv.hip EPI_RES / PRO_RS): O and down
 # add into the residual in place, QKV and gate_up take each row's factor from the residual
-# chunks they stream, so a layer has no add + RMSNorm launch.  "0" keeps the decode norms.
-GEMV_CHAIN = os.environ.get("MLOP_GEMV_CHAIN", "1") == "1"
-GEMV_CHAIN_MAX_M = min(8, max(1, int(os.environ.get("MLOP_GEMV_CHAIN_MAX_M", 4))))  # = gemv.hip gemv_chain_max_m
+# chunks they stream, so a layer has no add + RMSNorm launch.  False keeps the decode norms (the
+# GPU tests' A/B).
+GEMV_CHAIN = True
+GEMV_CHAIN_MAX_M = 4  # = gemv.hip gemv_chain_max_m
 
 
 def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
@@ -494,6 +492,8 @@ def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
         return H % 128 == 0
     if NORM_CHAIN == "0" or GEMM_BACKEND != "mlop" or H % 256:
         return False
+    if device is not None and torch.device(device).type != "cuda":
+        return False  # the torch reference path (CPU) has no chain kernels
     _need_gpu()
     if M <= GEMV_CHAIN_MAX_M:
         epis = epis or [EPI_NONE] * len(shapes)
@@ -581,55 +581,6 @@ def qkv_rope_cache_rs(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_hea
 
 
 EPI_ADD_SS, EPI_RS = 4, 8  # norm-chain epilogue flags (gemm_used() keys; gemm_w4.hip W4_ADD_SS / W4_RS)
-
-
-# Residual add + RMSNorm as the decode GEMV's prologue (gemv.hip NORM).  Measured a wash at
-# batch 1 (315-318 vs 318 tok/s unfused, scripts/history/run41.sh: the two norm launches it removes
-# cost what the heavier prologue adds to the two GEMVs) and a loss at batch 2-4, so it is
-# opt-in: MLOP_NORM_FUSION=1.  Re-measured with the K-split gate_up GEMV (scripts/history/run60.sh):
-# 302-306 fused vs 332-338 tok/s unfused at batch 1, 622 vs 617 at batch 2 — still off.
-NORM_FUSION = os.environ.get("MLOP_NORM_FUSION", "0") == "1"
-
-
-def norm_fusable(M: int, N: int, K: int, epi: int) -> bool:
-    """True when the residual add + RMSNorm can ride in the consuming projection
-    (decode sizes: the GEMV's NORM prologue, gemv.hip)."""
-    if not NORM_FUSION:
-        return False
-    _need_gpu()
-    return bool(torch.ops.mlop.gemm_norm_supported(M, N, K, epi))
-
-
-def norm_gemm(y, residual, norm_w, w, eps: float, epi: int = EPI_NONE):
-    """(epi(rmsnorm(residual + y) * norm_w @ w^T), residual + y) in ONE launch at decode
-    sizes (the add + norm become the GEMV's prologue); otherwise add_rmsnorm (residual
-    updated in place) + gemm.  Callers must use the returned residual."""
-    M, K = y.shape[0], y.shape[-1]
-    N = w.shape[0]
-    if y.is_cuda and norm_fusable(M, N, K, epi):
-        res_out = torch.empty_like(residual)
-        out = torch.empty(M, N if epi == EPI_NONE else N // 2, dtype=y.dtype, device=y.device)
-        if torch.ops.mlop.gemm_norm(out, res_out, y, residual, norm_w, w, eps, epi):
-            return out, res_out
-    x = add_rmsnorm(y, residual, norm_w, eps)
-    return gemm(x, w, epi=epi), residual
-
-
-def norm_qkv_rope_cache(y, residual, norm_w, w, positions, cos_sin, slots, k_cache, v_cache,
-                        n_q_heads: int, eps: float):
-    """QKV projection of the next layer with the previous layer's residual add + RMSNorm
-    as its prologue and RoPE + paged K/V stores as its epilogue (one launch at decode
-    sizes).  Returns (q, new residual)."""
-    M, K = y.shape[0], y.shape[-1]
-    N = w.shape[0]
-    if y.is_cuda and norm_fusable(M, N, K, EPI_ROPE):
-        res_out = torch.empty_like(residual)
-        q = torch.empty(M, n_q_heads, k_cache.shape[3], dtype=y.dtype, device=y.device)
-        if torch.ops.mlop.gemm_norm_rope(q, k_cache, v_cache, res_out, y, residual, norm_w, w, positions,
-                                         cos_sin, slots, eps):
-            return q, res_out
-    x = add_rmsnorm(y, residual, norm_w, eps)
-    return qkv_rope_cache(x, w, positions, cos_sin, slots, k_cache, v_cache, n_q_heads), residual
 
 
 GEMM_TABLE = Path(os.environ.get("MLOP_GEMM_TABLE", str(Path(__file__).with_name("gemm_table_gfx950.json"))))

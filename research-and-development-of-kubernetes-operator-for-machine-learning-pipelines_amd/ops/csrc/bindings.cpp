@@ -128,14 +128,11 @@ void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor 
                              (int)k_cache.size(0), cur_stream());
 }
 
-// Largest (tile, kv head) pair count that takes the in-launch split-KV combine
-// (MLOP_ATTN_FUSED_MAX_PAIRS; attn_fused_max_pairs() in-process, -1 reads it back).
-static int g_attn_fused_pairs = -1;
-static int attn_fused_pairs_cap() {
-  if (g_attn_fused_pairs < 0)
-    g_attn_fused_pairs = getenv("MLOP_ATTN_FUSED_MAX_PAIRS") ? atoi(getenv("MLOP_ATTN_FUSED_MAX_PAIRS")) : (1 << 30);
-  return g_attn_fused_pairs;
-}
+// Largest (tile, kv head) pair count that takes the in-launch split-KV combine: no cap (a cap of
+// 32 pairs measured the same at 16 x 32k contexts, BASELINE.md long context); settable in-process
+// for the tests (attn_fused_max_pairs(); -1 reads it back).
+static int g_attn_fused_pairs = 1 << 30;
+static int attn_fused_pairs_cap() { return g_attn_fused_pairs; }
 int64_t attn_fused_max_pairs(int64_t n) {
   const int prev = attn_fused_pairs_cap();
   if (n >= 0) g_attn_fused_pairs = (int)n;
@@ -229,6 +226,7 @@ int64_t vmm_chunks_ready(Tensor flat) { return mlop::vmm_chunks_ready(flat.data_
 int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
+int64_t gemm_half_tile(int64_t set) { return mlop::gemm_half_tile((int)set); }
 void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits) {
   mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits);
 }
@@ -242,11 +240,7 @@ bool gemm_sk_reserve() { return mlop::gemm_sk_reserve(); }
 int64_t gemm_sk_workgroups(int64_t M, int64_t N, int64_t K) { return mlop::gemm_sk_workgroups((int)M, (int)N, (int)K); }
 
 int64_t gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t epi) {
-  if (epi == 2) {  // GEMM + residual add + RMSNorm: the GEMV epilogue form's partials, else split-K slabs
-    const long g = mlop::gemv_addnorm_ws_floats((int)M, (int)N, (int)K);
-    if (g > 0) return g;
-    return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, 0);
-  }
+  if (epi == 2) return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, 0);  // GEMM + add + RMSNorm: split-K slabs
   return mlop::gemm_workspace_floats((int)M, (int)N, (int)K, (int)epi);
 }
 
@@ -433,61 +427,8 @@ bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor no
 
 // Decode projection with the residual add + RMSNorm feeding it fused in as a prologue
 // (gemv.hip NORM, M <= 4): res_out = bf16(res_in + y); out = epi(rmsnorm(res_out) * norm_w @ w^T).
-// epi 0 / 1 write out [M, N or N/2]; epi 3 (RoPE) writes q_out / k_cache / v_cache instead.
-// false = shape not on this path (caller runs add_rmsnorm + the projection).
-bool gemm_norm_impl(Tensor* out, Tensor* q_out, Tensor* k_cache, Tensor* v_cache, Tensor res_out,
-                    Tensor y, Tensor res_in, Tensor norm_w, Tensor w, const Tensor* pos,
-                    const Tensor* cos_sin, const Tensor* slots, double eps, int64_t epi) {
-  check_bf16(res_out, "res_out"); check_bf16(y, "y"); check_bf16(res_in, "res_in");
-  check_bf16(norm_w, "norm_w"); check_bf16(w, "w");
-  const int64_t N = w.size(0), K = w.size(1), M = y.numel() / std::max<int64_t>(K, 1);
-  TORCH_CHECK(w.dim() == 2 && y.numel() == M * K && res_in.numel() == M * K && res_out.numel() == M * K &&
-                  norm_w.numel() == K, "y / residual [M, K], norm_w [K], w [N, K]");
-  TORCH_CHECK(res_out.data_ptr() != res_in.data_ptr(), "res_out must not alias res_in");
-  if (!mlop::gemv_norm_takes((int)M, (int)N, (int)K, (int)epi)) return false;
-  mlop::NormPro np{(const uint16_t*)y.data_ptr(), (const uint16_t*)res_in.data_ptr(),
-                   (uint16_t*)res_out.data_ptr(), (const uint16_t*)norm_w.data_ptr(), (float)eps};
-  c10::DeviceGuard g(y.device());
-  if (epi == 3) {
-    check_bf16(*q_out, "q_out"); check_bf16(*k_cache, "k_cache"); check_bf16(*v_cache, "v_cache");
-    check_i32(*pos, "pos"); check_i32(*slots, "slots");
-    const int64_t Hq = q_out->size(1), D = q_out->size(2), Hkv = k_cache->size(1), BS = k_cache->size(2);
-    TORCH_CHECK(D == 128 && N == (Hq + 2 * Hkv) * D && q_out->size(0) == M && pos->numel() == M &&
-                    slots->numel() == M && v_cache->sizes() == k_cache->sizes(),
-                "qkv layout: head_dim 128, q_out [M, Hq, 128], k and v [NB,Hkv,BS,D]");
-    TORCH_CHECK(cos_sin->is_cuda() && cos_sin->scalar_type() == at::kFloat && cos_sin->size(1) == D, "cos_sin");
-    mlop::RopeEpi re{(uint16_t*)q_out->data_ptr(), (uint16_t*)k_cache->data_ptr(),
-                     (uint16_t*)v_cache->data_ptr(), pos->data_ptr<int>(), cos_sin->data_ptr<float>(),
-                     slots->data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
-    mlop::launch_gemv_norm(np, w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re, cur_stream());
-    return true;
-  }
-  check_bf16(*out, "out");
-  TORCH_CHECK(epi == 0 || epi == 1, "epi");
-  TORCH_CHECK(out->numel() == M * (epi == 0 ? N : N / 2), "out [M, N or N/2]");
-  mlop::launch_gemv_norm(np, w.data_ptr(), out->data_ptr(), (int)(epi == 0 ? N : N / 2), (int)M, (int)N,
-                         (int)K, (int)epi, mlop::RopeEpi{}, cur_stream());
-  return true;
-}
-
-bool gemm_norm(Tensor out, Tensor res_out, Tensor y, Tensor res_in, Tensor norm_w, Tensor w, double eps,
-               int64_t epi) {
-  return gemm_norm_impl(&out, nullptr, nullptr, nullptr, res_out, y, res_in, norm_w, w, nullptr, nullptr,
-                        nullptr, eps, epi);
-}
-
-bool gemm_norm_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor res_out, Tensor y, Tensor res_in,
-                    Tensor norm_w, Tensor w, Tensor pos, Tensor cos_sin, Tensor slots, double eps) {
-  return gemm_norm_impl(nullptr, &q_out, &k_cache, &v_cache, res_out, y, res_in, norm_w, w, &pos, &cos_sin,
-                        &slots, eps, 3);
-}
-
 bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
-}
-
-bool gemm_norm_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
-  return mlop::gemv_norm_takes((int)M, (int)N, (int)K, (int)epi);
 }
 
 // grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
@@ -684,7 +625,6 @@ void car_all_gather(int64_t h, Tensor out, Tensor piece) {
   mlop::car_all_gather((long)h, out.data_ptr(), (long)(out.numel() * out.element_size()), piece.data_ptr(), nbytes,
                        cur_stream());
 }
-int64_t gemv_addnorm_enable(int64_t on) { return mlop::gemv_addnorm_enable((int)on); }
 int64_t car_error(int64_t h) { return mlop::car_error((long)h); }
 int64_t car_mem_mode(int64_t h) { return mlop::car_mem_mode((long)h); }
 void car_destroy(int64_t h) { mlop::car_destroy((long)h); }
@@ -778,7 +718,6 @@ TORCH_LIBRARY(mlop, m) {
   m.def("car_broadcast(int h, Tensor(a!) buf, int root) -> ()");
   m.def("car_all_gather(int h, Tensor(a!) out, Tensor piece) -> ()");
   m.def("car_error(int h) -> int", &car_error);
-  m.def("gemv_addnorm_enable(int on) -> int", &gemv_addnorm_enable);
   m.def("attn_fused_max_pairs(int n) -> int", &attn_fused_max_pairs);
   m.def("car_mem_mode(int h) -> int", &car_mem_mode);
   m.def("car_destroy(int h) -> ()", &car_destroy);
@@ -802,6 +741,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("ep_destroy(int h) -> ()", &ep_destroy);
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
+  m.def("gemm_half_tile(int set=-1) -> int", &gemm_half_tile);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
   m.def("gemm_dense_plan(int variant, int bm, int bn, int splits) -> ()", &gemm_dense_plan);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
@@ -829,13 +769,7 @@ TORCH_LIBRARY(mlop, m) {
         "int epi) -> ()");
   m.def("gemm_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor a, Tensor w, Tensor norm_w, "
         "Tensor(c!) ws, float eps) -> bool");
-  m.def("gemm_norm_supported(int M, int N, int K, int epi) -> bool", &gemm_norm_supported);
   m.def("gemv_chain_supported(int M, int N, int K, int epi) -> bool", &gemv_chain_supported);
-  m.def("gemm_norm(Tensor(a!) out, Tensor(b!) res_out, Tensor y, Tensor res_in, Tensor norm_w, Tensor w, "
-        "float eps, int epi) -> bool");
-  m.def("gemm_norm_rope(Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor(d!) res_out, "
-        "Tensor y, Tensor res_in, Tensor norm_w, Tensor w, Tensor pos, Tensor cos_sin, Tensor slots, "
-        "float eps) -> bool");
   m.def("moe_route(Tensor(a!) topw, Tensor(b!) topi, Tensor logits) -> ()");
   m.def("moe_permute(Tensor(a!) xp, Tensor(b!) offsets, Tensor(c!) src, Tensor(d!) inv, Tensor x, "
         "Tensor topi, int e0, int n_local) -> ()");
@@ -877,8 +811,6 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("gemm_rs", &gemm_rs);
   m.impl("gemm_rs_rope", &gemm_rs_rope);
   m.impl("gemm_rope_cache", &gemm_rope_cache);
-  m.impl("gemm_norm", &gemm_norm);
-  m.impl("gemm_norm_rope", &gemm_norm_rope);
   m.impl("moe_route", &moe_route);
   m.impl("moe_dispatch_small", &moe_dispatch_small);
   m.impl("moe_combine_add_rmsnorm", &moe_combine_add_rmsnorm);

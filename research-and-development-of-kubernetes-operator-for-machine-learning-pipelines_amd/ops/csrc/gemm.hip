@@ -360,12 +360,7 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
                                m_tiles, splits, re);
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-static int g_small_stages = env_int("MLOP_GEMM_SMALL_STAGES", 3);
+static int g_small_stages = 3;
 int gemm_small_stages(int set) {
   if (set >= 0) g_small_stages = set;
   return g_small_stages;
@@ -377,20 +372,14 @@ int gemm_small_stages(int set) {
 // Default 64: M <= 32 cold projections 6-17 % faster than the 64 x 64 tile (qkv 18.3 -> 15.3 us,
 // o+norm 14.9 -> 12.9, gate_up 47.1 -> 45.6, down+norm 32.9 -> 27.3 at M = 16; BN 32 loses:
 // profiles/r02_midbatch_decode.md, scripts/run131.sh).  Run-time settable for A/B.
-static int g_small_tile = env_int("MLOP_GEMM_SMALL_TILE", 1);  // 1 = per-shape (plan); 64 x 64 for M 33-64
-// M 17-32 narrow projections on 32-column 8-deep tiles as at M <= 16: measured 1-2 % slower end
-// to end at batch 24 / 32 (scripts/run140.sh), off
-static const int g_small_bm32_narrow = env_int("MLOP_GEMM_BM32_NARROW", 0);
+static int g_small_tile = 1;  // 1 = per-shape (plan); 64 x 64 for M 33-64
 // ring depth of the grouped (MoE) 64-row tiles on narrow N (the down projection): 6 measured
 // neutral on Mixtral batch 32 / 64 (1,651 vs 1,655, 3,142 vs 3,134 tok/s, scripts/run141.sh)
-static const int g_grouped_small_stages = env_int("MLOP_GEMM_GROUPED_SMALL_STAGES", 3);
+constexpr int g_grouped_small_stages = 3;
 int gemm_small_tile(int set) {
   if (set >= 0) g_small_tile = set;
   return g_small_tile;
 }
-
-// round-4 planner rules (MLOP_GEMM_PLAN_R4=1): the same-box A/B of the round-5 tile choices
-static const int g_plan_r4 = env_int("MLOP_GEMM_PLAN_R4", 0);
 
 // grouped-plan override (scripts/bench_moe_decode.py compares MoE decode tilings in one process):
 // BM, BN, ring stages, K splits; -1 = the planner's own choice.  Only tile shapes launch_plan has
@@ -412,8 +401,8 @@ void gemm_grouped_plan(int bm, int bn, int stages, int splits) {
 // four-wave), BM, BN, K splits (plain gemm_kernel only); -1 = the planner's own choice
 static int g_dp[4] = {-1, -1, -1, -1};
 void gemm_dense_plan(int variant, int bm, int bn, int splits) {
-  if (variant >= 0 && variant != 0 && variant != 1 && variant != 3 && variant != 5)
-    throw std::runtime_error("gemm_dense_plan: variant must be 0, 1, 3 or 5");
+  if (variant >= 0 && variant != 0 && variant != 1 && variant != 3 && variant != 5 && variant != 6)
+    throw std::runtime_error("gemm_dense_plan: variant must be 0, 1, 3, 5 or 6");
   if (variant == 0) {
     static const int ok[][2] = {{64, 64}, {128, 64}, {256, 64}, {256, 128}};
     bool found = false;
@@ -423,12 +412,18 @@ void gemm_dense_plan(int variant, int bm, int bn, int splits) {
   g_dp[0] = variant, g_dp[1] = bm, g_dp[2] = bn, g_dp[3] = splits;
 }
 
-// large-M kernel choice (plan() variants below); MLOP_GEMM_BIG_VARIANT at load, and
-// settable at run time (gemm_big_variant op) so A/B microbenches run in one process
-static int g_big_variant = env_int("MLOP_GEMM_BIG_VARIANT", 5);
+// large-M kernel choice (plan() variants below), settable at run time (gemm_big_variant op) so
+// A/B microbenches run in one process
+static int g_big_variant = 5;
 int gemm_big_variant(int set) {
   if (set >= 0) g_big_variant = set;
   return g_big_variant;
+}
+// the planner's half-height four-wave tile (variant 6) on / off (gemm_half_tile op, A/B runs)
+static int g_half_tile = 1;
+int gemm_half_tile(int set) {
+  if (set >= 0) g_half_tile = set;
+  return g_half_tile;
 }
 
 // ---------------------------------------------------------------------------
@@ -868,9 +863,9 @@ struct SkBuf {
   int next = 0, cus = 0;
 };
 static SkBuf g_sk[16];
-static int g_sk_mode = env_int("MLOP_GEMM_SK", 1);
-static const int g_sk_min_iters = env_int("MLOP_GEMM_SK_MIN_ITERS", 16);
-static const int g_skip_dead = env_int("MLOP_GEMM_SKIP_DEAD", 1);
+static int g_sk_mode = 1;
+static const int g_sk_min_iters = 16;
+static const int g_skip_dead = 1;
 
 int gemm_sk_mode(int set) {
   if (set >= 0) g_sk_mode = set;
@@ -975,7 +970,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
     attr = true;
   }
   const int gx = (N + 255) / 256, gy = (M + 255) / 256 + (GROUPED ? n_groups : 0);
-  static const int group_m = env_int("MLOP_GEMM_PP_GROUP_M", 4);
+  constexpr int group_m = 4;
   const int gm = std::max(1, std::min(group_m, gy));
   int n_sk = 0;
   SkArgs sk = sk_plan(gx * gy, K / kBK, n_sk);
@@ -1036,7 +1031,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   // of the expert's weights) of the narrower kernels: Mixtral gate_up / down at 512 routed rows
   // 474 -> 370 / 266 -> 200 us, 1024 rows 692 -> 389 / 375 -> 208 us; 48 rows per expert equal
   // (scripts/bench_moe_decode.py, profiles/r05_moe_decode.md)
-  static const int pp_group_min_rows = g_plan_r4 ? 256 : 56;
+  constexpr int pp_group_min_rows = 56;
   if (grouped && mrows >= pp_group_min_rows && K % kBK == 0 && N % 256 == 0) {
     p.BM = 256; p.BN = 256; p.variant = 3;  // grouped ping-pong
   } else if (mrows <= 64 && !grouped && g_small_tile == 1) {
@@ -1045,7 +1040,9 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // 15.3 -> 13.5, o / down unchanged): more weight bytes in flight per CU
     p.BM = mrows <= 16 ? 16 : mrows <= 32 ? 32 : 64;
     p.BN = 64;
-    if (p.BM == 16 || (p.BM == 32 && g_small_bm32_narrow)) {
+    // (M 17-32 narrow projections on the 32-column 8-deep tiles of M <= 16: 1-2 % slower end to
+    // end at batch 24 / 32, scripts/history INDEX run140)
+    if (p.BM == 16) {
       const bool wide = N >= 16384;
       p.BN = wide ? 64 : 32;
       p.stages = wide ? (p.BM == 16 ? 6 : 0) : 8;
@@ -1065,19 +1062,19 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
   else if (mrows <= 256) {
-    static const int bn_min_tiles = env_int("MLOP_GEMM_BN128_MIN_TILES", 192);
+    constexpr int bn_min_tiles = 192;
     p.BM = 256;
     p.BN = ((N + 127) / 128 >= bn_min_tiles) ? 128 : 64;
   } else {
     const int big = g_big_variant;
-    static const int big_min_m = env_int("MLOP_GEMM_BIG_MIN_M", 1024);
+    constexpr int big_min_m = 1024;
     p.BM = 256;
     p.BN = 128;
     // 128: o / down at 2049-2816 rows (the mixed steps of batch ~512: 144-176 tiles, no K-half
     // tail for the four-wave kernel) ran on the 256 x 128 kernel at 0.55x hipBLASLt; the
     // ping-pong kernel's stream-K tail takes them (o at M = 2560: 122 -> 88 us, down 394 -> 269;
     // scripts/history/r4_m2560.sh)
-    static const int pp_min_tiles = env_int("MLOP_GEMM_PP_MIN_TILES", 128);
+    constexpr int pp_min_tiles = 128;
     const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
     // below pp_min_tiles the 256x256 grid leaves CUs idle, unless the stream-K tail can cut
     // every tile in two (T <= C / 2): o / down at M = 2040 (128 tiles)
@@ -1085,7 +1082,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // variant 5: the four-wave kernel where its grid fills the chip: >= w4_min_tiles tiles, or
     // a tail it can cut in K-halves (o / down at M = 2048: 128 tiles -> 256 half-tiles); else
     // the ping-pong kernel with its general stream-K tail
-    static const int w4_min_tiles = env_int("MLOP_GEMM_W4_MIN_TILES", 192);
+    constexpr int w4_min_tiles = 192;
     const bool w4_fills = t256 >= w4_min_tiles || gemm_w4_split_ok((int)t256, K / kBK);
     // Wide projections take the large-M kernels from 512 rows: gate_up / lm_head at M = 512 /
     // 768 ran 127 -> 87 / 191 -> 153 us (8B) and 511 -> 404 us (70B gate_up), batch-512 serving
@@ -1094,8 +1091,8 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     // Below ~72 tiles of 256 x 256 (o / down at M = 512 - 1024: 32 - 64 tiles) the 256 x 128
     // kernel beats them at every M measured short of 2048 (o at M = 1024: 44.7 vs 48.6 us, down
     // 114.7 vs 129.5); from 72 tiles (qkv at M = 768, 70B qkv at 512) the large-M kernels win.
-    static const int wide_min_m = env_int("MLOP_GEMM_BIG_WIDE_MIN_M", 512);
-    static const int mid_tiles = env_int("MLOP_GEMM_BIG_MID_TILES", 72);
+    constexpr int wide_min_m = 512;
+    constexpr int mid_tiles = 72;
     const int big_from = t256 >= mid_tiles ? std::min(big_min_m, wide_min_m) : std::max(big_min_m, 2048);
     if (big == 5 && !(mrows >= big_from && !grouped && w4_fills && gemm_w4_ok(M, N, K, K, K))) {
       if (mrows >= big_from && !grouped && pp_ok) { p.BN = 256; p.variant = 3; }
@@ -1103,7 +1100,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
       p.BN = 256;
       p.variant = big;
     }
-    if (!g_plan_r4 && !grouped && big == 5) {
+    if (!grouped && big == 5) {
       // long-K narrow projections (down, K = 14336) at 40-71 tiles of 256 x 256 (M 640-1279):
       // the ping-pong kernel's stream-K tail spreads the few tiles' K over every CU (down at
       // M = 768: 105 -> 90 us, 1024: 118 -> 108; hipBLASLt 90 / 111)
@@ -1125,11 +1122,29 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
         const float pp_est = 1.08f * (float)t256 / (float)C + 0.05f;
         if (pp_est < w4_est - 0.03f) p.variant = 3;
       }
+      // variant 6, the half-height (128 x 256) four-wave tile, where its grid is at most one
+      // round: up to twice the workgroups of the 256 x 256 grid (a lone tile of either height
+      // runs ~1.8x faster than one in a full round, so idle CUs cost more than the half tile's
+      // lower MFMA density).  bench_mid_m.py (profiles/r05_gemm_w4h.md), planner before -> after:
+      // o at M = 1024 / 1536 / 2048 46.2 -> 38.3 / 56.0 -> 47.6 / 65.6 -> 55.2 us, qkv at 384 /
+      // 512 / 1024 43.1 -> 33.1 / 44.4 -> 35.3 / 56.0 -> 47.5; past one round it loses to the
+      // full tile (qkv 1408: 75.9 vs 72.3).  Long K (down): only with its own K-half tail
+      // (t128 <= CUs / 2: 96 -> 256 items, M = 1024 110.8 -> 98.5); without it the full tile's
+      // K-halves win (M = 1152: 153.7 vs 131.1), and below ~80 tiles the 256 x 128 split-K kernel
+      // (M = 512: 83.1 vs 67.6).
+      const long t128 = (long)((M + 127) / 128) * ((N + 255) / 256);
+      const bool long_k = K >= 8192;
+      if (g_half_tile && b && mrows >= 384 && (long_k ? t128 >= 80 && 2 * t128 <= b->cus : t128 >= 64 && t128 <= b->cus) &&
+          (p.variant == 0 || p.variant == 3 || p.variant == 5) && gemm_w4_ok(M, N, K, K, K)) {
+        p.BM = 128;
+        p.BN = 256;
+        p.variant = 6;
+      }
     }
   }
   if (!grouped && g_dp[0] >= 0) {  // bench override (gemm_dense_plan)
     p.variant = g_dp[0];
-    p.BM = p.variant == 0 ? g_dp[1] : 256;
+    p.BM = p.variant == 0 ? g_dp[1] : p.variant == 6 ? 128 : 256;
     p.BN = p.variant == 0 ? g_dp[2] : 256;
     p.stages = 0;
   }
@@ -1145,9 +1160,9 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.splits = 1;
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
-  static const int split_target = env_int("MLOP_GEMM_SPLIT_TARGET", 256);  // run49: down -5..-15% at M 8-64
-  static const int split_max_tiles = env_int("MLOP_GEMM_SPLIT_MAX_TILES", 160);
-  if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3 && p.variant != 5) {
+  constexpr int split_target = 256;  // run49: down -5..-15% at M 8-64
+  constexpr int split_max_tiles = 160;
+  if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3 && p.variant < 5) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));
     int kc = ((K / s + kBK - 1) / kBK) * kBK;
     p.splits = (K + kc - 1) / kc;
@@ -1171,15 +1186,19 @@ static void launch_plan(const Plan& p, const uint16_t* A, int lda, const uint16_
                                                       p.m_tiles, st, re)
   if constexpr (EPI == EPI_ROPE) {  // whole heads per staged chunk, no split-K (launch_gemm_rope)
     if (p.BN == 128) MLOP_GEMM(256, 128, 4, 2, 3, false);
-    else if (!GROUPED && p.variant == 5 && gemm_w4_ok(M, N, K, lda, ldb, ldc)) run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re);
-    else if (!GROUPED && (p.variant == 3 || p.variant == 5)) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (!GROUPED && p.variant >= 5 && gemm_w4_ok(M, N, K, lda, ldb, ldc))
+      run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re, p.BM);
+    else if (!GROUPED && (p.variant == 3 || p.variant >= 5)) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
     else if (!GROUPED && p.variant == 2) MLOP_GEMM(256, 256, 2, 4, 2, true);
     else if (!GROUPED) MLOP_GEMM(256, 256, 2, 4, 2, false);
   } else {
     // weight-streaming tiles (M <= 128): a deeper LDS-DMA ring keeps more weight bytes in
     // flight per CU (3 stages x 16 KB per workgroup streamed gate_up at 4.7 TB/s at M = 64)
     const int sst = p.stages ? p.stages : g_small_stages;
-    if (p.BM == 16 && p.BN == 32 && sst >= 8) MLOP_GEMM(16, 32, 1, 2, 8, false);
+    if (!GROUPED && p.variant == 6 && p.splits == 1 && gemm_w4_ok(M, N, K, lda, ldb, ldc))
+      run_w4(EPI, A, lda, B, ldb, C, ldc, M, N, K, st, re, 128);
+    else if (!GROUPED && p.variant == 6) run_pp<EPI>(A, lda, B, ldb, C, ldc, M, N, K, st, re);
+    else if (p.BM == 16 && p.BN == 32 && sst >= 8) MLOP_GEMM(16, 32, 1, 2, 8, false);
     else if (p.BM == 16 && p.BN == 32 && sst >= 6) MLOP_GEMM(16, 32, 1, 2, 6, false);
     else if (p.BM == 16 && p.BN == 32) MLOP_GEMM(16, 32, 1, 2, 4, false);
     else if (p.BM == 16 && p.BN == 64 && sst >= 8) MLOP_GEMM(16, 64, 1, 2, 8, false);
@@ -1224,7 +1243,7 @@ int gemm_sk_workgroups(int M, int N, int K) {
 // fused into the RoPE + cache kernel (one launch instead of reduce + rope_cache).
 static bool rope_slabs_ok(const Plan& p, int M, int N) {
   const SkBuf* b = sk_buf();
-  return p.splits > 1 && p.variant != 3 && p.variant != 5 && b != nullptr &&
+  return p.splits > 1 && p.variant != 3 && p.variant < 5 && b != nullptr &&
          (size_t)p.splits * M * N <= (size_t)2 * kSkMaxWg * 256 * 256;
 }
 
@@ -1232,7 +1251,7 @@ bool gemm_rope_supported(int M, int N, int K) {
   if (M <= 0 || N % 128 || K % kBK) return false;
   if (gemv_takes(M, N, K, EPI_ROPE)) return true;  // decode M <= 8: gemv.hip
   const Plan p = plan(M, N, K, false, 0, 0);
-  return (p.BM == 256 && p.BN >= 128) || rope_slabs_ok(p, M, N);
+  return ((p.BM == 256 || p.variant == 6) && p.BN >= 128) || rope_slabs_ok(p, M, N);
 }
 
 bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
@@ -1244,7 +1263,7 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     return true;
   }
   Plan p = plan(M, N, K, false, 0, 0);
-  if (!(p.BM == 256 && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
+  if (!((p.BM == 256 || p.variant == 6) && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
     float* ws = sk_buf()->ws;
     launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
                                  M, N, K, nullptr, 0, st);
@@ -1264,20 +1283,22 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
 // Everything launch_w4_chain needs, so the caller decides the chain ONCE per forward (before the
 // first in-place residual update) and never meets a refusal mid-layer: the shape on the
 // four-wave kernel, the stream-K scratch that holds the band tickets reserved, and one ticket
-// per 256-row band.
+// per band of BM rows.
 bool w4_chain_ok(int M, int N, int K) {
   if (M <= 0 || gemv_takes(M, N, K, EPI_NONE) || gemv_takes(M, N, K, EPI_ROPE)) return false;
   int cus = 0;
-  if (!gemm_sk_available(&cus) || cus <= 0 || (M + 255) / 256 > kSkMaxWg) return false;
+  if (!gemm_sk_available(&cus) || cus <= 0) return false;
   const Plan p = plan(M, N, K, false, 0, 0);
-  return p.variant == 5 && p.splits == 1 && p.BM == 256 && p.BN == 256 && gemm_w4_ok(M, N, K, K, K, N);
+  return (p.variant == 5 || p.variant == 6) && p.splits == 1 && p.BN == 256 && (M + p.BM - 1) / p.BM <= kSkMaxWg &&
+         gemm_w4_ok(M, N, K, K, K, N);
 }
 
 bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K,
                      const RopeEpi& re, hipStream_t st) {
   if (M == 0) return true;
   if (!w4_chain_ok(M, N, K) || !gemm_w4_ok(M, N, K, lda, K, ldc)) return false;
-  if (!run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re)) return false;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  if (!run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re, p.BM)) return false;
   return true;
 }
 
@@ -1320,8 +1341,7 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              const void* w, float eps, float* ws, long ws_floats, int M, int N,
                              int K, hipStream_t st) {
   if (M == 0) return true;
-  if (gemv_takes(M, N, K, EPI_NONE))  // decode sizes: the GEMV's epilogue form (or false: GEMV + add_rmsnorm)
-    return launch_gemv_addnorm(A, lda, B, out, residual, w, eps, ws, ws_floats, M, N, K, st);
+  if (gemv_takes(M, N, K, EPI_NONE)) return false;  // decode sizes: GEMV + add_rmsnorm (or the norm chain)
   int splits;
   const Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
@@ -1361,7 +1381,7 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
   if (p.variant != 3 && K >= 2048 && g_gp[3] != 1) {
     const SkBuf* b = sk_buf();
     const long t_est = (long)((N + p.BN - 1) / p.BN) * std::max(1, std::min(n_groups, (M + p.BM - 1) / p.BM + n_groups));
-    static const int target = env_int("MLOP_GROUPED_SPLIT_TARGET", 1024);
+    constexpr int target = 1024;
     int s = (int)std::min<long>(8, std::max<long>(1, target / std::max<long>(1, t_est)));
     if (g_gp[3] > 1) s = g_gp[3];
     while (s > 1 && (K / s) % kBK) --s;

@@ -33,13 +33,9 @@
 // Prologue RS (the decode norm chain's QKV / gate_up, norm weights folded into B): A is the
 // raw residual; each row's sum of squares accumulates from the chunks the dots stream (one
 // v_dot2 per chunk, no extra load) and rsqrt(mean + eps) scales the finished sums.
-// Prologue NORM (the decoder's residual add + RMSNorm feeding this projection, one
-// launch fewer per norm): instead of loading A, every activation chunk is formed from
-// the previous projection's output y and the residual stream, r = bf16(res + y), and
-// x = bf16(r * norm_w); sum(r^2) accumulates beside the dots and the row's
-// rsqrt(mean(r^2) + eps) scales the finished sums (a per-row scalar commutes with the
-// dot; vs the unfused bf16(bf16(r * inv) * w) it skips one rounding).  The set-0 wave(s)
-// also store r to res_out (a different buffer than res_in: other waves still read it).
+// (Two rejected fusions were removed in round 5: a residual add + RMSNorm prologue that formed A
+// from y + residual, and an add + RMSNorm epilogue with a grid ticket.  Both measured slower
+// than the decode norm chain above: profiles/r04_decode_small_batch.md.)
 #include <stdlib.h>
 
 #include "common.h"
@@ -49,11 +45,11 @@ namespace mlop {
 
 namespace {
 
-enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3, EPI_ADDNORM = 4, EPI_RES = 5 };
-// prologues: none; NORM (residual add + RMSNorm of y and res_in, see above); RS (the row-scale
-// chain: A IS the raw residual and the norm weights are folded into B, so the rows'
-// rsqrt(mean(a^2) + eps) comes from the very chunks the dots stream: no extra load at all)
-enum { PRO_NONE = 0, PRO_NORM = 1, PRO_RS = 2 };
+enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3, EPI_RES = 5 };
+// prologues: none; RS (the row-scale chain: A IS the raw residual and the norm weights are
+// folded into B, so the rows' rsqrt(mean(a^2) + eps) comes from the very chunks the dots
+// stream: no extra load at all)
+enum { PRO_NONE = 0, PRO_RS = 2 };
 constexpr int kHeadD = 128;
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
@@ -94,7 +90,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                                                    uint16_t* __restrict__ C, int ldc, int N, int K,
                                                    RopeEpi re, NormPro np, GroupArgs ga = GroupArgs{}) {
   constexpr int R = 2 * RP;  // weight rows per wave
-  constexpr bool NORM = PRO == PRO_NORM, RS = PRO == PRO_RS;
+  constexpr bool RS = PRO == PRO_RS;
   static_assert(EPI != EPI_ROPE || RP == 1, "rope sets are single row pairs");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // row set: KW == 1 -> one per wave; KW == 4 -> one per workgroup (its waves split K)
@@ -156,10 +152,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-  float ss[M];  // NORM / RS: sum of r^2 over this lane's chunks
+  float ss[M];  // RS: sum of a^2 over this lane's chunks
 #pragma unroll
   for (int m = 0; m < M; ++m) ss[m] = 0.f;
-  const bool writer = NORM && (KW == 1 ? set == 0 : blockIdx.x == 0);
 
   // EPI_ROPE: the epilogue's per-row slot, position and the position's cos / sin are loaded
   // right after the first weight loads are issued, so their round trips (position -> cos / sin
@@ -184,29 +179,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       const bool ok = c < KC;
 #pragma unroll
       for (int r = 0; r < R; ++r) w[u][r] = ok ? __builtin_nontemporal_load(Bv[r] + c) : u32x4{0, 0, 0, 0};
-      if constexpr (NORM) {
-        const u32x4 wn = ok ? reinterpret_cast<const u32x4*>(np.w)[c] : u32x4{0, 0, 0, 0};
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          u32x4 rr = u32x4{0, 0, 0, 0};
-          if (ok) {
-            const u32x4 ya = reinterpret_cast<const u32x4*>(np.y + (size_t)m * K)[c];
-            const u32x4 ra = reinterpret_cast<const u32x4*>(np.res_in + (size_t)m * K)[c];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) rr[j] = pack2(lo_bf(ya[j]) + lo_bf(ra[j]), hi_bf(ya[j]) + hi_bf(ra[j]));
-            if (writer) reinterpret_cast<u32x4*>(np.res_out + (size_t)m * K)[c] = rr;
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float a0 = lo_bf(rr[j]), a1 = hi_bf(rr[j]);
-            ss[m] += a0 * a0 + a1 * a1;
-            x[u][m][j] = pack2(a0 * lo_bf(wn[j]), a1 * hi_bf(wn[j]));
-          }
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < M; ++m) x[u][m] = (ok && m < mc) ? Av[m][c] : u32x4{0, 0, 0, 0};
-      }
+      for (int m = 0; m < M; ++m) x[u][m] = (ok && m < mc) ? Av[m][c] : u32x4{0, 0, 0, 0};
     }
     if constexpr (EPI == EPI_RES) {
       if (c0 == 0 && res_lane) res_pf = C[(size_t)(lane / R) * ldc + set * R + lane % R];  // behind the weights
@@ -239,36 +213,36 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
-  if constexpr (NORM || RS) {
+  if constexpr (RS) {
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = wave_sum(ss[m]);
   }
 
   if constexpr (KW > 1) {
-    constexpr int NV = R * M + ((NORM || RS) ? M : 0);
+    constexpr int NV = R * M + (RS ? M : 0);
     __shared__ float red[KW][NV];
     if (lane == 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m) red[wv][r * M + m] = acc[r][m];
-      if constexpr (NORM || RS) {
+      if constexpr (RS) {
 #pragma unroll
         for (int m = 0; m < M; ++m) red[wv][R * M + m] = ss[m];
       }
     }
     __syncthreads();
-    if (EPI != EPI_ADDNORM && wv != 0) return;  // ADDNORM: every wave joins the grid ticket below
+    if (wv != 0) return;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       float t = 0.f;
 #pragma unroll
       for (int k = 0; k < KW; ++k) t += red[k][i];
       if (i < R * M) acc[i / M][i % M] = t;
-      else if constexpr (NORM || RS) ss[i - R * M] = t;
+      else if constexpr (RS) ss[i - R * M] = t;
     }
   }
-  if constexpr (NORM || RS) {
+  if constexpr (RS) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const float inv = rsqrtf(ss[m] / (float)K + np.eps);
@@ -321,99 +295,6 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
       const int m = lane / R, r = lane % R;
       C[(size_t)m * ldc + set * R + r] = f2bf(bf2f(res_pf) + bf2f(f2bf(acc_pick(acc, r, m))));
     }
-  } else if constexpr (EPI == EPI_ADDNORM) {
-    // Epilogue form of the decoder's residual add + RMSNorm (the norm AFTER this projection,
-    // fused into its launch): lane m*R + r owns output (m, set*R + r):
-    //   residual = bf16(residual + bf16(y)) (in place: read by later launches only) and the same
-    //   values into a scratch copy, the set's row partial of squares into the partials;
-    // then the grid hand-off of MI355X_MICROARCH.md "Valid forms" table row 1 (no L2 write-back
-    // fence per workgroup: 2048 of them cost ~60 us per launch): every handed-off byte is stored
-    // sc1 (4- / 8-B scratch words, 4-B partials) into scratch no workgroup of this launch read
-    // before, every storing wave drains (vmcnt(0)), a barrier, ONE lane's relaxed agent-scope
-    // ticket; the workgroup whose add returned last loads the partials and the scratch residual
-    // with sc1 loads only, sums each row's partials in a FIXED order (deterministic) and writes
-    // out = bf16(bf16(residual * rsqrt(mean + eps)) * w) for all M rows (norm.hip's rounding).
-    // Writer waves: every wave (KW == 1: 4 sets per workgroup) or wave 0 (KW > 1: one set).
-    __shared__ float s_red[16];
-    __shared__ int s_last;
-    const bool wwave = KW == 1 || wv == 0;
-    const int nsets = N / R;
-    float* part = np.part;                               // [nsets, M] fp32
-    uint16_t* rsc = reinterpret_cast<uint16_t*>(np.part + (size_t)nsets * M);  // [M, N] bf16 copy
-    const auto rs_part = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)((uint32_t)nsets * M * 4u), 0x00020000);
-    const auto rs_rsc = __builtin_amdgcn_make_buffer_rsrc(rsc, 0, (int)((uint32_t)M * N * 2u), 0x00020000);
-    if (wwave) {
-      float sq = 0.f;
-      uint32_t rb = 0;
-      const int m = lane / R, r = lane % R;
-      if (lane < M * R) {
-        uint16_t* rp = np.res_out + (size_t)m * ldc + set * R + r;
-        const uint16_t nb = f2bf(bf2f(*rp) + bf2f(f2bf(acc_pick(acc, r, m))));
-        *rp = nb;
-        const float rn = bf2f(nb);
-        sq = rn * rn;
-        rb = nb;
-      }
-      // the row's R adjacent values and their squares gather in lane m*R (R = 2 or 4, adjacent lanes)
-#pragma unroll
-      for (int o = 1; o < R; o <<= 1) sq += __shfl_xor(sq, o, 64);
-      // every lane shuffles (no inactive source lanes), lane m*R stores
-      const uint32_t r1 = __shfl_down(rb, 1, 64);
-      const uint32_t r2 = R == 4 ? __shfl_down(rb, 2, 64) : 0u, r3 = R == 4 ? __shfl_down(rb, 3, 64) : 0u;
-      if (lane < M * R && r == 0) {
-        const uint32_t off = (uint32_t)(m * N + set * R) * 2u;
-        if constexpr (R == 2)
-          __builtin_amdgcn_raw_buffer_store_b32(rb | (r1 << 16), rs_rsc, off, 0, 16 /* sc1 */);
-        else
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2{rb | (r1 << 16), r2 | (r3 << 16)}, rs_rsc, off, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq), rs_part, (uint32_t)(set * M + m) * 4u, 0, 16);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // two-level ticket: one counter serialises its adds (~10 ns each at the memory side, so
-      // 2048 workgroups on ONE counter cost ~20 us per launch); 16 shards on their own 32-B
-      // words take the adds in parallel and the last of each shard adds to the top counter.
-      // Every add follows its workgroup's drained sc1 stores, so whoever sees the final count
-      // sees every workgroup's bytes in memory.
-      constexpr int kShards = 16, kStride = 8;
-      const int G = gridDim.x, sh = blockIdx.x % kShards;
-      const int in_shard = (G - sh + kShards - 1) / kShards;  // workgroups of shard sh
-      const int nsh = G < kShards ? G : kShards;
-      int* sc = np.cnt + sh * kStride;
-      int* top = np.cnt + kShards * kStride;
-      int last = 0;
-      const int t1 = __hip_atomic_fetch_add(sc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t1 == in_shard - 1) {
-        __hip_atomic_store(sc, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
-        const int t2 = __hip_atomic_fetch_add(top, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t2 == nsh - 1) {
-          __hip_atomic_store(top, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          last = 1;
-        }
-      }
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    for (int m = 0; m < M; ++m) {
-      float t = 0.f;
-      for (int sidx = threadIdx.x; sidx < nsets; sidx += blockDim.x)
-        t += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_part, (uint32_t)(sidx * M + m) * 4u, 0, 16));
-      t = block_sum(t, s_red);
-      const float inv = rsqrtf(t / (float)N + np.eps);
-      for (int c = threadIdx.x * 8; c < N; c += blockDim.x * 8) {
-        const u32x4 rv = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_rsc, (uint32_t)(m * N + c) * 2u, 0, 16 /* sc1 */));
-        const u32x4 wv8 = *reinterpret_cast<const u32x4*>(np.w + c);
-        u32x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          o[q] = pack2(bf2f(f2bf(lo_bf(rv[q]) * inv)) * lo_bf(wv8[q]), bf2f(f2bf(hi_bf(rv[q]) * inv)) * hi_bf(wv8[q]));
-        *reinterpret_cast<u32x4*>(C + (size_t)m * ldc + c) = o;
-      }
-    }
   } else {
 #pragma unroll
     for (int m = 0; m < M; ++m)
@@ -423,28 +304,18 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   }
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 int gemv_max_m() {
-  // measured (scripts/run38.sh): the GEMV wins every decode projection at M <= 4 in the
-  // running model; at M = 8 the 64-row MFMA tiles stream gate_up / down faster
-  static const int max_m = std::min(8, env_int("MLOP_GEMV_MAX_M", 4));
-  return max_m;
+  // measured (scripts/history INDEX run38): the GEMV wins every decode projection at M <= 4 in
+  // the running model; at M = 8 the 64-row MFMA tiles stream gate_up / down faster
+  return 4;
 }
 
 // below this many row sets a workgroup's 4 waves share rows and split K (KW = 4): more loads
 // in flight per row.  Measured at batch-1/2/4 decode (scripts/run56.sh, run57.sh): at M <= 2
 // moving gate_up (7168 sets) to KW = 4 gives +3-4% tok/s at batch 1 and +1.5% at batch 2, at
 // M = 4 it loses 5% (the dot work per loaded byte grows with M), and o / qkv / down (2048-3072
-// sets) do not move.  MLOP_GEMV_KW4_SETS, when set, overrides both defaults; an explicit 0
-// disables KW = 4 everywhere (no launch has fewer than 0 sets).
-int gemv_kw4_sets(int M) {
-  static const int v = env_int("MLOP_GEMV_KW4_SETS", -1);
-  return v >= 0 ? v : (M <= 2 ? 8192 : 2048);
-}
+// sets) do not move.
+int gemv_kw4_sets(int M) { return M <= 2 ? 8192 : 2048; }
 
 template <int M, int EPI, int PRO>
 void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int N,
@@ -454,9 +325,8 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
   const int pairs = N / 2;
   const int rp = (EPI != EPI_ROPE && pairs / 2 >= 2048) ? 2 : 1;
   const int sets = pairs / rp;
-  // ADDNORM: one set per wave (4 per workgroup) keeps the grid ticket to N / 8 workgroups; the
-  // K-split form is for gate_up-size shards, o / down stream as fast without it (run56.sh)
-  const bool kw4 = EPI != EPI_ADDNORM && sets < gemv_kw4_sets(M);
+  // the K-split form is for gate_up-size shards, o / down stream as fast without it (run56)
+  const bool kw4 = sets < gemv_kw4_sets(M);
 #define MLOP_GEMV(RP, KW)                                                                          \
   do {                                                                                             \
     const int blocks = KW == 1 ? cdiv(sets, 4) : sets;                                             \
@@ -478,14 +348,7 @@ void run_gemv_m(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t
 template <int EPI, int PRO = PRO_NONE>
 void run_gemv(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M,
               int N, int K, const RopeEpi& re, hipStream_t st, const NormPro& np = NormPro{}) {
-  if constexpr (PRO == PRO_NORM) {  // the fused-norm prologue: decode sizes only (M <= 4)
-    switch (M) {
-      case 1: run_gemv_m<1, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      case 2: run_gemv_m<2, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      case 3: run_gemv_m<3, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-      default: run_gemv_m<4, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
-    }
-  } else {
+  {
     switch (M) {
       case 1: run_gemv_m<1, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
       case 2: run_gemv_m<2, EPI, PRO>(A, lda, B, ldb, C, ldc, N, K, re, np, st); break;
@@ -550,10 +413,9 @@ void run_gemv_grouped_m(const uint16_t* A, const uint16_t* B, uint16_t* C, int l
 #undef MLOP_GEMV_G
 }
 
-// MoE expert GEMMs at decode: M = routed rows in total (<= MLOP_GEMV_GROUPED_MAX_M, default 8)
+// MoE expert GEMMs at decode: M = routed rows in total (<= 8)
 bool gemv_grouped_takes(int M, int N, int K, int epi) {
-  static const int max_m = std::min(8, env_int("MLOP_GEMV_GROUPED_MAX_M", 8));
-  return M >= 1 && M <= max_m && K % 8 == 0 && N % (epi == EPI_SILU_MUL ? 32 : 4) == 0 &&
+  return M >= 1 && M <= 8 && K % 8 == 0 && N % (epi == EPI_SILU_MUL ? 32 : 4) == 0 &&
          (epi == EPI_NONE || epi == EPI_SILU_MUL);
 }
 
@@ -575,80 +437,16 @@ void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offse
 #undef MLOP_GG
 }
 
-// The epilogue form: residual add + RMSNorm fused into the projection that PRODUCES the
-// residual update (O, down), so the batch-1..4 decode step loses its 64 separate add_rmsnorm
-// launches (~4.7 us each, profiles/r01_decode_small_batch.md) for one small tail per launch.
-// measured (scripts/history/r4_b1.sh, profiles/r04_decode_small_batch.md): the fused tail costs
-// what the separate norm launch did (its three dependent round trips + the grid ticket ~= the
-// norm kernel's latency), batch 1 329 vs 351 tok/s, batch 4 952 vs 1090: off by default
-// (MLOP_GEMV_ADDNORM=1, or gemv_addnorm_enable() in-process: the GPU tests keep it verified)
-static int g_gemv_addnorm = -1;
-int gemv_addnorm_enable(int on) {
-  if (g_gemv_addnorm < 0) g_gemv_addnorm = env_int("MLOP_GEMV_ADDNORM", 0);
-  const int prev = g_gemv_addnorm;
-  if (on >= 0) g_gemv_addnorm = on ? 1 : 0;
-  return prev;
-}
-
-long gemv_addnorm_ws_floats(int M, int N, int K) {
-  // whole row sets in every wave of every workgroup (the grid ticket needs no early exits)
-  if (!gemv_addnorm_enable(-1) || !gemv_takes(M, N, K, EPI_NONE) || M > 4 || N % 16 || N > 16384) return 0;
-  return (long)(N / 2) * M + (long)(N / 2) * M;  // partials (>= sets x M, R = 2 or 4) + the bf16 residual copy
-}
-
-bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
-                         float* ws, long ws_floats, int M, int N, int K, hipStream_t st) {
-  if (gemv_addnorm_ws_floats(M, N, K) == 0 || ws_floats < gemv_addnorm_ws_floats(M, N, K)) return false;
-  float* wsk = nullptr;
-  int* cnt = nullptr;
-  int cus = 0;
-  if (!gemm_sk_scratch(&wsk, &cnt, &cus)) return false;  // the ticket counter lives there
-  NormPro np{nullptr, nullptr, (uint16_t*)residual, (const uint16_t*)w, eps, ws, cnt};
-  const RopeEpi none{};
-  auto* a = (const uint16_t*)A;
-  auto* b = (const uint16_t*)B;
-  auto* o = (uint16_t*)out;
-  switch (M) {
-    case 1: run_gemv_m<1, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    case 2: run_gemv_m<2, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    case 3: run_gemv_m<3, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
-    default: run_gemv_m<4, EPI_ADDNORM, PRO_NONE>(a, lda, b, K, o, N, N, K, none, np, st); break;
-  }
-  return true;
-}
-
-// residual add + RMSNorm fused into the projection that consumes it (prologue NORM):
-// C = epi(rmsnorm(res_in + y) @ B^T), res_out = bf16(res_in + y); M <= 4 only.
-// Each wave re-forms the normed activations of every K chunk it streams, so the prologue's
-// VALU work grows with M: measured (scripts/run40.sh) it pays at M = 1 (-5 us per layer) and
-// loses at M = 2 / 4 (gate_up turns VALU-bound); MLOP_NORM_FUSION_MAX_M (default 1, max 4).
-bool gemv_norm_takes(int M, int N, int K, int epi) {
-  static const int max_m = std::min(4, env_int("MLOP_NORM_FUSION_MAX_M", 1));
-  return M <= max_m && gemv_takes(M, N, K, epi);
-}
-
-void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M, int N, int K, int epi,
-                      const RopeEpi& re, hipStream_t st) {
-  auto* b = (const uint16_t*)B;
-  auto* c = (uint16_t*)C;
-  if (epi == EPI_SILU_MUL) run_gemv<EPI_SILU_MUL, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
-  else if (epi == EPI_ROPE) run_gemv<EPI_ROPE, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
-  else run_gemv<EPI_NONE, PRO_NORM>(nullptr, K, b, K, c, ldc, M, N, K, re, st, np);
-}
-
 // The decode norm chain (M <= gemv_chain_max_m(), norm weights folded into the consuming projections:
 // LlamaModel.fold_norms): O and down add their output into the residual in place (EPI_RES),
 // QKV and gate_up read the raw residual and scale each row's sums by rsqrt(mean(a^2) + eps)
 // taken from the chunks they stream anyway (PRO_RS).  A decode layer is then five launches
 // and no add + RMSNorm pass: the GEMV form of gemm_w4.hip's large-M chain (W4_ADD_SS / W4_RS).
-// rows the chain's GEMV form takes (MLOP_GEMV_CHAIN_MAX_M, default 4, at most 8; above
-// gemv_max_m() the GEMV takes nothing anyway).  Measured (scripts/history/r4_chain8.sh): the
-// GEMV with the chain at 6 / 8 rows streams 1,419 / 1,612 tok/s against the MFMA path's
-// 1,522 / 1,936 (its split-K reduce already carries the add + RMSNorm), so 4 stays.
-int gemv_chain_max_m() {
-  static const int v = std::min(8, std::max(1, env_int("MLOP_GEMV_CHAIN_MAX_M", 4)));
-  return v;
-}
+// rows the chain's GEMV form takes (above gemv_max_m() the GEMV takes nothing anyway).
+// Measured (scripts/history INDEX r4_chain8): the GEMV with the chain at 6 / 8 rows streams
+// 1,419 / 1,612 tok/s against the MFMA path's 1,522 / 1,936 (its split-K reduce already
+// carries the add + RMSNorm), so 4 stays.
+int gemv_chain_max_m() { return 4; }
 
 bool gemv_chain_takes(int M, int N, int K, int epi) {
   return M <= gemv_chain_max_m() && gemv_takes(M, N, K, epi);

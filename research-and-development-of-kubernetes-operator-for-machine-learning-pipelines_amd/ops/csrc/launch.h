@@ -62,16 +62,18 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // large-M kernel variant of the GEMM planner (gemm.hip plan(): 0 256x128, 1/2 256x256
 // 8-wave, 3 ping-pong, 5 four-wave asm K-loop); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
+int gemm_half_tile(int set);
 void gemm_grouped_plan(int bm, int bn, int stages, int splits);
 void gemm_dense_plan(int variant, int bm, int bn, int splits);
-// variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip); epi 0 / 1 / 3
+// variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip), variant 6 its 128x256
+// half-height tile; epi 0 / 1 / 3
 bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
 // the four-wave kernel cuts its r = T % CUs tail tiles into K-halves (2r <= CUs, nk even)
 bool gemm_w4_split_ok(int T, int nk);
 bool gemm_sk_scratch(float** ws, int** cnt, int* cus);
 bool gemm_sk_available(int* cus);
 bool run_w4(int epi, const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N,
-            int K, hipStream_t st, const RopeEpi& re);
+            int K, hipStream_t st, const RopeEpi& re, int bm = 256);
 // norm chain on the four-wave kernel (epi flags: 4 = C += A.B^T with ss partials, 8 = rows scaled
 // by re.ss_in; 4, 0|8, 1|8, 3|8 are built): true when every such GEMM of this shape runs there
 bool w4_chain_ok(int M, int N, int K);
@@ -90,25 +92,10 @@ void launch_gemv(const void* A, int lda, const void* B, int ldb, void* C, int ld
                  int epi, hipStream_t st);
 void launch_gemv_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st);
-// residual add + RMSNorm prologue (gemv.hip NORM): rows of y / res_in / res_out are K wide
+// the decode norm chain's row-scale prologue parameters (gemv.hip PRO_RS)
 struct NormPro {
-  const uint16_t* y;
-  const uint16_t* res_in;
-  uint16_t* res_out;
-  const uint16_t* w;
-  float eps;
-  float* part = nullptr;  // epilogue form (launch_gemv_addnorm): per-(set, row) partial sums of squares
-  int* cnt = nullptr;     // epilogue form: the grid ticket
+  float eps = 0.f;
 };
-// decode projection with the residual add + RMSNorm AFTER it in the same launch (gemv.hip
-// epilogue form, M <= 4): residual <- bf16(residual + bf16(A.B^T)); out <- rmsnorm(residual) * w.
-// ws: gemv_addnorm_ws_floats(M, N, K) floats; false = shape not on this path.
-long gemv_addnorm_ws_floats(int M, int N, int K);
-// the epilogue's opt-in switch: on = 0 / 1 sets it, -1 queries; returns the previous state
-int gemv_addnorm_enable(int on);
-bool launch_gemv_addnorm(const void* A, int lda, const void* B, void* out, void* residual, const void* w, float eps,
-                         float* ws, long ws_floats, int M, int N, int K, hipStream_t st);
-bool gemv_norm_takes(int M, int N, int K, int epi);
 // decode norm chain (gemv.hip PRO_RS / EPI_RES, M <= 4): C = epi(rowscale(A) . B^T) with
 // rowscale = rsqrt(mean(A_row^2) + eps) (norm weights folded into B); residual += A . B^T
 bool gemv_chain_takes(int M, int N, int K, int epi);
@@ -119,8 +106,6 @@ void launch_gemv_res(const void* A, int lda, const void* B, void* residual, int 
 bool gemv_grouped_takes(int M, int N, int K, int epi);
 void launch_gemv_grouped(const void* A, const void* B, void* C, const int* offsets, int n_groups, int M, int N,
                          int K, int epi, hipStream_t st);
-void launch_gemv_norm(const NormPro& np, const void* B, void* C, int ldc, int M, int N, int K, int epi,
-                      const RopeEpi& re, hipStream_t st);
 bool gemm_rope_supported(int M, int N, int K);
 bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K, const RopeEpi& re,
                       hipStream_t st);

@@ -132,16 +132,14 @@ __global__ void __launch_bounds__(256) rmsnorm_wave_kernel(uint16_t* __restrict_
   }
 }
 
-// fewer rows: the block form's 8-wave fan-out per row wins (MLOP_NORM_WAVE_MIN_M: A/B; at batch 1
-// the wave form measured 345 vs 351 tok/s, scripts/history/r4_norm1.sh)
+// fewer rows: the block form's 8-wave fan-out per row wins (at batch 1 the wave form measured
+// 345 vs 351 tok/s, scripts/history INDEX r4_norm1)
 constexpr int kWaveRowsMinM = 256;
 
 template <bool ADD>
 static bool dispatch_wave(uint16_t* out, uint16_t* residual, const uint16_t* x, const uint16_t* w,
                           float eps, int M, int H, hipStream_t st) {
-  static const bool on = !getenv("MLOP_NORM_WAVE") || atoi(getenv("MLOP_NORM_WAVE")) != 0;
-  static const int min_m = getenv("MLOP_NORM_WAVE_MIN_M") ? atoi(getenv("MLOP_NORM_WAVE_MIN_M")) : kWaveRowsMinM;
-  if (!on || M < min_m || H % 512) return false;
+  if (M < kWaveRowsMinM || H % 512) return false;
   const int g = cdiv(M, 4);
   switch (H / 512) {
     case 1: rmsnorm_wave_kernel<1, ADD><<<g, 256, 0, st>>>(out, residual, x, w, eps, M, H); return true;

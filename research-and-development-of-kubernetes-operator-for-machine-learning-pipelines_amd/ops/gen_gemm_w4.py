@@ -38,6 +38,14 @@ Hazards handled in the text (hipcc pads nothing inside an asm statement):
   * v_accvgpr_write (zeroing) -> first MFMA: the prologue's barrier + reads lie between;
   * last MFMA -> v_accvgpr_read (readout statements): 3 x s_nop 7 at the end.
 
+Half-height variant (BM = 128, round 5): the same schedule shape over 64 MFMAs per K-tile --
+each wave owns 64 x 128 outputs (4 x 8 accumulators, 128 AGPRs), the A operand is 128 rows
+(4 fragments per k-half, 4 of the 12 LDS-DMA pieces per wave), so a grid has twice the tiles
+(QKV at M = 4088: 768 tiles = 3 whole rounds of the 256 CUs instead of 1.5; O at 1536-2560 rows
+one full round instead of K-half tails).  Slots: rd1 at 1..12, B1 at 20 (8 MFMAs of slack for
+the reads' return), 12 DMAs at 21..43, B2 at 45, rd0 at 46..57 (6 MFMAs of slack before the next
+K-tile's first MFMA); the fragment-reuse distance (>= 8 MFMAs) holds as in the full tile.
+
 Run ``python -m mlopamd.ops.gen_gemm_w4`` to regenerate the header (committed; the build
 does not run Python).
 """
@@ -47,18 +55,26 @@ from pathlib import Path
 
 OUT = Path(__file__).resolve().parent / "csrc" / "gemm_w4_asm.h"
 
-NF = 8            # fragments per operand per k-half (8 x 16 rows / cols)
-LOOPCTL_SLOT = 127
+NFB = 8           # B fragments per k-half (8 x 16 columns: the wave's 128 columns)
 
 
 class Sched:
-    """Slot placement of one K-tile iteration (slot m = before MFMA m)."""
+    """Slot placement of one K-tile iteration (slot m = before MFMA m) for a tile of ``bm`` rows:
+    ``nfa`` = bm / 32 A fragments per wave and k-half, ``na`` = bm / 32 A pieces of the ``npc``
+    LDS-DMA pieces per wave, ``nmma`` MFMAs per K-tile."""
 
-    def __init__(self, rd1, b1, dma, b2, rd0, toggle1=60, pol_a="", pol_b=""):
+    def __init__(self, rd1, b1, dma, b2, rd0, toggle1=60, pol_a="", pol_b="", bm=256):
         self.rd1, self.b1, self.dma, self.b2, self.rd0, self.toggle1 = rd1, b1, dma, b2, rd0, toggle1
         self.pol = {"srdA": pol_a, "srdB": pol_b}  # cache-policy bits of each operand's LDS-DMA
-        assert len(rd1) == 16 and len(rd0) == 16 and len(dma) == 16
-        assert max(rd1) < b1 < min(dma) and b2 < min(rd0) and max(rd0) <= 127 and toggle1 > max(rd1)
+        self.bm = bm
+        self.nfa = bm // 32
+        self.na = bm // 32
+        self.npc = self.na + 8
+        self.nmma = 2 * self.nfa * NFB
+        self.loopctl = self.nmma - 1
+        nrd = NFB + self.nfa
+        assert len(rd1) == nrd and len(rd0) == nrd and len(dma) == self.npc
+        assert max(rd1) < b1 < min(dma) and b2 < min(rd0) and max(rd0) <= self.nmma - 1 and toggle1 > max(rd1)
         self.dma_before_b2 = sum(1 for m in dma if m < b2)
 
 
@@ -68,6 +84,9 @@ class Sched:
 # non-temporal weight / activation DMAs (2-8 % slower).
 SCHEDS = [Sched(rd1=[1 + 2 * k for k in range(16)], b1=38, dma=[40 + 4 * k for k in range(16)], b2=102,
                 rd0=[103 + round(k * 24 / 15) for k in range(16)])]
+# the half-height tile (BM = 128): 64 MFMAs, 12 fragment reads per k-half, 12 DMA pieces
+SCHED_H = Sched(rd1=[1 + k for k in range(12)], b1=20, dma=[21 + 2 * k for k in range(12)], b2=45,
+                rd0=[46 + k for k in range(12)], toggle1=19, bm=128)
 
 
 def frag(name, i):
@@ -113,14 +132,13 @@ class Stream:
         self.queue = []
 
 
-def reads_k1(s: Stream):
+def reads_k1(sc: Sched):
     """ds_reads of the k-half-1 fragments (FB1 then FA1) of the current tile."""
-    ops = [(("fb1_", j), "rB1", j * 2048) for j in range(NF)] + [(("fa1_", i), "rA1", i * 2048) for i in range(NF)]
-    return ops
+    return [(("fb1_", j), "rB1", j * 2048) for j in range(NFB)] + [(("fa1_", i), "rA1", i * 2048) for i in range(sc.nfa)]
 
 
-def reads_k0():
-    return [(("fb0_", j), "rB0", j * 2048) for j in range(NF)] + [(("fa0_", i), "rA0", i * 2048) for i in range(NF)]
+def reads_k0(sc: Sched):
+    return [(("fb0_", j), "rB0", j * 2048) for j in range(NFB)] + [(("fa0_", i), "rA0", i * 2048) for i in range(sc.nfa)]
 
 
 def body(s: Stream, sc: Sched, kind: str, first: bool = False):
@@ -128,16 +146,17 @@ def body(s: Stream, sc: Sched, kind: str, first: bool = False):
     first: the tile's K-tile 0 -- the H0 MFMAs start the accumulators from 0 (no zeroing pass)."""
     dma = kind == "steady"
     nxt = kind != "last"
-    slots: dict[int, list] = {m: [] for m in range(129)}
-    for m, op in zip(sc.rd1, reads_k1(s)):
+    NM = sc.nmma
+    slots: dict[int, list] = {m: [] for m in range(NM + 1)}
+    for m, op in zip(sc.rd1, reads_k1(sc)):
         slots[m].append(("read", op))
     if dma:
         slots[sc.b1].append(("b1",))
         slots[sc.dma[0] - 1].append(("emit", "s_mov_b32 m0, %[dbase]"))
         for k, m in enumerate(sc.dma):
-            srd = "srdA" if k < 8 else "srdB"
+            srd = "srdA" if k < sc.na else "srdB"
             slots[m].append(("emit", f"buffer_load_dwordx4 %[vo{k}], %[{srd}], %[koff] offen{sc.pol[srd]} lds"))
-            if k < 15:
+            if k < sc.npc - 1:
                 slots[m].append(("emit", "s_add_u32 m0, m0, 0x1000"))
         slots[sc.dma[-1] + 1].append(("emit", "s_add_u32 %[koff], %[koff], 0x80"))
         slots[sc.dma[-1] + 1].append(("emit", "s_xor_b32 %[dbase], %[dbase], 0x10000"))
@@ -147,12 +166,12 @@ def body(s: Stream, sc: Sched, kind: str, first: bool = False):
         slots[sc.b2].append(("b2", sc.dma_before_b2 if dma else 0))
         slots[sc.b2].append(("emit", "v_xor_b32_e32 %[rA0], 0x10000, %[rA0]"))
         slots[sc.b2].append(("emit", "v_xor_b32_e32 %[rB0], 0x10000, %[rB0]"))
-        for m, op in zip(sc.rd0, reads_k0()):
+        for m, op in zip(sc.rd0, reads_k0(sc)):
             slots[m].append(("read", op))
     if kind == "steady" and not first:
-        slots[LOOPCTL_SLOT].append(("emit", "s_sub_u32 %[iter], %[iter], 1"))
-        slots[LOOPCTL_SLOT].append(("emit", "s_cmp_lg_u32 %[iter], 0"))
-    for m in range(129):
+        slots[sc.loopctl].append(("emit", "s_sub_u32 %[iter], %[iter], 1"))
+        slots[sc.loopctl].append(("emit", "s_cmp_lg_u32 %[iter], 0"))
+    for m in range(NM + 1):
         for op in slots[m]:
             if op[0] == "read":
                 dst, addr, off = op[1]
@@ -165,13 +184,13 @@ def body(s: Stream, sc: Sched, kind: str, first: bool = False):
             elif op[0] == "b2":
                 s.emit(f"s_waitcnt vmcnt({op[1]})")
                 s.emit("s_barrier")
-        if m == 128:
+        if m == NM:
             break
-        h, mm = divmod(m, 64)
-        i, j = divmod(mm, 8)
+        h, mm = divmod(m, NM // 2)
+        i, j = divmod(mm, NFB)
         a, b = (("fa0_", i), ("fb0_", j)) if h == 0 else (("fa1_", i), ("fb1_", j))
         s.need(a, b)
-        s.emit(mfma(8 * i + j, frag(*a), frag(*b), zero_c=first and h == 0))
+        s.emit(mfma(NFB * i + j, frag(*a), frag(*b), zero_c=first and h == 0))
 
 
 def suffix(q, q0):
@@ -185,11 +204,11 @@ def issue_two(s: Stream, vo: str, sc: Sched):
     for t in range(2):
         s.emit("s_mov_b32 m0, %[dbase]" if t == 0 else "s_xor_b32 m0, %[dbase], 0x10000")
         s.emit("s_nop 0")
-        for k in range(16):
-            srd = "srdA" if k < 8 else "srdB"
+        for k in range(sc.npc):
+            srd = "srdA" if k < sc.na else "srdB"
             soff = "0" if t == 0 else "%[k128]"
             s.emit(f"buffer_load_dwordx4 %[{vo}{k}], %[{srd}], {soff} offen{sc.pol[srd]} lds")
-            if k < 15:
+            if k < sc.npc - 1:
                 s.emit("s_add_u32 m0, m0, 0x1000")
                 s.emit("s_nop 0")
 
@@ -207,14 +226,14 @@ def kloop(n_stores: int, sc: Sched) -> list[str]:
     s.emit("s_cmp_eq_u32 %[first], 0")
     s.emit("s_cbranch_scc1 L_w4_pref_%=")
     issue_two(s, "vo", sc)
-    s.emit("s_waitcnt vmcnt(16)")
+    s.emit(f"s_waitcnt vmcnt({sc.npc})")
     s.emit("s_branch L_w4_go_%=")
     s.emit("L_w4_pref_%=:")
-    assert 16 + n_stores <= 63
-    s.emit(f"s_waitcnt vmcnt({16 + n_stores})")
+    assert sc.npc + n_stores <= 63
+    s.emit(f"s_waitcnt vmcnt({sc.npc + n_stores})")
     s.emit("L_w4_go_%=:")
     s.emit("s_barrier")
-    for dst, addr, off in reads_k0():
+    for dst, addr, off in reads_k0(sc):
         s.read(dst, addr, off)
     q0 = list(s.queue)
     body(s, sc, "steady", first=True)
@@ -262,6 +281,13 @@ def render() -> str:
                 out.append(f'  "{ln}\\n" \\')
             out.append('  ""')
             out.append("")
+    # half-height tile: every epilogue issues half the stores (plain 16, SiLU-mul 8; +2 under W4_RS)
+    for ns in (16, 8, 18, 10):
+        out.append(f"#define MLOP_W4H_KLOOP_S{ns}_ASM \\")
+        for ln in kloop(ns, SCHED_H):
+            out.append(f'  "{ln}\\n" \\')
+        out.append('  ""')
+        out.append("")
     for i in range(8):
         out.append(f"#define MLOP_W4_READ{i}_ASM \\")
         for ln in readout(i):

@@ -356,13 +356,13 @@ class GlooAllGather:
 
 
 def make_host_allgather(cpu_group, max_words: int):
-    """The shared-memory all-gather when every rank can map it (``MLOP_EP_CONTROL=gloo`` forces
-    the gloo fallback), else ``GlooAllGather``; decided collectively."""
+    """The shared-memory all-gather when every rank can map it, else ``GlooAllGather``; decided
+    collectively.  (The gloo form measured the same EP = 2 serving rate on one GPU:
+    profiles/r05_ep_control.md.)"""
     import sys
 
-    if os.environ.get("MLOP_EP_CONTROL", "shm") == "shm":
-        try:
-            return HostAllGather(cpu_group, max_words)
-        except HostAllGather.Unavailable as e:
-            print(f"[comm] shared-memory all-gather unavailable ({e}): gloo", file=sys.stderr)
+    try:
+        return HostAllGather(cpu_group, max_words)
+    except HostAllGather.Unavailable as e:
+        print(f"[comm] shared-memory all-gather unavailable ({e}): gloo", file=sys.stderr)
     return GlooAllGather(cpu_group, max_words)

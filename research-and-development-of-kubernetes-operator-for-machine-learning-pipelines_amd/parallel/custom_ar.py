@@ -22,10 +22,10 @@ import torch.distributed as dist
 
 # registered buffer per parity: one-shot messages up to this size, two-shot ones up to half of it
 # (tensor-parallel prefill chunks: 8192 x 4096 bf16 = 64 MiB at Llama-3-70B TP 8, chunked below)
-DEFAULT_MAX_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_MAX_BYTES", 64 << 20))
+DEFAULT_MAX_BYTES = 64 << 20
 # above this message size the two-shot kernel (reduce-scatter + all-gather, each one hop over the
 # full mesh: 2 (N-1)/N x the message per rank instead of the one-shot's N-1 x)
-TWO_SHOT_MIN_BYTES = int(os.environ.get("MLOP_CUSTOM_AR_TWO_SHOT_MIN", 512 << 10))
+TWO_SHOT_MIN_BYTES = 512 << 10
 
 
 # data parities in their own cached buffer, flags alone uncached (allreduce.hip "Memory").  Off

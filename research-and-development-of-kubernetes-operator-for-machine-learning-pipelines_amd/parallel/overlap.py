@@ -20,8 +20,8 @@ import torch
 
 from .. import ops
 
-MIN_ROWS = int(os.environ.get("MLOP_TP_OVERLAP_MIN_ROWS", 1024))
-CHUNK_ROWS = int(os.environ.get("MLOP_TP_OVERLAP_CHUNK", 1024))  # a multiple of the GEMM's 256-row tile
+MIN_ROWS = 1024
+CHUNK_ROWS = 1024  # a multiple of the GEMM's 256-row tile
 _COMM: dict = {}
 
 

@@ -48,11 +48,11 @@ class AttnMeta:
 
 # 128-token partitions: one 32-token page pair per wave at batch 1 (256: 312 tok/s, 128: 322,
 # 64: 246 - the reduce pass and partial traffic grow faster than the parallelism; run38/39)
-MIN_PART = int(os.environ.get("MLOP_ATTN_MIN_PART", 128))
+MIN_PART = 128
 # workgroups a decode launch aims for before it splits contexts into partitions (2048 / 4096:
 # batch 64 11,361 / 11,221 vs 11,643 tok/s at 1024, batch 16 flat: scripts/history/r4_twgs.sh);
 # at most 2048, so tiles x kv heads x partitions stays within MetaBuffers.wp_capacity
-TARGET_WGS = min(2048, int(os.environ.get("MLOP_ATTN_TARGET_WGS", 1024)))
+TARGET_WGS = 1024
 
 
 def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int | None = None,
@@ -130,8 +130,7 @@ class MetaBuffers:
         self.wp_capacity = 4096
         self.part_o = torch.empty(self.wp_capacity * 16 * 128, dtype=torch.float32, device=self.device)
         self.part_ml = torch.empty(self.wp_capacity * 16 * 2, dtype=torch.float32, device=self.device)
-        self.part_sem = (torch.zeros(self.wp_capacity, dtype=torch.int32, device=self.device)
-                         if os.environ.get("MLOP_ATTN_FUSED_REDUCE", "1") != "0" else None)
+        self.part_sem = torch.zeros(self.wp_capacity, dtype=torch.int32, device=self.device)
         bt = self.view_h("block_tables").reshape(max_seqs, max_blocks_per_seq)
         self.bt_h = bt  # numpy view [max_seqs, mb]
 

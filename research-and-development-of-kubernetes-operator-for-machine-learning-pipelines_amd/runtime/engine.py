@@ -73,9 +73,9 @@ class StepSync:
         self.is_leader = group.rank == 0
         self.hdr = torch.zeros(self.NHDR, dtype=torch.int64)
         # the header's host path: the native shared-memory channel (TP groups live on one node),
-        # gloo's broadcast as the fallback (MLOP_TP_HEADER=gloo, or the channel cannot be built)
+        # gloo's broadcast as the fallback (the channel cannot be built on every rank)
         self.chan = None
-        if cpu_group is not None and os.environ.get("MLOP_TP_HEADER", "shm") == "shm":
+        if cpu_group is not None:
             from ..parallel.comm import HostChannel
 
             try:  # collective: every rank gets a channel, or every rank raises and uses gloo
@@ -363,9 +363,7 @@ class Engine:
 
         # TP decode graphs capture the row-parallel all-reduces (K15 one-shot kernel, or RCCL
         # inside capture); the vocab gather runs after the replay (``_gather``).
-        # MLOP_TP_GRAPHS=0: eager TP decode (A/B)
-        tp_graphs = tp.size == 1 or os.environ.get("MLOP_TP_GRAPHS", "1") != "0"
-        if cfg.use_graphs and self.device.type == "cuda" and tp_graphs:
+        if cfg.use_graphs and self.device.type == "cuda":
             self.capture_graphs()
         self.kv.start_background_fill()  # after capture: the rest of a lazy KV arena
         self.stats["kv_ready_blocks_at_start"] = self.alloc.available
@@ -373,11 +371,12 @@ class Engine:
     def _setup_ep_exchange(self):
         """DP-attention + EP on GPU: the device-side MoE exchange over IPC peer memory
         (parallel/ep_ipc.py), sized for the largest forward this engine runs; collective over
-        the EP group (every rank builds its engine together).  MLOP_EP_IPC=0: RCCL all_to_all."""
+        the EP group (every rank builds its engine together).  Without it (CPU): the group's
+        all_to_all (parallel/moe.py)."""
         import os
 
         ep, mc = self.model.ps.ep, self.model.cfg
-        if os.environ.get("MLOP_EP_IPC", "1") == "0" or ep.ex is not None or not getattr(mc, "num_experts", 0):
+        if ep.ex is not None or not getattr(mc, "num_experts", 0):
             return
         from ..parallel.ep_ipc import EPExchange
 
@@ -1267,7 +1266,7 @@ class Engine:
         self.graph_pool = torch.cuda.graph_pool_handle()
         empty = np.zeros(0, dtype=np.int32)
         t0 = time.perf_counter()
-        verbose = os.environ.get("MLOP_VERBOSE", "0") == "1"
+        verbose = False
         with torch.cuda.stream(stream):
             for bi, b in enumerate(sorted(self.buckets, reverse=True)):
                 self.meta.fill_decode(empty, empty, np.zeros(0, dtype=np.int64), pad_to=b)

@@ -168,7 +168,7 @@ class EPBackend(LLMBackend):
         self.load = [0] * ps.ep.size
         self._rid = itertools.count()
         self._by_rid: dict[int, object] = {}
-        self.heartbeat_s = float(os.environ.get("MLOP_EP_HEARTBEAT_S", 1.0))
+        self.heartbeat_s = 1.0  # an idle group's empty iteration per second: a dead rank is noticed
         self.stopped = threading.Event()
 
     def _assign(self) -> int:

@@ -8,7 +8,7 @@ zeroed before first use (the attention kernel relies on finite unused slots).
 
 Two ways to back it:
 
-* eager: two ``torch.empty`` + ``zero_`` (CPU, TP ranks, ``MLOP_KV_LAZY=0``);
+* eager: two ``torch.empty`` + ``zero_`` (CPU, TP ranks, ``kv_cache.LAZY = False``);
 * lazy (default on one GPU): ``ops/csrc/vmm.hip`` reserves the whole virtual range, backs
   and zeroes the first chunk of pages before the engine reports ready, and a native worker
   thread backs the rest while it serves.  A 134 GB hipMalloc waits 0.7-4.8 s for the
@@ -39,8 +39,11 @@ def _sync(device) -> None:
         torch.cuda.synchronize(device)
 
 
+LAZY = True  # GPU pools lazily backed (tests flip it for the eager / lazy A/B)
+
+
 def _lazy_default(device) -> bool:
-    if torch.device(device).type != "cuda" or os.environ.get("MLOP_KV_LAZY", "1") == "0":
+    if torch.device(device).type != "cuda" or not LAZY:
         return False
     from .. import ops
 

@@ -1,7 +1,7 @@
 """GEMM microbench on the Llama-3-8B (or BENCH_MODEL=70b: Llama-3-70B) projection shapes: the hand-written MFMA
 GEMM (forced, ``ops.GEMM_BACKEND = "mlop"``) vs torch.matmul (hipBLASLt).
 One process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24), random data.
-Env knobs of the C++ planner are swept by re-running with MLOP_GEMM_* set."""
+Individual tilings are forced with ``torch.ops.mlop.gemm_dense_plan`` (scripts/bench_mid_m.py)."""
 import json
 import os
 import sys

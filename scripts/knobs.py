@@ -44,10 +44,17 @@ def main():
     if "--check" in sys.argv:
         doc = (ROOT / "docs" / "KNOBS.md").read_text()
         missing = [n for n in found if f"`{n}`" not in doc]
+        # and the reverse: a documented knob nothing reads any more (a removed A/B switch)
+        import re
+
+        documented = {m for row in doc.splitlines() if row.startswith("| `MLOP_")
+                      for m in re.findall(r"`(MLOP_[A-Z0-9_]+)`", row.split("|")[1])}
+        stale = sorted(n for n in documented if n not in found and not n.startswith("MLOP_ENGINE_"))
         if missing:
             print("not in docs/KNOBS.md:", ", ".join(sorted(missing)))
-            return 1
-        return 0
+        if stale:
+            print("documented but read nowhere:", ", ".join(stale))
+        return 1 if (missing or stale) else 0
     for name in sorted(found):
         e = found[name]
         print(f"| `{name}` | {e['default'] or '—'} | {', '.join(e['where'][:2])} |")

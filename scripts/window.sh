@@ -2,7 +2,7 @@
 # Timed-window kernel profile of one bench configuration: rocprofv3 kernel trace + stats, then
 # the per-step breakdown of the last STEPS forwards (trace_window.py).
 # Usage: gpurun -- bash scripts/window.sh LABEL STEPS [extra bench.py args...]
-#        (env vars before `bash` reach the bench: MLOP_NORM_CHAIN=0 bash scripts/window.sh ...)
+#        (env vars before `bash` reach the bench: MLOP_GEMM_BACKEND=auto bash scripts/window.sh ...)
 source scripts/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 L=$1; S=$2; shift 2

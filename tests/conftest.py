@@ -40,22 +40,9 @@ def pp_variant(gpu):
 
 
 @pytest.fixture
-def gemv_addnorm_on(gpu):
-    """Turn the opt-in GEMV add + RMSNorm epilogue on for the test (off by default: a measured
-    loss, profiles/r04_decode_small_batch.md), so its numerics and race tests keep running."""
-    import torch
-
-    prev = torch.ops.mlop.gemv_addnorm_enable(1)
-    try:
-        yield
-    finally:
-        torch.ops.mlop.gemv_addnorm_enable(prev)
-
-
-@pytest.fixture
 def attn_fused_all(gpu):
-    """Lift the (tile, kv head) pair cap of paged attention's in-launch split-KV combine
-    (MLOP_ATTN_FUSED_MAX_PAIRS) so a test's part_sem launch takes the fused path at any size."""
+    """Lift the (tile, kv head) pair cap of paged attention's in-launch split-KV combine (none
+    by default; the op sets it) so a test's part_sem launch takes the fused path at any size."""
     import torch
 
     prev = torch.ops.mlop.attn_fused_max_pairs(1 << 30)

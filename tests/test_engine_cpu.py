@@ -167,24 +167,6 @@ def test_moe_reference_ops_roundtrip():
     assert int((inv2 >= 0).sum()) == int(off2[-1])
 
 
-@pytest.mark.parametrize("cfg", ["llama", "mixtral"])
-def test_decode_forward_with_norm_fusion(tiny, cfg):
-    """MLOP_NORM_FUSION=1 routes steps of <= 4 tokens through forward_decode (the
-    residual add + RMSNorm carried into the next projection; on CPU the reference
-    add_rmsnorm + gemm run in its place): outputs equal the dense oracle."""
-    model = tiny if cfg == "llama" else build_model(TINY_MIXTRAL, device="cpu", dtype=torch.float32, seed=2)
-    ops.NORM_FUSION = True
-    try:
-        eng = Engine(model, EngineConfig(max_num_seqs=3, max_num_batched_tokens=64, max_model_len=128,
-                                         num_kv_blocks=32, use_graphs=False, mixed_prefill=False))
-        prompts = [torch.randint(2, 500, (n,)).tolist() for n in (3, 9, 4)]
-        outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
-    finally:
-        ops.NORM_FUSION = False
-    for p, o in zip(prompts, outs):
-        assert o == greedy_ref(model, p, 5)
-
-
 def test_block_allocator_grow():
     """Lazily backed KV: only ids below ``available`` are handed out until grow()."""
     a = BlockAllocator(100, available=10)

@@ -1,4 +1,5 @@
-"""Four-wave hand-scheduled 256x256 GEMM (gemm_w4.hip, planner variant 5) vs the fp32
+"""Four-wave hand-scheduled GEMM (gemm_w4.hip: 256x256, planner variant 5, and the 128x256
+half-height tile, variant 6) vs the fp32
 PyTorch oracle: plain, SiLU-mul and RoPE + paged-cache epilogues, ragged M, persistent
 workgroups walking 1-7 tiles (the next tile's first K-tiles prefetched under the epilogue
 stores), the shortest K the peeled loop supports (192: first + nodma + last, no steady)."""
@@ -16,14 +17,19 @@ def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
 
-@pytest.fixture
-def w4(gpu):
+@pytest.fixture(params=[256, 128], ids=["bm256", "bm128"])
+def w4(gpu, request):
+    """The four-wave kernel at both tile heights: 256 x 256 (planner variant 5) and the
+    128 x 256 half-height tile (variant 6, forced through the dense-plan override)."""
     prev = torch.ops.mlop.gemm_big_variant(-1)
     torch.ops.mlop.gemm_big_variant(5)
+    if request.param == 128:
+        torch.ops.mlop.gemm_dense_plan(6, 128, 256, -1)
     ops.GEMM_BACKEND = "mlop"
     try:
-        yield
+        yield request.param
     finally:
+        torch.ops.mlop.gemm_dense_plan(-1, -1, -1, -1)
         torch.ops.mlop.gemm_big_variant(prev)
         ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
 

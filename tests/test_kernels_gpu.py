@@ -822,103 +822,3 @@ def test_moe_pipeline(gpu, T, E, k, H, I):
         # bf16 rounding noise scales with the output magnitude (large I: |out| ~ 20)
         close(out, exp, atol=3e-2 + 3e-3 * float(exp.abs().max()), rtol=3e-2)
         assert n == int(((idx >= e0) & (idx < e0 + nl)).sum())
-
-
-@pytest.mark.parametrize("M", [1, 2, 4])
-@pytest.mark.parametrize("epi,N,K", [(0, 4096, 4096), (1, 28672, 4096), (0, 1280, 8192), (1, 7168, 8192)])
-def test_norm_gemm_fused(gpu, M, epi, N, K):
-    """Residual add + RMSNorm as the GEMV's prologue (gemv.hip NORM) vs add_rmsnorm + fp32
-    matmul: the new residual is bit-exact, the output within bf16 tolerance (the fused form
-    applies 1/rms after the dot, one rounding fewer)."""
-    torch.manual_seed(M + N + K)
-    y = torch.randn(M, K, device=gpu, dtype=bf)
-    res = torch.randn(M, K, device=gpu, dtype=bf)
-    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(bf)
-    w = (0.03 * torch.randn(N, K, device=gpu)).to(bf)
-    ops.NORM_FUSION = True  # opt-in path (MLOP_NORM_FUSION=1)
-    try:
-        fused = ops.norm_fusable(M, N, K, epi)
-    finally:
-        ops.NORM_FUSION = False
-    assert fused == (M == 1)  # MLOP_NORM_FUSION_MAX_M default
-    ops.NORM_FUSION = True
-    try:
-        out, r2 = ops.norm_gemm(y, res.clone(), nw, w, 1e-5, epi)
-    finally:
-        ops.NORM_FUSION = False
-    x_ref, r_ref = ref.add_rmsnorm(y, res, nw, 1e-5)
-    assert torch.equal(r2.cpu(), r_ref.cpu())
-    exp = (x_ref.float() @ ops.deinterleave_rows(w).float().t() if epi else x_ref.float() @ w.float().t())
-    if epi:  # SiLU-mul amplifies the one-rounding-fewer difference of the deferred 1/rms
-        exp = ref.silu_mul(exp.to(bf))
-    close(out, exp, atol=1.5e-1 if epi else 3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("M,Hq,Hkv", [(1, 32, 8), (4, 32, 8), (2, 8, 1)])
-def test_norm_qkv_rope_fused(gpu, M, Hq, Hkv):
-    from mlopamd.models.layers import rope_table
-
-    D, K, BS, NB = 128, 4096, 16, 32
-    N = (Hq + 2 * Hkv) * D
-    torch.manual_seed(M + Hq)
-    cs = rope_table(D, 8192, 5e5, device=gpu)
-    y = torch.randn(M, K, device=gpu, dtype=bf)
-    res = torch.randn(M, K, device=gpu, dtype=bf)
-    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(bf)
-    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
-    pos = torch.randint(0, 8000, (M,), device=gpu, dtype=torch.int32)
-    slots = torch.randperm(NB * BS, device=gpu)[:M].to(torch.int32)
-    kc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    vc = torch.zeros(NB, Hkv, BS, D, device=gpu, dtype=bf)
-    ops.NORM_FUSION = True
-    try:
-        q, r2 = ops.norm_qkv_rope_cache(y, res.clone(), nw, w, pos, cs, slots, kc, vc, Hq, 1e-5)
-    finally:
-        ops.NORM_FUSION = False
-    x_ref, r_ref = ref.add_rmsnorm(y, res, nw, 1e-5)
-    assert torch.equal(r2.cpu(), r_ref.cpu())
-    qkv_ref = (x_ref.float() @ w.float().t()).to(bf).cpu()
-    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
-    q_ref = ref.rope_cache(qkv_ref, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, Hq)
-    close(q, q_ref, atol=3e-2, rtol=3e-2)
-    close(kc, kr, atol=3e-2, rtol=3e-2)
-    close(vc, vr, atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (2, 4096, 14336), (3, 4096, 4096), (4, 8192, 1024),
-                                   (1, 1024, 4096)])
-def test_gemv_add_rmsnorm_epilogue(gpu, gemv_addnorm_on, M, N, K):
-    """Decode sizes: residual add + RMSNorm as the GEMV's epilogue (grid ticket, the last
-    workgroup normalises): residual bit-equal to GEMV -> add_rmsnorm (same roundings), the normed
-    output vs the fp32 oracle, relaunch bit-identical (partials summed in a fixed order; the
-    ticket re-arms), and inside a captured graph."""
-    torch.manual_seed(M * N + K)
-    assert torch.ops.mlop.gemm_workspace(M, N, K, ops.EPI_ADD_RMSNORM) > 0
-    x = torch.randn(M, K, device=gpu, dtype=bf)
-    w = (0.02 * torch.randn(N, K, device=gpu)).to(bf)
-    res = torch.randn(M, N, device=gpu, dtype=bf)
-    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(bf)
-    y = ops.gemm(x, w)
-    r_ref = res.clone()
-    out_ref = ops.add_rmsnorm(y, r_ref, nw, 1e-5)
-    exp_out, _ = ref.add_rmsnorm((x.float() @ w.float().t()).to(bf), res, nw, 1e-5)
-    ops.GEMM_BACKEND = "mlop"
-    try:
-        r1, r2 = res.clone(), res.clone()
-        o1 = ops.gemm_add_rmsnorm(x, w, r1, nw, 1e-5)
-        o2 = ops.gemm_add_rmsnorm(x, w, r2, nw, 1e-5)
-        rg = res.clone()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            og = ops.gemm_add_rmsnorm(x, w, rg, nw, 1e-5)
-        rg.copy_(res)
-        g.replay()
-        torch.cuda.synchronize()
-    finally:
-        ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
-    assert torch.equal(r1, r_ref) and torch.equal(r1, r2) and torch.equal(o1, o2)
-    assert torch.equal(rg, r1) and torch.equal(og, o1)
-    close(o1, out_ref, atol=1.6e-2, rtol=1e-2)  # the sum of squares' order differs from norm.hip's
-    close(o1, exp_out, atol=5e-2, rtol=3e-2)

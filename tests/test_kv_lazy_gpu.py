@@ -74,8 +74,10 @@ def test_engine_grows_kv_mid_run(gpu, small_chunks, monkeypatch):
     prompts = [torch.randint(2, 500, (200 + 10 * i,), generator=torch.Generator().manual_seed(i)).tolist()
                for i in range(24)]
     outs = {}
+    from mlopamd.runtime import kv_cache
+
     for lazy in ("1", "0"):
-        monkeypatch.setenv("MLOP_KV_LAZY", lazy)
+        monkeypatch.setattr(kv_cache, "LAZY", lazy == "1")
         eng = Engine(model, EngineConfig(max_num_seqs=24, max_num_batched_tokens=2048, max_model_len=512,
                                          num_kv_blocks=2048, use_graphs=True, graph_buckets=(1, 8, 24)))
         assert eng.kv.lazy == (lazy == "1")

@@ -19,15 +19,20 @@ def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
 
-@pytest.fixture
-def w4(gpu):
+@pytest.fixture(params=[256, 128], ids=["bm256", "bm128"])
+def w4(gpu, request):
+    """The four-wave kernel at both tile heights: 256 x 256 (planner variant 5) and the
+    128 x 256 half-height tile (variant 6, forced through the dense-plan override)."""
     prev = torch.ops.mlop.gemm_big_variant(-1)
     torch.ops.mlop.gemm_big_variant(5)
+    if request.param == 128:
+        torch.ops.mlop.gemm_dense_plan(6, 128, 256, -1)
     ops.GEMM_BACKEND = "mlop"
     ops._sk_reserve(torch.device(gpu))
     try:
-        yield
+        yield request.param
     finally:
+        torch.ops.mlop.gemm_dense_plan(-1, -1, -1, -1)
         torch.ops.mlop.gemm_big_variant(prev)
         ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
 
@@ -234,7 +239,7 @@ def test_gemm_res_ss_odd_group_count(gpu, w4):
 def test_checkpoint_norms_folded_chain_matches_hf(gpu, w4, tmp_path, monkeypatch):
     """A checkpoint with trained (non-unit) RMSNorm weights: load_pretrained folds them into
     QKV / gate_up, so the 2048-row prefill runs the norm chain, and its first tokens are the
-    fp32 transformers model's argmax (up to bf16 near-ties).  MLOP_FOLD_NORMS=0 keeps the norm
+    fp32 transformers model's argmax (up to bf16 near-ties).  fold_norms=False keeps the norm
     weights and the chain off."""
     transformers = pytest.importorskip("transformers")
     from mlopamd.models import loader
@@ -251,9 +256,7 @@ def test_checkpoint_norms_folded_chain_matches_hf(gpu, w4, tmp_path, monkeypatch
             layer.input_layernorm.weight.uniform_(0.5, 1.5)
             layer.post_attention_layernorm.weight.uniform_(0.5, 1.5)
     hf.save_pretrained(tmp_path)
-    monkeypatch.setenv("MLOP_FOLD_NORMS", "0")
-    assert not loader.load_pretrained(tmp_path, device=gpu).unit_norms
-    monkeypatch.delenv("MLOP_FOLD_NORMS")
+    assert not loader.load_pretrained(tmp_path, device=gpu, fold_norms=False).unit_norms
     model = loader.load_pretrained(tmp_path, device=gpu)
     assert model.unit_norms and model._chain_ok(2048)
     eng = Engine(model, EngineConfig(max_num_seqs=8, max_num_batched_tokens=2048, max_model_len=512,
