@@ -431,22 +431,53 @@ void launch_paged_attention(void* out, float* part_o, float* part_ml, const void
 }
 
 // ---------------------------------------------------------------------------
-// K7 flash prefill: the same S^T / O^T formulation, re-blocked for prompt
-// chunks.  One workgroup = 128 MFMA q-rows (128/G query tokens x the G heads of
-// one kv head) against EVERY key of its causal range; each wave owns 2 column
-// tiles (32 q-rows), so every K/V fragment read from LDS feeds 2 MFMAs and
-// every K/V byte fetched from HBM/L2 feeds all 128 q-rows (vs 16 in the decode
-// tile above: 8x the arithmetic intensity).  K/V page pairs (32 keys, 16 KB)
-// stream through a 3-deep LDS ring by LDS-DMA (global_load_lds, counted vmcnt,
-// one raw barrier per pair), swizzled through the SOURCE address:
-//   K page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ k        (ds_read_b128, 16 keys/group)
-//   V page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ vswz(k)  (ds_read_b64_tr_b16)
-// both conflict-free for the fragment reads below.
-#ifndef FLASH_WG_PER_CU
-#define FLASH_WG_PER_CU 3
-#endif
-template <int G>
-__global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
+// K7 flash prefill on the 32x32x16 MFMA (cdna_hip_programming.md "Fused attention prefill":
+// swapped QK^T, an accumulator tile as the next MFMA's operand).  One workgroup = 128 MFMA
+// q-rows (128/G query tokens x the G heads of one kv head) against EVERY key of its causal
+// range, so every K/V byte fetched from L2 feeds all 128 q-rows.  K/V page pairs (32 keys, 16 KB)
+// stream through a 3-deep LDS ring by LDS-DMA (global_load_lds, counted vmcnt, one raw barrier
+// per pair), swizzled through the SOURCE address:
+//   K page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ k       (ds_read_b128)
+//   V page [16 keys][16 x 16 B]: chunk c of key k at slot c ^ vswz(k) (ds_read_b64_tr_b16)
+// both conflict-free for the fragment reads below (SQ_LDS_BANK_CONFLICT = 0).  Per wave 32
+// q-rows, ONE per lane column:
+//   S^T [32 keys x 32 q] = K . Q^T: 8 MFMAs (A = K rows by ds_read_b128, B = Q^T in registers);
+//     lane l holds the 16 keys (r & 3) + 8 (r >> 2) + 4 h (h = l >> 5) of q column l & 31, so
+//     the row max is 15 lane-local max + ONE permlane32 swap, the row sum lane-local (the two
+//     halves' partial sums meet once, in the epilogue);
+//   O^T [128 d x 32 q] += V^T . P^T: 8 MFMAs, P^T straight from the S registers (registers
+//     8s .. 8s+7 -> bf16 = the k-step s fragment, k order permuted), V^T by two
+//     ds_read_b64_tr_b16 per fragment from the token-major image (keys 16s + 4h + 0..3 and
+//     + 8, dims 32 dblk + (l & 31)).
+// Half the MFMA issue slots of a 16x16x32 form for the same FLOPs (an MFMA holds the SIMD's
+// vector issue for 8 cycles either way, MI355X_MICROARCH.md constants) and a quarter of its
+// cross-lane max steps: +4 % at 1 x 8192, +19 % at 4 x 2048 and 16 x 512 over the round-4
+// 16x16x32 kernel (profiles/r05_flash32.md).  Two workgroups per CU (up to 256 VGPRs) beat
+// three (168) by 1-5 %.
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr float kRescaleLog2 = 8.f;  // flash32 deferred-rescale threshold (exp2 units)
+// two floats -> one dword of two bf16 in ONE v_cvt_pk_bf16_f32 (pack2's two scalar casts
+// become two cvt + shift + or)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// byte offset (page 0, dim block 0, rows 4h + q) of lane l's first transposed V read: lane
+// 4q + p of 16-lane group g addresses row t = 4h + q, chunk 2 (g & 1) + (p >> 1), half p & 1.
+// Dim block dblk flips address bits 6-7 (^ 64 dblk: the chunk's high bits only meet q there),
+// rows + 8 flip bit 5 and add 2048, page B adds 4096.
+__device__ __forceinline__ uint32_t vt32_base(int lane) {
+  const int g = lane >> 4, h = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
+  const int t = 4 * h + q, c = 2 * (g & 1) + (p >> 1);
+  return 256u * t + 16u * (c ^ vswz(t)) + 8u * (p & 1);
+}
+
+template <int G, int WPC>
+__global__ void __launch_bounds__(256, WPC) flash32_prefill_kernel(
     uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
@@ -458,166 +489,199 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
   constexpr int PAGE = kBS * kD;
   __shared__ __attribute__((aligned(256))) uint16_t smem[STAGES * STAGE];
 
-  // 1-D grid, kv head fastest: blocks are dealt to the 8 XCDs round-robin, so with 8 kv
-  // heads every workgroup of one head runs on ONE XCD and the 64+ q-tiles of a sequence
-  // re-read that head's K/V pages from its L2 instead of from the fabric
-  const int tile = blockIdx.x / Hkv, kvh = blockIdx.x % Hkv;
+  const int tile = blockIdx.x / Hkv, kvh = blockIdx.x % Hkv;  // kv head fastest: one XCD per head
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = ptile_seq[tile], q0 = ptile_q0[tile];
   const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
   const int last_q = min(q0 + QB, ql) - 1;
-  const int kv_end = ctx - ql + last_q + 1;  // exclusive causal limit of the workgroup
+  const int kv_end = ctx - ql + last_q + 1;
   const int n_pairs = (kv_end + 31) >> 5;
   const int n_pages = (kv_end + kBS - 1) / kBS;
-  const int wg_min_pos = ctx - ql + q0;      // position of the workgroup's first query token
-  const int r = lane & 15, g4 = lane >> 4;
+  const int wg_min_pos = ctx - ql + q0;
+  const int col = lane & 31, h = lane >> 5;
 
-  bf16x8 qf[2][4];
-  int pos_r[2];
+  // this lane's q row (MFMA column): R = 32 wid + col
+  const int R = 32 * wid + col;
+  const int qi = q0 + R / G;
+  const bool q_ok = qi < ql;
+  const int pos_r = q_ok ? ctx - ql + qi : -1;
+  bf16x8 qf[8];
+  {
+    const uint16_t* qrow = q + ((size_t)(qs + (q_ok ? qi : 0)) * Hq + kvh * G + R % G) * kD + 8 * h;
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int R = 32 * wid + 16 * c + r;
-    const int qi = q0 + R / G;
-    const bool ok = qi < ql;
-    pos_r[c] = ok ? ctx - ql + qi : -1;
-    const uint16_t* qrow = q + ((size_t)(qs + (ok ? qi : 0)) * Hq + kvh * G + R % G) * kD;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + kk * 32 + g4 * 8);
-      qf[c][kk] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < 8; ++t) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + 16 * t);
+      qf[t] = q_ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-
-  f32x4 o[2][8];
+  f32x16 o[4];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int d = 0; d < 4; ++d)
 #pragma unroll
-    for (int d = 0; d < 8; ++d) o[c][d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {kNegBig, kNegBig}, l[2] = {0.f, 0.f};
+    for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
+  float m = kNegBig, l = 0.f;
 
   const int* bt = block_tables + (size_t)s * bt_stride;
   const size_t page_stride = (size_t)Hkv * PAGE;
-  // this lane's DMA source offsets inside a page (wave w moves piece w of each page)
   const int kkey = wid * 4 + (lane >> 4);
-  // page B's K image is swizzled with an extra ^4: the permuted row order below reads keys
-  // {0-3, 8-11} (or {4-7, 12-15}) of BOTH pages in one 16-lane group, all 16 slots distinct
+  // K image: chunk c of key k at slot c ^ k on BOTH pages (the 32x32 A-operand reads take keys
+  // {0-3, 12-15} of one page and {4-11} of the other per 16-lane group: 16 distinct slots)
   const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
-  const int k_offB = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15) ^ 4) << 3);
-  // V image: [16 token rows][256 B] per page, 16-B chunk c of row t at slot c ^ vswz(t)
   const int v_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ vswz(kkey)) << 3);
-  // page ids of pair pp; the loop reads them one iteration ahead of their DMA, so the
-  // block-table load's latency is not paid in front of every issue
-  // per-lane transposed-read base of the stage-0 V image (stage ST adds a constant)
-  const uint32_t vt_b0 = (uint32_t)(uintptr_t)smem + vt_base(lane);
   auto page_of = [&](int idx) { return idx < n_pages ? min(max(bt[idx], 0), num_blocks - 1) : -1; };
   auto issue_pages = [&](int buf, int pgA, int pgB) {
     if (pgB < 0) pgB = pgA;
     uint16_t* base = smem + buf * STAGE + wid * 512;
     __builtin_amdgcn_global_load_lds((const void*)(kc + pgA * page_stride + k_off), (lds_void_t*)(base), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_offB), (lds_void_t*)(base + PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pgB * page_stride + k_off), (lds_void_t*)(base + PAGE), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(vc + pgA * page_stride + v_off), (lds_void_t*)(base + 2 * PAGE), 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(vc + pgB * page_stride + v_off), (lds_void_t*)(base + 3 * PAGE), 16, 0, 0);
+  };
+  // K fragment t of this lane: key col of the pair (page col >> 4, row col & 15), chunk 2t + h at
+  // slot (2t + h) ^ (col & 15): byte k_b0 ^ 32 t
+  const int k15 = col & 15;
+  const uint32_t k_b0 = (uint32_t)(uintptr_t)smem + (uint32_t)((col >> 4) * PAGE * 2 + k15 * 256 + ((h ^ k15) << 4));
+  const uint32_t v_b0 = (uint32_t)(uintptr_t)smem + 2 * PAGE * 2 + vt32_base(lane);
+
+  // S^T of the pair in ring slot ST: K fragment t at k_b0 ^ 32 t, four reads in flight (inline
+  // asm with counted waits: as plain loads the compiler reused one register set and waited
+  // lgkmcnt(0) in front of every MFMA, one LDS latency per fragment)
+  auto qk = [&](auto st_tag) {
+    constexpr uint32_t so = (uint32_t)(decltype(st_tag)::value * STAGE * 2);
+    uint32_t kb = k_b0;
+    asm volatile("" : "+v"(kb));
+    auto kread = [&](int t, bf16x8& f) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(kb ^ (32u * t)), "n"(so));
+    };
+    f32x16 sc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sc[e] = 0.f;
+    bf16x8 kf[4];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // nothing else (SMEM) in the counts below
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kread(t, kf[t]);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      bf16x8& f = kf[t & 3];
+      if (t <= 4) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(f));
+      else if (t == 5) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f));
+      else if (t == 6) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(f));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f));
+      sc = mfma32(f, qf[t], sc);
+      if (t + 4 < 8) kread(t + 4, kf[t & 3]);
+    }
+    return sc;
+  };
+  // online softmax on the lane's 16 keys of its q column (raw score units; the scale folds into
+  // the exponent's FMA) -> P^T fragments of the two k-steps; O and l rescaled when the max moved
+  auto softmax = [&](f32x16 sc, int pp, bf16x8 (&pf)[2]) {
+    if (pp * 32 + 31 > wg_min_pos) {  // a pair crossing the workgroup's causal diagonal
+      // (a side effect keeps this a branch: if-converted, the 47 compare / select / add of the
+      // mask ran on every pair, a third of the loop's VALU)
+      asm volatile("");
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tok = pp * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        sc[r] = tok <= pos_r ? sc[r] : -INFINITY;
+      }
+    }
+    float mx = fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+    mx = fmaxf(mx, sc[15]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    // deferred rescale (cdna_hip_programming.md T13): the running max moves only when some row's
+    // new max exceeds it by more than 2^kRescaleLog2 in exp2 units (always on a row's first
+    // keys: m starts at -1e30); otherwise P stays scaled against the old max, <= 2^8, which
+    // bf16 P and f32 O / l carry exactly as well.  The decision covers this pair's P and is
+    // taken before it is exponentiated, with the previous pair's P.V complete, so O, l and P
+    // all see the same factor.
+    float alpha = 1.f;
+    if (__ballot((mx - m) * scale_log2 > kRescaleLog2)) {
+      const float m_new = fmaxf(m, mx);
+      alpha = fast_exp2((m - m_new) * scale_log2);
+      m = m_new;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+      l *= alpha;
+    }
+    const float mc = -m * scale_log2;
+    float rs = 0.f;
+    u32x4 w[2];
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const float p0 = fast_exp2(fmaf(sc[r], scale_log2, mc)), p1 = fast_exp2(fmaf(sc[r + 1], scale_log2, mc));
+      rs += p0 + p1;
+      w[r >> 3][(r & 7) >> 1] = cvt_pk_bf16(p0, p1);
+    }
+    pf[0] = __builtin_bit_cast(bf16x8, w[0]);
+    pf[1] = __builtin_bit_cast(bf16x8, w[1]);
+    l += rs;
+  };
+  // O^T += V^T . P^T from ring slot ST; the V^T fragment of (dblk, page) = two transposed reads.
+  // The reads are inline asm: as builtins the compiler put s_waitcnt vmcnt(0) in front of them
+  // (it cannot tell them from the in-flight LDS-DMA of the next pairs), which exposed the
+  // latency of the DMA just issued on every pair.  The ring protocol (vmcnt + barrier at the
+  // top of the step) already covers this pair; the asm waits below count only these reads.
+  auto pv = [&](auto st_tag, const bf16x8 (&pf)[2]) {
+    constexpr uint32_t so = (uint32_t)(decltype(st_tag)::value * STAGE * 2);
+    uint32_t vb = v_b0;
+    asm volatile("" : "+v"(vb));
+    // both pages' fragments of dim block dblk: 4 reads, results in (lo, hi) of f0 (page A), f1
+    auto issue = [&](int dblk, v4s16 (&r)[4]) {
+      const uint32_t a0 = vb ^ (64u * dblk), a1 = a0 ^ 32u;
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %4 offset:%6\n"
+          "ds_read_b64_tr_b16 %1, %5 offset:%7\n"
+          "ds_read_b64_tr_b16 %2, %4 offset:%8\n"
+          "ds_read_b64_tr_b16 %3, %5 offset:%9\n"
+          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+          : "v"(a0), "v"(a1), "n"(so), "n"(so + 2048u), "n"(so + 4096u), "n"(so + 6144u));
+    };
+    auto frag = [&](const v4s16& lo, const v4s16& hi) {
+      bf16x8 f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = lo[e];
+        f[4 + e] = hi[e];
+      }
+      return f;
+    };
+    v4s16 ra[4], rb[4];
+    issue(0, ra);
+#pragma unroll
+    for (int dblk = 0; dblk < 4; ++dblk) {
+      v4s16 (&cur)[4] = (dblk & 1) ? rb : ra;
+      v4s16 (&nxt)[4] = (dblk & 1) ? ra : rb;
+      if (dblk < 3) {
+        issue(dblk + 1, nxt);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+      }
+      o[dblk] = mfma32(frag(cur[0], cur[1]), pf[0], o[dblk]);
+      o[dblk] = mfma32(frag(cur[2], cur[3]), pf[1], o[dblk]);
+    }
   };
 
   issue_pages(0, page_of(0), page_of(1));
   if (n_pairs > 1) issue_pages(1, page_of(2), page_of(3));
-  int nxtA = page_of(4), nxtB = page_of(5);  // pair 2
-  // one pair through ring slot ST (= pp % STAGES, a template constant: the slot's LDS offset
-  // becomes the ds_read immediate instead of a per-read VALU add)
+  int nxtA = page_of(4), nxtB = page_of(5);
   auto pair_step = [&](auto st_tag, int pp) {
     constexpr int ST = decltype(st_tag)::value;
     if (pp + 1 < n_pairs) wait_vmcnt<4>(); else wait_vmcnt<0>();
-    raw_barrier();  // pair pp visible to every wave; buffer (pp-1)%3 free
+    raw_barrier();  // pair pp visible to every wave; ring slot (pp - 1) % 3 free
     if (pp + 2 < n_pairs) {
       issue_pages((ST + 2) % STAGES, nxtA, nxtB);
       nxtA = page_of(2 * pp + 6);
       nxtB = page_of(2 * pp + 7);
     }
-    const uint16_t* sK = smem + ST * STAGE;
-    const uint16_t* sV = sK + 2 * PAGE;
-    // S^T = K . Q^T for both column tiles, each K fragment read once and used twice
-    f32x4 sa[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sb[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      // decode kernel's token order: MFMA row r of the first product is pair token
-      // 8(r>>2) + (r&3), of the second that + 4, so lane group g4 ends up owning the 8
-      // consecutive tokens 8g4..8g4+7 and its V^T fragment is one 16-B LDS read
-      const int ch = kk * 4 + g4;
-      const uint16_t* kp = sK + (r >> 3) * PAGE;
-      const int key_a = 8 * ((r >> 2) & 1) + (r & 3), key_b = key_a + 4, pb4 = (r >> 3) << 2;
-      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kp + key_a * kD + ((ch ^ key_a ^ pb4) << 3));
-      const bf16x8 kb = *reinterpret_cast<const bf16x8*>(kp + key_b * kD + ((ch ^ key_b ^ pb4) << 3));
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        sa[c] = mfma16(ka, qf[c][kk], sa[c]);
-        sb[c] = mfma16(kb, qf[c][kk], sb[c]);
-      }
-    }
-    const int tokA = pp * 32 + g4 * 8, tokB = tokA + 4;
-    const bool full_pair = pp * 32 + 31 <= wg_min_pos;  // every key of the pair is visible to every row
     bf16x8 pf[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      // running max kept in RAW score units (scale > 0 preserves order); the scale
-      // folds into the exponent's FMA: p = exp2(s*c - m*c).  The causal mask is applied
-      // only on pairs that cross the workgroup's diagonal (wave-uniform test).
-      float pa[4], pb[4];
-      if (full_pair) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { pa[i] = sa[c][i]; pb[i] = sb[c][i]; }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          pa[i] = (tokA + i <= pos_r[c]) ? sa[c][i] : -INFINITY;
-          pb[i] = (tokB + i <= pos_r[c]) ? sb[c][i] : -INFINITY;
-        }
-      }
-      float mx = fmaxf(fmaxf(fmaxf(pa[0], pa[1]), fmaxf(pa[2], pa[3])),
-                       fmaxf(fmaxf(pb[0], pb[1]), fmaxf(pb[2], pb[3])));
-      mx = max_x16_x32(mx);
-      const float m_new = fmaxf(m[c], mx);
-      const float alpha = fast_exp2((m[c] - m_new) * scale_log2);
-      m[c] = m_new;
-      const float mc = -m_new * scale_log2;
-      float rs = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pa[i] = fast_exp2(fmaf(pa[i], scale_log2, mc));
-        pb[i] = fast_exp2(fmaf(pb[i], scale_log2, mc));
-        rs += pa[i] + pb[i];
-        pf[c][i] = (short)f2bf(pa[i]);
-        pf[c][4 + i] = (short)f2bf(pb[i]);
-      }
-      l[c] = l[c] * alpha + rs;
-      // rescale O only when some row's running max moved (after the first pairs of a
-      // causal prefill it rarely does): wave-uniform branch, 32 v_mul saved per tile
-      if (__ballot(alpha != 1.f)) {
-#pragma unroll
-        for (int d = 0; d < 8; ++d) o[c][d] *= alpha;
-      }
-    }
-    // O^T += V^T . P^T: one V fragment per 16-dim block, read just in time and used by
-    // both column tiles (8 VGPRs of V live instead of 32: 3 waves per SIMD fit)
-    {
-      // rows 8 g4 .. 8 g4 + 7 of the two stacked page images (page g4 >> 1), one fragment per
-      // 16-dim block read just in time and used by both column tiles
-      constexpr uint32_t vo = (uint32_t)(ST * STAGE * 2 + 4 * PAGE);
-      // opaque per pair: otherwise the 16 loop-invariant read addresses are hoisted out of the
-      // loop and spilled (168-VGPR budget of 3 workgroups per CU)
-      uint32_t vb = vt_b0 + vo;
-      asm volatile("" : "+v"(vb));
-      // fragment d + 1 is read while d's two MFMAs run (two register sets; 1.5-3 % faster than
-      // reading each just in time, scripts/history/r4_flash.sh)
-      bf16x8 vf = vt_frag(vb, 0);
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        bf16x8 nx = vf;
-        if (d < 7) nx = vt_frag(vb, d + 1);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) o[c][d] = mfma16(vf, pf[c], o[c][d]);
-        vf = nx;
-      }
-    }
+    softmax(qk(st_tag), pp, pf);
+    pv(st_tag, pf);
   };
   for (int pp = 0; pp < n_pairs; pp += STAGES) {
     pair_step(std::integral_constant<int, 0>{}, pp);
@@ -625,23 +689,24 @@ __global__ void __launch_bounds__(256, FLASH_WG_PER_CU) flash_prefill_kernel(
     if (pp + 2 < n_pairs) pair_step(std::integral_constant<int, 2>{}, pp + 2);
   }
 
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    float L = l[c];
-    L = sum_x16_x32(L);
-    const int R = 32 * wid + 16 * c + r;
-    const int qi = q0 + R / G;
-    if (qi >= ql) continue;
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    uint16_t* orow = out + ((size_t)(qs + qi) * Hq + kvh * G + R % G) * kD + g4 * 4;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      u32x2 v;
-      v[0] = pack2(o[c][d][0] * inv, o[c][d][1] * inv);
-      v[1] = pack2(o[c][d][2] * inv, o[c][d][3] * inv);
-      *reinterpret_cast<u32x2*>(orow + d * 16) = v;
-    }
+  // the two lane halves' partial row sums; O^T element r of dim block d is dim
+  // 32 d + 8 (r >> 2) + 4 h + (r & 3) of q row R
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
+  if (!q_ok) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  uint16_t* orow = out + ((size_t)(qs + qi) * Hq + kvh * G + R % G) * kD + 4 * h;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      u32x2 v;
+      v[0] = pack2(o[d][4 * b] * inv, o[d][4 * b + 1] * inv);
+      v[1] = pack2(o[d][4 * b + 2] * inv, o[d][4 * b + 3] * inv);
+      *reinterpret_cast<u32x2*>(orow + 32 * d + 8 * b) = v;
+    }
 }
 
 void launch_flash_prefill(void* out, const void* q, const void* kc, const void* vc, const int* bt,
@@ -652,7 +717,7 @@ void launch_flash_prefill(void* out, const void* q, const void* kc, const void* 
   dim3 grid(num_ptiles * Hkv);
 #define MLOP_FLASH_CASE(GG)                                                                       \
   case GG:                                                                                        \
-    flash_prefill_kernel<GG><<<grid, 256, 0, st>>>(                                              \
+    flash32_prefill_kernel<GG, 2><<<grid, 256, 0, st>>>(                                          \
         (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt,        \
         bt_stride, ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks); \
     break;

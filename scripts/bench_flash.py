@@ -49,6 +49,7 @@ kc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
 vc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
 q = torch.randn(S * L, Hq, D, device=dev, dtype=bf)
 out = torch.empty_like(q)
+flops = 4 * S * (L * (L + 1) // 2) * D * Hq
 for _ in range(3):
     ops.paged_attention(q, kc, vc, m, out=out)
 torch.cuda.synchronize()
@@ -61,11 +62,10 @@ for _ in range(3):
     ev[1].record()
     ev[1].synchronize()
     best = min(best, ev[0].elapsed_time(ev[1]) / ITERS * 1e3)
-flops = 4 * S * (L * (L + 1) // 2) * D * Hq
-print(json.dumps(dict(S=S, L=L, tiles=len(pts), us=round(best, 1), tflops=round(flops / best / 1e6, 1))), flush=True)
+line = dict(S=S, L=L, tiles=len(pts), us=round(best, 1), tflops=round(flops / best / 1e6, 1))
 if os.environ.get("CHECK"):
     from mlopamd.ops import reference as ref
 
     exp = ref.paged_attention(q, kc, vc, m)
-    err = (out.float() - exp.float()).abs().max().item()
-    print(json.dumps(dict(max_abs_err=err)), flush=True)
+    line["max_abs_err"] = (out.float() - exp.float()).abs().max().item()
+print(json.dumps(line), flush=True)

@@ -186,6 +186,28 @@ def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
     close(out, ref.paged_attention(q, kc, vc, m), atol=2e-2, rtol=2e-2)
 
 
+def test_flash_prefill_growing_scores(gpu):
+    """Scores whose row max keeps growing along the keys (K scaled up page by page): the
+    deferred rescale (threshold 2^8) fires again and again, the path random data rarely takes."""
+    torch.manual_seed(1)
+    np.random.seed(1)
+    Hq, Hkv, L = 32, 8, 700
+    NB = (L + 15) // 16 + 8
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    m, T = make_meta(gpu, [L], [L], Hkv, Hq // Hkv, NB, flash_min_q=17)
+    # positive K growing with the LOGICAL page index (through the block table): q . k grows
+    # along the keys of the sequence
+    row = int(torch.nonzero(m.q_len == L)[0, 0])
+    n = (L + 15) // 16
+    pages = m.block_tables[row, :n].long()
+    kc = torch.zeros(NB, Hkv, 16, 128, device=gpu)
+    kc[pages] = torch.randn(n, Hkv, 16, 128, device=gpu).abs() * torch.linspace(0.2, 3.0, n, device=gpu).view(n, 1, 1, 1)
+    kc = kc.to(bf)
+    q = (torch.rand(T, Hq, 128, device=gpu) + 0.5).to(bf)
+    out = ops.paged_attention(q, kc, vc, m)
+    close(out, ref.paged_attention(q, kc, vc, m), atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
 @pytest.mark.parametrize("case", ["decode", "prefill", "mixed", "split", "split_fused"])
 def test_paged_attention(gpu, Hq, Hkv, case, attn_fused_all):
