@@ -279,6 +279,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(uint16_t* __restrict
   }
 }
 
+constexpr int kMaxSplits = 8;  // plan(): split-K factors are at most 8
 // split-K reduce fused with the decoder's residual add + RMSNorm (one row per block):
 //   y = bf16(sum_s slab[s][r]);  residual[r] = bf16(residual[r] + y);  out[r] = rmsnorm(residual[r]) * w
 template <int VPT>
@@ -290,18 +291,35 @@ __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
   const int nvec = N >> 3;
   float v[VPT][8];
   float ss = 0.f;
+  // the norm weights load with the slabs (one memory latency on the chain, not two)
+  u32x4 wpre[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) wpre[i] = *reinterpret_cast<const u32x4*>(w + vi * 8);
+  }
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int vi = threadIdx.x + i * blockDim.x;
     if (vi < nvec) {
+      // every slab's two loads (and the residual's) in flight together: a runtime-bound loop
+      // waited out one L2 round trip per split (~5 us per call at batch 8-64, twice per layer)
+      float4 x[kMaxSplits], y[kMaxSplits];
+#pragma unroll
+      for (int s = 0; s < kMaxSplits; ++s)
+        if (s < splits) {
+          const float4* p = reinterpret_cast<const float4*>(ws + ((size_t)s * M + r) * N + vi * 8);
+          x[s] = p[0];
+          y[s] = p[1];
+        }
+      const u32x4 res = *reinterpret_cast<const u32x4*>(residual + (size_t)r * N + vi * 8);
       float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int s = 0; s < splits; ++s) {
-        const float4* p = reinterpret_cast<const float4*>(ws + ((size_t)s * M + r) * N + vi * 8);
-        float4 x = p[0], y = p[1];
-        a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
-        a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
-      }
-      u32x4 res = *reinterpret_cast<const u32x4*>(residual + (size_t)r * N + vi * 8);
+#pragma unroll
+      for (int s = 0; s < kMaxSplits; ++s)
+        if (s < splits) {
+          a[0] += x[s].x; a[1] += x[s].y; a[2] += x[s].z; a[3] += x[s].w;
+          a[4] += y[s].x; a[5] += y[s].y; a[6] += y[s].z; a[7] += y[s].w;
+        }
       u32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -322,7 +340,7 @@ __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
   for (int i = 0; i < VPT; ++i) {
     const int vi = threadIdx.x + i * blockDim.x;
     if (vi < nvec) {
-      u32x4 wv = *reinterpret_cast<const u32x4*>(w + vi * 8);
+      const u32x4 wv = wpre[i];
       u32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1344,7 +1362,7 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
   if (gemv_takes(M, N, K, EPI_NONE)) return false;  // decode sizes: GEMV + add_rmsnorm (or the norm chain)
   int splits;
   const Plan p = plan(M, N, K, false, 0, 0);
-  if (p.splits <= 1 || (long)p.splits * M * N > ws_floats || N % 8) return false;
+  if (p.splits <= 1 || p.splits > kMaxSplits || (long)p.splits * M * N > ws_floats || N % 8) return false;
   launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
                                M, N, K, nullptr, 0, st);
   splits = p.splits;
