@@ -227,8 +227,8 @@ int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
 int64_t gemm_half_tile(int64_t set) { return mlop::gemm_half_tile((int)set); }
-void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits) {
-  mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits);
+void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits, int64_t stages) {
+  mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits, (int)stages);
 }
 void gemm_grouped_plan(int64_t bm, int64_t bn, int64_t stages, int64_t splits) {
   mlop::gemm_grouped_plan((int)bm, (int)bn, (int)stages, (int)splits);
@@ -743,7 +743,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
   m.def("gemm_half_tile(int set=-1) -> int", &gemm_half_tile);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
-  m.def("gemm_dense_plan(int variant, int bm, int bn, int splits) -> ()", &gemm_dense_plan);
+  m.def("gemm_dense_plan(int variant, int bm, int bn, int splits, int stages=0) -> ()", &gemm_dense_plan);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);
   m.def("gemm_small_tile(int set=-1) -> int", &gemm_small_tile);
   m.def("gemm_sk_mode(int set=-1) -> int", &gemm_sk_mode);

@@ -416,18 +416,19 @@ void gemm_grouped_plan(int bm, int bn, int stages, int splits) {
 
 // dense-plan override (scripts/bench_mid_m.py sweeps the mid-M projection tilings in one
 // process): variant (0 = gemm_kernel BM x BN, 1 = 256x256 two-stage, 3 = ping-pong, 5 =
-// four-wave), BM, BN, K splits (plain gemm_kernel only); -1 = the planner's own choice
-static int g_dp[4] = {-1, -1, -1, -1};
-void gemm_dense_plan(int variant, int bm, int bn, int splits) {
+// four-wave, 6 = four-wave half height), BM, BN, K splits (plain gemm_kernel only), LDS ring
+// depth of the small tiles (0 = the default); -1 = the planner's own choice
+static int g_dp[5] = {-1, -1, -1, -1, 0};
+void gemm_dense_plan(int variant, int bm, int bn, int splits, int stages) {
   if (variant >= 0 && variant != 0 && variant != 1 && variant != 3 && variant != 5 && variant != 6)
     throw std::runtime_error("gemm_dense_plan: variant must be 0, 1, 3, 5 or 6");
   if (variant == 0) {
-    static const int ok[][2] = {{64, 64}, {128, 64}, {256, 64}, {256, 128}};
+    static const int ok[][2] = {{16, 32}, {16, 64}, {32, 32}, {32, 64}, {64, 32}, {64, 64}, {128, 64}, {256, 64}, {256, 128}};
     bool found = false;
     for (const auto& t : ok) found = found || (t[0] == bm && t[1] == bn);
     if (!found) throw std::runtime_error("gemm_dense_plan: no dense config for this tile");
   }
-  g_dp[0] = variant, g_dp[1] = bm, g_dp[2] = bn, g_dp[3] = splits;
+  g_dp[0] = variant, g_dp[1] = bm, g_dp[2] = bn, g_dp[3] = splits, g_dp[4] = stages > 0 ? stages : 0;
 }
 
 // large-M kernel choice (plan() variants below), settable at run time (gemm_big_variant op) so
@@ -1164,7 +1165,7 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     p.variant = g_dp[0];
     p.BM = p.variant == 0 ? g_dp[1] : p.variant == 6 ? 128 : 256;
     p.BN = p.variant == 0 ? g_dp[2] : 256;
-    p.stages = 0;
+    p.stages = g_dp[4];
   }
   if (grouped && g_gp[0] > 0) {  // bench override (gemm_grouped_plan)
     p.BM = g_gp[0];

@@ -64,7 +64,7 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 int gemm_big_variant(int set);
 int gemm_half_tile(int set);
 void gemm_grouped_plan(int bm, int bn, int stages, int splits);
-void gemm_dense_plan(int variant, int bm, int bn, int splits);
+void gemm_dense_plan(int variant, int bm, int bn, int splits, int stages = 0);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip), variant 6 its 128x256
 // half-height tile; epi 0 / 1 / 3
 bool gemm_w4_ok(int M, int N, int K, int lda, int ldb, int ldc = 0);
