@@ -752,6 +752,35 @@ def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int, pro=None)
     return topw, topi, xp, offsets, src, inv
 
 
+def moe_dispatch_mid(x, router_w, top_k: int, e0: int, n_local: int, pro=None):
+    """Mid-size MoE dispatch in ONE launch (16 < T <= 1024 tokens; moe.hip): router GEMV + route
+    per token workgroup, the last workgroup sorts the slots by local expert.  Returns (topw, topi,
+    x, offsets, arow, inv) -- x itself (the normed rows under ``pro``) and arow [T*k], the token row
+    of each permuted row: the grouped GEMM reads x through it (``grouped_gemm(a_rows=arow)``),
+    there is no gathered copy -- or None when the shape is not on this path (nothing written)."""
+    if not x.is_cuda or not (16 < x.shape[0] <= 1024):
+        return None
+    _need_gpu()
+    T, H = x.shape
+    dev = x.device
+    _sk_reserve(dev)  # the launch's ticket counter lives in the stream-K scratch
+    topw = torch.empty(T, top_k, dtype=torch.float32, device=dev)
+    topi = torch.empty(T, top_k, dtype=torch.int32, device=dev)
+    offsets = torch.empty(n_local + 1, dtype=torch.int32, device=dev)
+    arow = torch.empty(T * top_k, dtype=torch.int32, device=dev)
+    inv = torch.empty(T * top_k, dtype=torch.int32, device=dev)
+    if pro is None:
+        xs = x.contiguous()
+        args = (xs, router_w.contiguous(), e0, n_local)
+    else:  # the kernel writes the normed rows to xs
+        y, residual, norm_w, eps = pro
+        xs = torch.empty_like(y)
+        args = (xs, router_w.contiguous(), e0, n_local, y.contiguous(), residual, norm_w, float(eps))
+    if not torch.ops.mlop.moe_dispatch_mid(topw, topi, offsets, arow, inv, *args):
+        return None
+    return topw, topi, xs, offsets, arow, inv
+
+
 def moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps: float):
     """residual <- residual + combine(y); returns rmsnorm(residual) * norm_w (one launch on GPU)."""
     if y.is_cuda:
@@ -772,18 +801,23 @@ def moe_combine(y, inv, topw):
     return out
 
 
-def grouped_gemm(xp, w, offsets, epi: int = EPI_NONE, avg_rows: int | None = None):
+def grouped_gemm(xp, w, offsets, epi: int = EPI_NONE, avg_rows: int | None = None, a_rows=None):
     """Per group e: rows offsets[e]:offsets[e+1] of xp times w[e]^T in ONE launch
-    (tiles enumerate (group, m-tile) pairs on device: no host sync, graph-safe)."""
+    (tiles enumerate (group, m-tile) pairs on device: no host sync, graph-safe).  ``a_rows``
+    [R]: permuted row r is row a_rows[r] of xp (R output rows; moe_dispatch_mid)."""
+    if a_rows is not None and not xp.is_cuda:
+        xp = xp[a_rows.long()]
+        a_rows = None
     if not xp.is_cuda:
         y = ref.grouped_gemm(xp, w, offsets)
         return ref.silu_mul(deinterleave_cols(y)) if epi == EPI_SILU_MUL else y
     _need_gpu()
     N = w.shape[1]
-    out = torch.empty(xp.shape[0], N if epi == EPI_NONE else N // 2, dtype=xp.dtype, device=xp.device)
-    if xp.shape[0] == 0:
+    R = xp.shape[0] if a_rows is None else a_rows.numel()
+    out = torch.empty(R, N if epi == EPI_NONE else N // 2, dtype=xp.dtype, device=xp.device)
+    if R == 0:
         return out
-    rows = avg_rows if avg_rows is not None else max(1, xp.shape[0] // max(1, w.shape[0]))
+    rows = avg_rows if avg_rows is not None else max(1, R // max(1, w.shape[0]))
     _sk_reserve(xp.device)
-    torch.ops.mlop.grouped_gemm(out, xp, w, offsets, rows, epi)
+    torch.ops.mlop.grouped_gemm(out, xp, w, offsets, rows, epi, a_rows)
     return out

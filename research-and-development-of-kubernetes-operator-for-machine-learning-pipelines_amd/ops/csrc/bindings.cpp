@@ -432,16 +432,23 @@ bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
 }
 
 // grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
-void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi) {
+void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi,
+                  std::optional<Tensor> a_rows) {
   check_bf16(out, "out"); check_bf16(a, "a"); check_bf16(w, "w"); check_i32(offsets, "offsets");
   TORCH_CHECK(a.dim() == 2 && w.dim() == 3 && w.size(2) == a.size(1), "a [M, K], w [G, N, K]");
-  const int64_t M = a.size(0), K = a.size(1), N = w.size(1), G = w.size(0);
+  // with a_rows the permuted rows are out's (M = out rows) and a holds the token rows they name
+  const int64_t M = a_rows ? out.size(0) : a.size(0), K = a.size(1), N = w.size(1), G = w.size(0);
   TORCH_CHECK(offsets.numel() == G + 1, "offsets must be [G + 1]");
   TORCH_CHECK(K % 64 == 0 && N % 32 == 0, "K % 64, N % 32");
   TORCH_CHECK(out.size(0) == M && out.size(1) == (epi == 0 ? N : N / 2), "out shape");
+  if (a_rows) {
+    check_i32(*a_rows, "a_rows");
+    TORCH_CHECK(a_rows->numel() >= M, "a_rows [M]: every permuted row's token row");
+  }
   c10::DeviceGuard g(a.device());
   mlop::launch_grouped_gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), offsets.data_ptr<int>(),
-                            (int)G, (int)M, (int)N, (int)K, (int)max_rows, (int)epi, cur_stream());
+                            (int)G, (int)M, (int)N, (int)K, (int)max_rows, (int)epi, cur_stream(),
+                            a_rows ? a_rows->data_ptr<int>() : nullptr);
 }
 
 void moe_route(Tensor topw, Tensor topi, Tensor logits) {
@@ -499,6 +506,36 @@ bool moe_dispatch_small(Tensor topw, Tensor topi, Tensor xp, Tensor offsets, Ten
                                   pro ? pro_y->data_ptr() : nullptr, pro ? pro_res->data_ptr() : nullptr,
                                   pro ? pro_w->data_ptr() : nullptr, (float)pro_eps, pro ? x.data_ptr() : nullptr,
                                   cur_stream());
+  return true;
+}
+
+// mid-size dispatch (16 < T <= 1024): router GEMV + route per workgroup, the last sorts; no
+// gather (arow: token row of each permuted row); false = not taken
+bool moe_dispatch_mid(Tensor topw, Tensor topi, Tensor offsets, Tensor arow, Tensor inv, Tensor x, Tensor router_w,
+                      int64_t e0, int64_t n_local, std::optional<Tensor> pro_y, std::optional<Tensor> pro_res,
+                      std::optional<Tensor> pro_w, double pro_eps) {
+  check_bf16(x, "x"); check_bf16(router_w, "router_w"); check_i32(topi, "topi");
+  check_i32(offsets, "offsets"); check_i32(arow, "arow"); check_i32(inv, "inv");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous(), "topw f32");
+  const int64_t T = x.size(0), H = x.size(1), E = router_w.size(0), k = topi.size(1);
+  if (!mlop::moe_dispatch_mid_takes((int)T, (int)E, (int)k, (int)H)) return false;
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && router_w.size(1) == H && router_w.is_contiguous(),
+              "x [T, H], router_w [E, H]");
+  TORCH_CHECK(topi.size(0) == T && topi.is_contiguous() && topw.numel() == T * k, "topi/topw [T, k]");
+  TORCH_CHECK(n_local >= 1 && n_local <= 64 && offsets.numel() == n_local + 1 && arow.numel() == T * k &&
+                  inv.numel() == T * k, "offsets / arow / inv");
+  const bool pro = pro_y.has_value();
+  if (pro) {  // x is the OUTPUT of the prologue here
+    check_bf16(*pro_y, "pro_y"); check_bf16(*pro_res, "pro_res"); check_bf16(*pro_w, "pro_w");
+    TORCH_CHECK(pro_y->numel() == T * H && pro_res->numel() == T * H && pro_w->numel() == H && H <= 8192,
+                "prologue y / residual [T, H], w [H]");
+  }
+  c10::DeviceGuard g(x.device());
+  mlop::launch_moe_dispatch_mid(topw.data_ptr<float>(), topi.data_ptr<int>(), offsets.data_ptr<int>(),
+                                arow.data_ptr<int>(), inv.data_ptr<int>(), x.data_ptr(), router_w.data_ptr(), (int)T,
+                                (int)E, (int)k, (int)H, (int)e0, (int)n_local, pro ? pro_y->data_ptr() : nullptr,
+                                pro ? pro_res->data_ptr() : nullptr, pro ? pro_w->data_ptr() : nullptr, (float)pro_eps,
+                                pro ? x.data_ptr() : nullptr, cur_stream());
   return true;
 }
 
@@ -766,7 +803,7 @@ TORCH_LIBRARY(mlop, m) {
         "Tensor pos, Tensor cos_sin, Tensor slots) -> bool");
   m.def("gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor(b!) ws, int epi) -> ()");
   m.def("grouped_gemm(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int max_rows, "
-        "int epi) -> ()");
+        "int epi, Tensor? a_rows=None) -> ()");
   m.def("gemm_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor a, Tensor w, Tensor norm_w, "
         "Tensor(c!) ws, float eps) -> bool");
   m.def("gemv_chain_supported(int M, int N, int K, int epi) -> bool", &gemv_chain_supported);
@@ -777,6 +814,9 @@ TORCH_LIBRARY(mlop, m) {
   m.def("moe_dispatch_small(Tensor(a!) topw, Tensor(b!) topi, Tensor(c!) xp, Tensor(d!) offsets, Tensor(e!) src, "
         "Tensor(f!) inv, Tensor(g!) x, Tensor router_w, int e0, int n_local, Tensor? pro_y=None, "
         "Tensor(h!)? pro_res=None, Tensor? pro_w=None, float pro_eps=0.0) -> bool");
+  m.def("moe_dispatch_mid(Tensor(a!) topw, Tensor(b!) topi, Tensor(c!) offsets, Tensor(d!) arow, Tensor(e!) inv, "
+        "Tensor(f!) x, Tensor router_w, int e0, int n_local, Tensor? pro_y=None, Tensor(g!)? pro_res=None, "
+        "Tensor? pro_w=None, float pro_eps=0.0) -> bool");
   m.def("moe_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor y, Tensor inv, Tensor topw, "
         "Tensor norm_w, float eps) -> bool");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
@@ -813,6 +853,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("gemm_rope_cache", &gemm_rope_cache);
   m.impl("moe_route", &moe_route);
   m.impl("moe_dispatch_small", &moe_dispatch_small);
+  m.impl("moe_dispatch_mid", &moe_dispatch_mid);
   m.impl("moe_combine_add_rmsnorm", &moe_combine_add_rmsnorm);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);

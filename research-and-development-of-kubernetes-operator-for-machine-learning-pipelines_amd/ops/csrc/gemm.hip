@@ -112,7 +112,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
     const int r = p * 8 + prow;
     const int pchunk = (lane & 7) ^ swz(r);     // source chunk for LDS slot (lane & 7)
     if (r < BM) {
-      const int gr = min(m0 + r, m_end - 1);
+      int gr = min(m0 + r, m_end - 1);
+      if (GROUPED && re.a_rows != nullptr) gr = re.a_rows[gr];
       src[i] = A + (size_t)gr * lda + kbeg + pchunk * 8;
     } else {
       const int gn = min(n0 + r - BM, N - 1);
@@ -643,7 +644,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
         // resource's num_records makes the LDS-DMA a dropped out-of-range access, still counted
         // by vmcnt (the counted waits stay exact) but fetching no line.  Their LDS rows hold
         // don't-care values that only ever reach accumulator rows that are never stored.
-        voff[h][i] = h < 2 ? (m0 + r < m_end ? (uint32_t)((size_t)(m0 + r) * lda * 2) + ch * 16 : 0x80000000u)
+        const int arow = (GROUPED && re.a_rows != nullptr && m0 + r < m_end) ? re.a_rows[m0 + r] : m0 + r;
+        voff[h][i] = h < 2 ? (m0 + r < m_end ? (uint32_t)((size_t)arow * lda * 2) + ch * 16 : 0x80000000u)
                            : (uint32_t)((size_t)min(n0 + r, N - 1) * ldb * 2) + ch * 16;
       }
     auto issue_half = [&](int buf, int h, int kt) {
@@ -1384,9 +1386,9 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
 }
 
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
-                         int M, int N, int K, int max_rows, int epi, hipStream_t st) {
+                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows) {
   if (M == 0) return;
-  if (gemv_grouped_takes(M, N, K, epi)) {  // MoE decode: stream only the routed experts' weights
+  if (a_rows == nullptr && gemv_grouped_takes(M, N, K, epi)) {  // MoE decode: stream only the routed experts' weights
     launch_gemv_grouped(A, B, C, offsets, n_groups, M, N, K, epi, st);
     return;
   }
@@ -1410,12 +1412,14 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
       ws = b->ws;
     }
   }
+  RopeEpi re{};
+  re.a_rows = a_rows;
   if (epi == EPI_NONE)
     launch_plan<EPI_NONE, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C, N,
-                                ws, M, N, K, offsets, n_groups, st);
+                                ws, M, N, K, offsets, n_groups, st, re);
   else
     launch_plan<EPI_SILU_MUL, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C,
-                                    N / 2, ws, M, N, K, offsets, n_groups, st);
+                                    N / 2, ws, M, N, K, offsets, n_groups, st, re);
   if (p.splits > 1) {
     const int outw = epi == EPI_NONE ? N : N / 2;
     const long total = (long)M * (outw / 8);

@@ -54,6 +54,9 @@ struct RopeEpi {
   float* ss_tot = nullptr;
   int* ss_cnt = nullptr;
   float ss_inv_k = 0.f, ss_eps = 0.f;
+  // grouped GEMM: A row of permuted row r is a_rows[r] (moe_dispatch_mid: the experts read the
+  // token rows in place, no gathered copy); nullptr = row r
+  const int* a_rows = nullptr;
 };
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
@@ -115,7 +118,14 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              const void* w, float eps, float* ws, long ws_floats, int M, int N,
                              int K, hipStream_t st);
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
-                         int M, int N, int K, int max_rows, int epi, hipStream_t st);
+                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows = nullptr);
+// mid-size MoE dispatch (16 < T <= 1024 tokens): router GEMV + route per token workgroup, the last
+// workgroup (agent-scope ticket) sorts the T*k slots by local expert -> offsets, inv and arow (the
+// token row of each permuted row: the grouped GEMM reads x through it, no gather)
+bool moe_dispatch_mid_takes(int T, int E, int k, int H);
+void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, int* inv, const void* x, const void* wr,
+                             int T, int E, int k, int H, int e0, int n_local, const void* pro_y, void* pro_res,
+                             const void* pro_w, float pro_eps, void* pro_xn, hipStream_t st);
 void launch_moe_route(float* topw, int* topi, const void* logits, int T, int E, int k,
                       hipStream_t st);
 void launch_moe_permute(void* xp, int* offsets, int* src, int* inv, const void* x, const int* topi,

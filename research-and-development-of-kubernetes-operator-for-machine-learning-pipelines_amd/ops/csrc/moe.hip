@@ -9,6 +9,8 @@
 // fp32 accumulate, one bf16 rounding), not an atomic scatter: bitwise
 // reproducible whatever order the permutation assigned rows in
 // (cdna_hip_programming.md App. B "Scatter / gather": store-then-sum form).
+#include <stdexcept>
+
 #include "common.h"
 #include "launch.h"
 
@@ -296,6 +298,183 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
   moe_dispatch_small_kernel<CH><<<1, 64 * kDispWaves, 0, st>>>(topw, topi, (uint16_t*)xp, offsets, src, inv, \
                                                                (const uint16_t*)x, (const uint16_t*)wr, T, E, k, \
                                                                H, e0, n_local, pro)
+  switch (H) {
+    case 1024: MLOP_DISP(2); break;
+    case 2048: MLOP_DISP(4); break;
+    case 4096: MLOP_DISP(8); break;
+    default: MLOP_DISP(16); break;
+  }
+#undef MLOP_DISP
+}
+
+// ---------------------------------------------------------------------------
+// Mid-size MoE dispatch (16 < T <= kMidT tokens) in ONE launch.  At batch 64 the separate
+// route is five ~5 us graph nodes per layer (router GEMM + its split-K reduce, top-k, sort,
+// gather: profiles/r05_windows.md), each a few us of work at most.  Here:
+//   workgroup w (tokens kMidTok w ..): the optional add + RMSNorm prologue, router logits
+//     (wave e = expert e: the router row loaded once, bf16-rounded as the separate projection
+//     stores them), softmax / top-k / renormalise -> topw, topi (written through, sc1);
+//   the LAST workgroup (one agent-scope ticket per launch, reset by it: graph-safe; dispatch
+//     order and co-residency are not assumed) counts the T*k slots per local expert and writes
+//     offsets, inv (slot -> permuted row) and arow (permuted row -> token row).
+// There is no gathered copy: the grouped gate_up GEMM reads x rows through arow.  Rows inside
+// an expert come in ticket order (LDS atomics), which changes no value: each row's product is
+// independent of its position and the combine gathers by inv.
+constexpr int kMidT = 1024, kMidTok = 4;
+
+template <int CH>
+__global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
+    float* __restrict__ topw, int* __restrict__ topi, int* __restrict__ offsets, int* __restrict__ arow,
+    int* __restrict__ inv, const uint16_t* __restrict__ x, const uint16_t* __restrict__ wr, int T, int E, int k,
+    int H, int e0, int n_local, MoePro pro, int* __restrict__ ticket) {
+  __shared__ float lg[kMidTok][kMaxE];
+  __shared__ int cnt[kMaxE + 1];
+  __shared__ int base[kMaxE + 1];
+  __shared__ float red[16];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int t0 = blockIdx.x * kMidTok, nt = min(kMidTok, T - t0);
+  if (pro.y != nullptr) {
+    // prologue for this workgroup's tokens: residual += y; x = rmsnorm(residual) * w
+    for (int t = t0; t < t0 + nt; ++t) {
+      u32x4 r[2];
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = (threadIdx.x + i * 64 * kDispWaves) * 8;
+        if (c >= H) continue;
+        const u32x4 a = *reinterpret_cast<const u32x4*>(pro.y + (size_t)t * H + c);
+        const u32x4 b = *reinterpret_cast<const u32x4*>(pro.residual + (size_t)t * H + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          r[i][q] = pack2(lo_bf(a[q]) + lo_bf(b[q]), hi_bf(a[q]) + hi_bf(b[q]));
+          ss += lo_bf(r[i][q]) * lo_bf(r[i][q]) + hi_bf(r[i][q]) * hi_bf(r[i][q]);
+        }
+        *reinterpret_cast<u32x4*>(pro.residual + (size_t)t * H + c) = r[i];
+      }
+      const float rs = rsqrtf(block_sum(ss, red) / (float)H + pro.eps);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = (threadIdx.x + i * 64 * kDispWaves) * 8;
+        if (c >= H) continue;
+        const u32x4 wv8 = *reinterpret_cast<const u32x4*>(pro.w + c);
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = pack2(bf2f(f2bf(lo_bf(r[i][q]) * rs)) * lo_bf(wv8[q]), bf2f(f2bf(hi_bf(r[i][q]) * rs)) * hi_bf(wv8[q]));
+        *reinterpret_cast<u32x4*>(pro.xn + (size_t)t * H + c) = o;
+      }
+    }
+    __syncthreads();  // this workgroup's x rows are read back below by other threads
+    x = pro.xn;
+  }
+  // router logits of this workgroup's tokens
+  for (int e = wv; e < E; e += kDispWaves) {
+    const uint16_t* we = wr + (size_t)e * H + lane * 8;
+    u32x4 b[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const u32x4*>(we + i * 512);
+    for (int t = 0; t < nt; ++t) {
+      const uint16_t* xt = x + (size_t)(t0 + t) * H + lane * 8;
+      u32x4 a[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) a[i] = *reinterpret_cast<const u32x4*>(xt + i * 512);
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc += lo_bf(a[i][q]) * lo_bf(b[i][q]) + hi_bf(a[i][q]) * hi_bf(b[i][q]);
+      acc = wave_sum(acc);
+      if (lane == 0) lg[t][e] = bf2f(f2bf(acc));
+    }
+  }
+  __syncthreads();
+  const auto rs_topi = __builtin_amdgcn_make_buffer_rsrc((void*)topi, 0, T * k * 4, 0x00020000);
+  if (threadIdx.x < nt) {  // moe_route_kernel's math
+    const int t = threadIdx.x;
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) mx = fmaxf(mx, lg[t][e]);
+    float sum = 0.f;
+    for (int e = 0; e < E; ++e) sum += __expf(lg[t][e] - mx);
+    const float rinv = 1.f / sum;
+    float picked = 0.f, wsel[8];
+    int isel[8];
+    unsigned long long used = 0ull;
+    for (int j = 0; j < k; ++j) {
+      int best = 0;
+      float bv = -1.f;
+      for (int e = 0; e < E; ++e) {
+        const float v = __expf(lg[t][e] - mx);
+        if (!((used >> e) & 1ull) && v > bv) { bv = v; best = e; }
+      }
+      used |= 1ull << best;
+      isel[j] = best;
+      wsel[j] = bv * rinv;
+      picked += bv * rinv;
+    }
+    const float rn = picked > 0.f ? 1.f / picked : 0.f;
+    for (int j = 0; j < k; ++j) {
+      topw[(t0 + t) * k + j] = wsel[j] * rn;
+      // written through (sc1) for the sorting workgroup, which may sit on another XCD
+      __builtin_amdgcn_raw_buffer_store_b32(isel[j], rs_topi, (uint32_t)(((t0 + t) * k + j) * 4), 0, 16 /* sc1 */);
+    }
+  }
+  // every wave drains its stores, then one lane takes the ticket (the K-half hand-off of
+  // gemm_w4.hip: sc1 stores, vmcnt(0), barrier, relaxed agent-scope counter, sc1 loads)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  __syncthreads();
+  if (!last) return;
+  // counting sort of the T*k slots by local expert
+  const int n_slots = T * k;
+  for (int e = threadIdx.x; e <= n_local; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int s = threadIdx.x; s < n_slots; s += blockDim.x) {
+    const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_topi, (uint32_t)(s * 4), 0, 16 /* sc1 */) - e0;
+    inv[s] = (e >= 0 && e < n_local) ? atomicAdd(&cnt[e], 1) : -1;  // rank in its expert
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < n_local; ++e) {
+      base[e] = acc;
+      offsets[e] = acc;
+      acc += cnt[e];
+    }
+    offsets[n_local] = acc;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < n_slots; s += blockDim.x) {
+    const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_topi, (uint32_t)(s * 4), 0, 16 /* sc1 */) - e0;
+    if (e >= 0 && e < n_local) {
+      const int row = base[e] + inv[s];
+      inv[s] = row;
+      arow[row] = s / k;
+    }
+  }
+}
+
+bool moe_dispatch_mid_takes(int T, int E, int k, int H) {
+  return T > kSmallT && T <= kMidT && E <= kMaxE && k <= 8 && (H == 1024 || H == 2048 || H == 4096 || H == 8192);
+}
+
+void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, int* inv, const void* x, const void* wr,
+                             int T, int E, int k, int H, int e0, int n_local, const void* pro_y, void* pro_res,
+                             const void* pro_w, float pro_eps, void* pro_xn, hipStream_t st) {
+  float* ws = nullptr;
+  int* ticket = nullptr;
+  int cus = 0;
+  if (!gemm_sk_scratch(&ws, &ticket, &cus)) throw std::runtime_error("moe_dispatch_mid: stream-K scratch not reserved");
+  const MoePro pro{(const uint16_t*)pro_y, (uint16_t*)pro_res, (const uint16_t*)pro_w, pro_eps, (uint16_t*)pro_xn};
+  const int grid = (T + kMidTok - 1) / kMidTok;
+#define MLOP_DISP(CH)                                                                                           \
+  moe_dispatch_mid_kernel<CH><<<grid, 64 * kDispWaves, 0, st>>>(topw, topi, offsets, arow, inv, (const uint16_t*)x, \
+                                                                (const uint16_t*)wr, T, E, k, H, e0, n_local, pro, ticket)
   switch (H) {
     case 1024: MLOP_DISP(2); break;
     case 2048: MLOP_DISP(4); break;

@@ -37,12 +37,15 @@ def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None
     ``dispatched``: (xp, offsets, inv) from ops.moe_dispatch_small; ``combine=False``
     returns (y, inv) so the caller can fuse the weighted gather into its next kernel."""
     T, k = topi.shape
+    arow = None
     if dispatched is None:
         xp, offsets, src, inv = ops.moe_permute(x, topi, e0, n_local)
+    elif len(dispatched) == 4:  # moe_dispatch_mid: the token rows, read through arow (no gather)
+        xp, offsets, inv, arow = dispatched
     else:
         xp, offsets, inv = dispatched
     avg = max(1, (T * k) // max(1, n_local))
-    a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg)
+    a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg, a_rows=arow)
     y = ops.grouped_gemm(a, w2, offsets, avg_rows=avg)
     return ops.moe_combine(y, inv, topw) if combine else (y, inv)
 
@@ -50,18 +53,28 @@ def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None
 def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int, residual, norm_w, eps: float,
                          pre=None):
     """Single-rank MoE block followed by the decoder's residual add + RMSNorm.  At decode
-    sizes the router GEMV, routing, sort and gather are ONE launch (moe_dispatch_small) and
-    the weighted combine rides in the add + RMSNorm launch: 6 MoE glue launches -> 2.
+    sizes the router GEMV, routing, sort and gather are ONE launch (moe_dispatch_small; at
+    16 < T <= 1024 moe_dispatch_mid, whose experts read x in place) and the weighted combine
+    rides in the add + RMSNorm launch: 6 MoE glue launches -> 2.
     ``pre=(o, pre_norm_w)``: x is not formed yet; the block's own input add + RMSNorm
     (residual += o, x = rmsnorm(residual)) becomes the dispatch launch's prologue."""
+    mid = None
     if pre is not None:
         o, pre_w = pre
         d = ops.moe_dispatch_small(o, router_w, top_k, e0, n_local, pro=(o, residual, pre_w, eps))
         if d is None:
+            mid = ops.moe_dispatch_mid(o, router_w, top_k, e0, n_local, pro=(o, residual, pre_w, eps))
+        if d is None and mid is None:
             x = ops.add_rmsnorm(o, residual, pre_w, eps)
     else:
         d = ops.moe_dispatch_small(x, router_w, top_k, e0, n_local)
-    if d is None:
+        if d is None:
+            mid = ops.moe_dispatch_mid(x, router_w, top_k, e0, n_local)
+    if mid is not None:  # 16 < T <= 1024: one dispatch launch, the experts read x through arow
+        topw, topi, xs, offsets, arow, inv = mid
+        y, inv = local_experts(xs, topw, topi, w13, w2, e0, n_local, dispatched=(xs, offsets, inv, arow),
+                               combine=False)
+    elif d is None:
         topw, topi = route(x, router_w, top_k)
         y, inv = local_experts(x, topw, topi, w13, w2, e0, n_local, combine=False)
     else:

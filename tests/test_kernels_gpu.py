@@ -789,6 +789,96 @@ def test_moe_dispatch_small_prologue(gpu, T, E, k, H):
     close(xp[:T * k], xp_r[:T * k], atol=2e-2, rtol=2e-2)
 
 
+def _check_mid_layout(topi, off, arow, inv, T, k, e0, nl):
+    """offsets = per-local-expert counts; every local slot s has a row in its expert's range
+    whose token row is s // k; non-local slots are -1; rows are a permutation of [0, n)."""
+    ti = topi.flatten().cpu().long() - e0
+    local = (ti >= 0) & (ti < nl)
+    counts = torch.bincount(ti[local], minlength=nl)
+    assert torch.equal(off.cpu().long(), torch.cat([torch.zeros(1, dtype=torch.long), counts.cumsum(0)]))
+    invc = inv.cpu().long()
+    assert torch.all(invc[~local] == -1)
+    rows = invc[local]
+    assert torch.equal(rows.sort().values, torch.arange(int(off[-1])))
+    lo, hi = off.cpu().long()[ti[local]], off.cpu().long()[ti[local] + 1]
+    assert torch.all((rows >= lo) & (rows < hi))
+    slots = torch.nonzero(local).flatten()
+    assert torch.equal(arow.cpu().long()[rows], slots // k)
+
+
+@pytest.mark.parametrize("T,E,k,H", [(17, 8, 2, 4096), (64, 8, 2, 4096), (130, 8, 2, 1024), (1024, 8, 2, 4096),
+                                     (40, 16, 4, 2048), (300, 8, 2, 8192)])
+def test_moe_dispatch_mid(gpu, T, E, k, H):
+    """Multi-workgroup dispatch (router GEMV + route per workgroup, last-workgroup sort, no
+    gather) against the separate router projection + moe_route, for the full and a partial
+    (expert-parallel) local expert range; twice in a row (the ticket resets itself)."""
+    torch.manual_seed(T * E + H)
+    x = torch.randn(T, H, device=gpu, dtype=bf)
+    wr = (0.05 * torch.randn(E, H, device=gpu)).to(bf)
+    logits = (x.float() @ wr.float().t()).to(bf)
+    p = torch.softmax(logits.float(), -1)
+    for e0, nl in [(0, E), (E // 2, E - E // 2), (0, E)]:
+        topw, topi, xs, off, arow, inv = ops.moe_dispatch_mid(x, wr, k, e0, nl)
+        assert xs.data_ptr() == x.data_ptr()  # no copy of the token rows
+        w_ref, i_ref = ops.moe_route(logits, k)
+        close(p.gather(1, topi.long()), p.gather(1, i_ref.long()), atol=1e-3, rtol=1e-3)
+        close(topw, w_ref, atol=2e-3, rtol=2e-3)
+        _check_mid_layout(topi, off, arow, inv, T, k, e0, nl)
+
+
+@pytest.mark.parametrize("T,H", [(33, 4096), (200, 2048)])
+def test_moe_dispatch_mid_prologue(gpu, T, H):
+    """Mid dispatch with the residual add + RMSNorm prologue == add_rmsnorm, then route."""
+    E, k = 8, 2
+    torch.manual_seed(T + H)
+    o = torch.randn(T, H, device=gpu, dtype=bf)
+    res = torch.randn(T, H, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    wr = (0.05 * torch.randn(E, H, device=gpu)).to(bf)
+    x_ref, res_ref = ref.add_rmsnorm(o, res, nw, 1e-5)
+    r2 = res.clone()
+    topw, topi, xs, off, arow, inv = ops.moe_dispatch_mid(o, wr, k, 0, E, pro=(o, r2, nw, 1e-5))
+    close(r2, res_ref, atol=0, rtol=0)
+    close(xs, x_ref, atol=2e-2, rtol=2e-2)
+    p = torch.softmax(x_ref.float() @ wr.float().t(), -1)
+    w_ref, i_ref = ops.moe_route((x_ref.float() @ wr.float().t()).to(bf), k)
+    close(p.gather(1, topi.long()), p.gather(1, i_ref.long()), atol=2e-3, rtol=2e-3)
+    _check_mid_layout(topi, off, arow, inv, T, k, 0, E)
+
+
+@pytest.mark.parametrize("T,H,I", [(24, 1024, 512), (64, 4096, 1024), (300, 1024, 512)])
+def test_moe_block_mid_dispatch_matches_fp32(gpu, T, H, I):
+    """The whole single-rank MoE block through the mid dispatch (grouped GEMMs reading x via
+    arow, combine + add + RMSNorm) against the fp32 reference MoE on the same routing."""
+    from mlopamd.parallel import moe as moe_mod
+
+    E, k = 8, 2
+    torch.manual_seed(T + I)
+    x = torch.randn(T, H, device=gpu, dtype=bf)
+    wr = (0.05 * torch.randn(E, H, device=gpu)).to(bf)
+    w13 = (0.03 * torch.randn(E, 2 * I, H, device=gpu)).to(bf)
+    w2 = (0.03 * torch.randn(E, H, I, device=gpu)).to(bf)
+    res = torch.randn(T, H, device=gpu, dtype=bf)
+    nw = (1 + 0.1 * torch.randn(H, device=gpu)).to(bf)
+    mid = ops.moe_dispatch_mid(x, wr, k, 0, E)
+    assert mid is not None
+    topw, topi = mid[0], mid[1]
+    r2 = res.clone()
+    out = moe_mod.moe_forward_add_norm(x, wr, w13, w2, k, 0, E, r2, nw, 1e-5)
+    # fp32 oracle on the kernel's own routing (bf16 logits may tie differently in torch)
+    xf = x.float()
+    y = torch.zeros(T, H, device=gpu)
+    for t in range(T):
+        for j in range(k):
+            e = int(topi[t, j])
+            gu = xf[t] @ w13[e].float().t()  # w13 rows gate / up interleaved in groups of 16
+            h = ref.silu_mul(ops.deinterleave_cols(gu.to(bf).view(1, -1))).float().view(-1)
+            y[t] += topw[t, j] * (h.to(bf).float() @ w2[e].float().t())
+    exp_out, exp_res = ref.add_rmsnorm(y.to(bf), res, nw, 1e-5)
+    close(r2, exp_res, atol=3e-2, rtol=3e-2)
+    close(out, exp_out, atol=5e-2, rtol=5e-2)
+
+
 @pytest.mark.parametrize("T,k,H", [(1, 2, 4096), (9, 2, 4096), (3, 1, 8192), (16, 8, 2048)])
 def test_moe_combine_add_rmsnorm(gpu, T, k, H):
     torch.manual_seed(H + T)
