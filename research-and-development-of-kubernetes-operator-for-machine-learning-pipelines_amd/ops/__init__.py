@@ -791,6 +791,22 @@ def moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps: float):
     return add_rmsnorm(moe_combine(y, inv, topw), residual, norm_w, eps)
 
 
+def moe_down_combine_add_rmsnorm(a, w2, offsets, inv, topw, residual, norm_w, eps: float, avg_rows: int):
+    """The MoE block's tail: y = grouped down GEMM of the SiLU-mul rows ``a``; residual <-
+    residual + combine(y); returns rmsnorm(residual) * norm_w.  On GPU the combine sums the
+    GEMM's split-K partials itself (one launch fewer than GEMM + reduce + combine)."""
+    if a.is_cuda and a.shape[0] > 0:
+        _need_gpu()
+        _sk_reserve(a.device)
+        out = torch.empty_like(residual)
+        y = torch.empty(a.shape[0], w2.shape[1], dtype=a.dtype, device=a.device)
+        if torch.ops.mlop.moe_down_combine_add_rmsnorm(out, residual, y, a, w2, offsets, avg_rows, inv,
+                                                       topw.contiguous(), norm_w, eps):
+            return out
+    y = grouped_gemm(a, w2, offsets, avg_rows=avg_rows)
+    return moe_combine_add_rmsnorm(y, inv, topw, residual, norm_w, eps)
+
+
 def moe_combine(y, inv, topw):
     """out[t] = sum_j topw[t,j] * y[inv[t*k+j]] (inv < 0 skipped), fp32 accumulate."""
     if not y.is_cuda:

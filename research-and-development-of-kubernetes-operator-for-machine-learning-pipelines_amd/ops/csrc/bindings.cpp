@@ -553,6 +553,26 @@ bool moe_combine_add_rmsnorm(Tensor out, Tensor residual, Tensor y, Tensor inv, 
                                               (float)eps, (int)T, (int)k, (int)H, cur_stream());
 }
 
+// grouped down GEMM + combine + residual add + RMSNorm: the combine sums the GEMM's split-K slabs
+// itself (y is written only when the GEMM does not split); false = shape not supported
+bool moe_down_combine_add_rmsnorm(Tensor out, Tensor residual, Tensor y, Tensor a, Tensor w2, Tensor offsets,
+                                  int64_t max_rows, Tensor inv, Tensor topw, Tensor norm_w, double eps) {
+  check_bf16(out, "out"); check_bf16(residual, "residual"); check_bf16(y, "y"); check_bf16(a, "a");
+  check_bf16(w2, "w2"); check_bf16(norm_w, "norm_w"); check_i32(offsets, "offsets"); check_i32(inv, "inv");
+  TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.dim() == 2, "topw");
+  TORCH_CHECK(a.dim() == 2 && w2.dim() == 3 && w2.size(2) == a.size(1), "a [R, I], w2 [G, H, I]");
+  const int64_t R = a.size(0), I = a.size(1), H = w2.size(1), G = w2.size(0);
+  const int64_t T = topw.size(0), k = topw.size(1);
+  TORCH_CHECK(offsets.numel() == G + 1 && I % 64 == 0 && H % 32 == 0, "offsets [G + 1], I % 64, H % 32");
+  TORCH_CHECK(y.size(0) == R && y.size(1) == H && out.numel() == T * H && residual.numel() == T * H &&
+                  inv.numel() == T * k && norm_w.numel() == H, "y [R, H], out / residual [T, H]");
+  c10::DeviceGuard g(a.device());
+  return mlop::launch_moe_down_combine_add_rmsnorm(
+      out.data_ptr(), residual.data_ptr(), y.data_ptr(), a.data_ptr(), w2.data_ptr(), offsets.data_ptr<int>(), (int)G,
+      (int)R, (int)H, (int)I, (int)max_rows, inv.data_ptr<int>(), topw.data_ptr<float>(), norm_w.data_ptr(),
+      (float)eps, (int)T, (int)k, cur_stream());
+}
+
 void moe_combine(Tensor out, Tensor y, Tensor inv, Tensor topw) {
   check_bf16(out, "out"); check_bf16(y, "y"); check_i32(inv, "inv");
   TORCH_CHECK(topw.scalar_type() == at::kFloat && topw.is_contiguous() && topw.dim() == 2, "topw");
@@ -817,6 +837,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("moe_dispatch_mid(Tensor(a!) topw, Tensor(b!) topi, Tensor(c!) offsets, Tensor(d!) arow, Tensor(e!) inv, "
         "Tensor(f!) x, Tensor router_w, int e0, int n_local, Tensor? pro_y=None, Tensor(g!)? pro_res=None, "
         "Tensor? pro_w=None, float pro_eps=0.0) -> bool");
+  m.def("moe_down_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor(c!) y, Tensor a, Tensor w2, "
+        "Tensor offsets, int max_rows, Tensor inv, Tensor topw, Tensor norm_w, float eps) -> bool");
   m.def("moe_combine_add_rmsnorm(Tensor(a!) out, Tensor(b!) residual, Tensor y, Tensor inv, Tensor topw, "
         "Tensor norm_w, float eps) -> bool");
   m.def("argmax(Tensor(a!) out, Tensor logits) -> ()");
@@ -854,6 +876,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("moe_route", &moe_route);
   m.impl("moe_dispatch_small", &moe_dispatch_small);
   m.impl("moe_dispatch_mid", &moe_dispatch_mid);
+  m.impl("moe_down_combine_add_rmsnorm", &moe_down_combine_add_rmsnorm);
   m.impl("moe_combine_add_rmsnorm", &moe_combine_add_rmsnorm);
   m.impl("moe_permute", &moe_permute);
   m.impl("moe_combine", &moe_combine);

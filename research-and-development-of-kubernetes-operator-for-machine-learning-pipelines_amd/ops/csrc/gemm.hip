@@ -1386,9 +1386,11 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
 }
 
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
-                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows) {
+                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows,
+                         float** defer_ws, int* defer_splits) {
+  if (defer_splits) *defer_splits = 1;
   if (M == 0) return;
-  if (a_rows == nullptr && gemv_grouped_takes(M, N, K, epi)) {  // MoE decode: stream only the routed experts' weights
+  if (a_rows == nullptr && defer_splits == nullptr && gemv_grouped_takes(M, N, K, epi)) {  // MoE decode: stream only the routed experts' weights
     launch_gemv_grouped(A, B, C, offsets, n_groups, M, N, K, epi, st);
     return;
   }
@@ -1420,7 +1422,10 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
   else
     launch_plan<EPI_SILU_MUL, true>(p, (const uint16_t*)A, K, (const uint16_t*)B, K, (uint16_t*)C,
                                     N / 2, ws, M, N, K, offsets, n_groups, st, re);
-  if (p.splits > 1) {
+  if (p.splits > 1 && defer_splits != nullptr && epi == EPI_NONE) {  // the caller sums the slabs
+    *defer_ws = ws;
+    *defer_splits = p.splits;
+  } else if (p.splits > 1) {
     const int outw = epi == EPI_NONE ? N : N / 2;
     const long total = (long)M * (outw / 8);
     const int g = (int)std::min<long>((total + 255) / 256, 4096);

@@ -118,7 +118,12 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              const void* w, float eps, float* ws, long ws_floats, int M, int N,
                              int K, hipStream_t st);
 void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offsets, int n_groups,
-                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows = nullptr);
+                         int M, int N, int K, int max_rows, int epi, hipStream_t st, const int* a_rows = nullptr,
+                         float** defer_ws = nullptr, int* defer_splits = nullptr);
+bool launch_moe_down_combine_add_rmsnorm(void* out, void* residual, void* y, const void* a, const void* w2,
+                                         const int* offsets, int n_groups, int R, int H, int I, int max_rows,
+                                         const int* inv, const float* topw, const void* norm_w, float eps, int T,
+                                         int k, hipStream_t st);
 // mid-size MoE dispatch (16 < T <= 1024 tokens): router GEMV + route per token workgroup, the last
 // workgroup (agent-scope ticket) sorts the T*k slots by local expert -> offsets, inv and arow (the
 // token row of each permuted row: the grouped GEMM reads x through it, no gather)

@@ -320,7 +320,7 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
 // There is no gathered copy: the grouped gate_up GEMM reads x rows through arow.  Rows inside
 // an expert come in ticket order (LDS atomics), which changes no value: each row's product is
 // independent of its position and the combine gathers by inv.
-constexpr int kMidT = 1024, kMidTok = 4;
+constexpr int kMidT = 1024, kMidTok = 2;
 
 template <int CH>
 __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
@@ -374,18 +374,23 @@ __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
     u32x4 b[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const u32x4*>(we + i * 512);
-    for (int t = 0; t < nt; ++t) {
-      const uint16_t* xt = x + (size_t)(t0 + t) * H + lane * 8;
-      u32x4 a[CH];
+    // both token rows' chunks in flight together with the router row's (one latency, not three)
+    u32x4 a[kMidTok][CH];
 #pragma unroll
-      for (int i = 0; i < CH; ++i) a[i] = *reinterpret_cast<const u32x4*>(xt + i * 512);
+    for (int t = 0; t < kMidTok; ++t)
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        a[t][i] = *reinterpret_cast<const u32x4*>(x + (size_t)(t0 + min(t, nt - 1)) * H + lane * 8 + i * 512);
+#pragma unroll
+    for (int t = 0; t < kMidTok; ++t) {
       float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < CH; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc += lo_bf(a[i][q]) * lo_bf(b[i][q]) + hi_bf(a[i][q]) * hi_bf(b[i][q]);
+        for (int q = 0; q < 4; ++q)
+          acc += lo_bf(a[t][i][q]) * lo_bf(b[i][q]) + hi_bf(a[t][i][q]) * hi_bf(b[i][q]);
       acc = wave_sum(acc);
-      if (lane == 0) lg[t][e] = bf2f(f2bf(acc));
+      if (lane == 0 && t < nt) lg[t][e] = bf2f(f2bf(acc));
     }
   }
   __syncthreads();
@@ -488,10 +493,13 @@ void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, in
 // elements per thread: at decode sizes every row's reads are in flight at once):
 //   m = bf16(sum_j topw[t, j] * y[inv[t*k + j]])   (moe_combine_kernel's rounding)
 //   residual[t] = bf16(residual[t] + m);  out[t] = bf16(bf16(residual[t] * rsqrt(mean sq + eps)) * w)
+// SLABS: y is not formed; the grouped down GEMM's fp32 split-K slabs ws[s][R][H] are summed
+// here (splitk_reduce_kernel's rounding: one bf16 rounding of the sum), one launch fewer
+template <bool SLABS>
 __global__ void __launch_bounds__(1024) moe_combine_add_rmsnorm_kernel(
     uint16_t* __restrict__ out, uint16_t* __restrict__ residual, const uint16_t* __restrict__ y,
     const int* __restrict__ inv, const float* __restrict__ topw, const uint16_t* __restrict__ w, float eps,
-    int k, int H) {
+    int k, int H, const float* __restrict__ ws, int splits, int R) {
   __shared__ float scratch[16];
   const int t = blockIdx.x, c = threadIdx.x * 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -499,7 +507,20 @@ __global__ void __launch_bounds__(1024) moe_combine_add_rmsnorm_kernel(
     const int row = inv[t * k + j];
     if (row < 0) continue;
     const float wt = topw[t * k + j];
-    const u32x4 v = *reinterpret_cast<const u32x4*>(y + (size_t)row * H + c);
+    u32x4 v;
+    if constexpr (SLABS) {
+      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int sp = 0; sp < splits; ++sp) {
+        const float4* p = reinterpret_cast<const float4*>(ws + ((size_t)sp * R + row) * H + c);
+        const float4 x0 = p[0], x1 = p[1];
+        a[0] += x0.x; a[1] += x0.y; a[2] += x0.z; a[3] += x0.w;
+        a[4] += x1.x; a[5] += x1.y; a[6] += x1.z; a[7] += x1.w;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = pack2(a[2 * q], a[2 * q + 1]);
+    } else {
+      v = *reinterpret_cast<const u32x4*>(y + (size_t)row * H + c);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       acc[2 * q] += wt * lo_bf(v[q]);
@@ -529,8 +550,29 @@ bool launch_moe_combine_add_rmsnorm(void* out, void* residual, const void* y, co
                                     const void* w, float eps, int T, int k, int H, hipStream_t st) {
   if (T == 0) return true;
   if (H % 512 || H > 8192) return false;  // whole 64-thread waves, <= 1024 threads
-  moe_combine_add_rmsnorm_kernel<<<T, H / 8, 0, st>>>((uint16_t*)out, (uint16_t*)residual, (const uint16_t*)y,
-                                                      inv, topw, (const uint16_t*)w, eps, k, H);
+  moe_combine_add_rmsnorm_kernel<false><<<T, H / 8, 0, st>>>((uint16_t*)out, (uint16_t*)residual, (const uint16_t*)y,
+                                                             inv, topw, (const uint16_t*)w, eps, k, H, nullptr, 0, 0);
+  return true;
+}
+
+// the MoE block's tail in two launches: grouped down GEMM (its split-K partials left in the
+// slab buffer) + the combine that sums them, adds into the residual and normalises.  y [R, H]
+// is written only when the GEMM does not split.
+bool launch_moe_down_combine_add_rmsnorm(void* out, void* residual, void* y, const void* a, const void* w2,
+                                         const int* offsets, int n_groups, int R, int H, int I, int max_rows,
+                                         const int* inv, const float* topw, const void* norm_w, float eps, int T,
+                                         int k, hipStream_t st) {
+  if (T == 0) return true;
+  if (H % 512 || H > 8192) return false;
+  float* ws = nullptr;
+  int splits = 1;
+  launch_grouped_gemm(a, w2, y, offsets, n_groups, R, H, I, max_rows, 0, st, nullptr, &ws, &splits);
+  if (splits > 1)
+    moe_combine_add_rmsnorm_kernel<true><<<T, H / 8, 0, st>>>((uint16_t*)out, (uint16_t*)residual, nullptr, inv, topw,
+                                                              (const uint16_t*)norm_w, eps, k, H, ws, splits, R);
+  else
+    moe_combine_add_rmsnorm_kernel<false><<<T, H / 8, 0, st>>>((uint16_t*)out, (uint16_t*)residual, (const uint16_t*)y,
+                                                               inv, topw, (const uint16_t*)norm_w, eps, k, H, nullptr, 0, 0);
   return true;
 }
 

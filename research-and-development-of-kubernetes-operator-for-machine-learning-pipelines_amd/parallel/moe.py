@@ -29,13 +29,15 @@ def route(x: torch.Tensor, router_w: torch.Tensor, top_k: int):
     return ops.moe_route(logits, top_k)
 
 
-def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None, combine: bool = True):
+def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None, combine=True):
     """Sum over the top-k slots whose expert is in [e0, e0+n_local) of w * expert(x).
 
     permute (K12) -> grouped gate_up GEMM with fused SiLU-mul (K13, w13 rows
     gate/up-interleaved) -> grouped down GEMM (K13) -> weighted gather (K14).
     ``dispatched``: (xp, offsets, inv) from ops.moe_dispatch_small; ``combine=False``
-    returns (y, inv) so the caller can fuse the weighted gather into its next kernel."""
+    returns (y, inv) so the caller can fuse the weighted gather into its next kernel;
+    ``combine=(residual, norm_w, eps)`` runs the down GEMM, the combine and the residual add +
+    RMSNorm as one op (ops.moe_down_combine_add_rmsnorm) and returns the normed rows."""
     T, k = topi.shape
     arow = None
     if dispatched is None:
@@ -46,6 +48,9 @@ def local_experts(x, topw, topi, w13, w2, e0: int, n_local: int, dispatched=None
         xp, offsets, inv = dispatched
     avg = max(1, (T * k) // max(1, n_local))
     a = ops.grouped_gemm(xp, w13, offsets, epi=ops.EPI_SILU_MUL, avg_rows=avg, a_rows=arow)
+    if isinstance(combine, tuple):
+        residual, norm_w, eps = combine
+        return ops.moe_down_combine_add_rmsnorm(a, w2, offsets, inv, topw, residual, norm_w, eps, avg)
     y = ops.grouped_gemm(a, w2, offsets, avg_rows=avg)
     return ops.moe_combine(y, inv, topw) if combine else (y, inv)
 
@@ -72,9 +77,9 @@ def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int
             mid = ops.moe_dispatch_mid(x, router_w, top_k, e0, n_local)
     if mid is not None:  # 16 < T <= 1024: one dispatch launch, the experts read x through arow
         topw, topi, xs, offsets, arow, inv = mid
-        y, inv = local_experts(xs, topw, topi, w13, w2, e0, n_local, dispatched=(xs, offsets, inv, arow),
-                               combine=False)
-    elif d is None:
+        return local_experts(xs, topw, topi, w13, w2, e0, n_local, dispatched=(xs, offsets, inv, arow),
+                             combine=(residual, norm_w, eps))
+    if d is None:
         topw, topi = route(x, router_w, top_k)
         y, inv = local_experts(x, topw, topi, w13, w2, e0, n_local, combine=False)
     else:
