@@ -753,12 +753,12 @@ def moe_dispatch_small(x, router_w, top_k: int, e0: int, n_local: int, pro=None)
 
 
 def moe_dispatch_mid(x, router_w, top_k: int, e0: int, n_local: int, pro=None):
-    """Mid-size MoE dispatch in ONE launch (16 < T <= 1024 tokens; moe.hip): router GEMV + route
+    """MoE dispatch in ONE launch (16 < T <= 16384 tokens; moe.hip): router GEMV + route
     per token workgroup, the last workgroup sorts the slots by local expert.  Returns (topw, topi,
     x, offsets, arow, inv) -- x itself (the normed rows under ``pro``) and arow [T*k], the token row
     of each permuted row: the grouped GEMM reads x through it (``grouped_gemm(a_rows=arow)``),
     there is no gathered copy -- or None when the shape is not on this path (nothing written)."""
-    if not x.is_cuda or not (16 < x.shape[0] <= 1024):
+    if not x.is_cuda or x.shape[0] <= 16:
         return None
     _need_gpu()
     T, H = x.shape

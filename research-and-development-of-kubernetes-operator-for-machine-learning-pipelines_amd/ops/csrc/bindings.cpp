@@ -227,6 +227,7 @@ int64_t vmm_error(Tensor flat) { return mlop::vmm_error(flat.data_ptr()); }
 
 int64_t gemm_big_variant(int64_t set) { return mlop::gemm_big_variant((int)set); }
 int64_t gemm_half_tile(int64_t set) { return mlop::gemm_half_tile((int)set); }
+int64_t moe_mid_max_tokens(int64_t set) { return mlop::moe_mid_max_tokens((int)set); }
 void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits, int64_t stages) {
   mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits, (int)stages);
 }
@@ -509,7 +510,7 @@ bool moe_dispatch_small(Tensor topw, Tensor topi, Tensor xp, Tensor offsets, Ten
   return true;
 }
 
-// mid-size dispatch (16 < T <= 1024): router GEMV + route per workgroup, the last sorts; no
+// mid-size dispatch (16 < T <= moe_mid_max_tokens): router GEMV + route per workgroup, the last sorts; no
 // gather (arow: token row of each permuted row); false = not taken
 bool moe_dispatch_mid(Tensor topw, Tensor topi, Tensor offsets, Tensor arow, Tensor inv, Tensor x, Tensor router_w,
                       int64_t e0, int64_t n_local, std::optional<Tensor> pro_y, std::optional<Tensor> pro_res,
@@ -799,6 +800,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_workspace(int M, int N, int K, int epi) -> int", &gemm_workspace);
   m.def("gemm_big_variant(int set=-1) -> int", &gemm_big_variant);
   m.def("gemm_half_tile(int set=-1) -> int", &gemm_half_tile);
+  m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
   m.def("gemm_dense_plan(int variant, int bm, int bn, int splits, int stages=0) -> ()", &gemm_dense_plan);
   m.def("gemm_small_stages(int set=-1) -> int", &gemm_small_stages);

@@ -124,10 +124,11 @@ bool launch_moe_down_combine_add_rmsnorm(void* out, void* residual, void* y, con
                                          const int* offsets, int n_groups, int R, int H, int I, int max_rows,
                                          const int* inv, const float* topw, const void* norm_w, float eps, int T,
                                          int k, hipStream_t st);
-// mid-size MoE dispatch (16 < T <= 1024 tokens): router GEMV + route per token workgroup, the last
+// mid-size MoE dispatch (16 < T <= 16384 tokens): router GEMV + route per token workgroup, the last
 // workgroup (agent-scope ticket) sorts the T*k slots by local expert -> offsets, inv and arow (the
 // token row of each permuted row: the grouped GEMM reads x through it, no gather)
 bool moe_dispatch_mid_takes(int T, int E, int k, int H);
+int moe_mid_max_tokens(int set);
 void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, int* inv, const void* x, const void* wr,
                              int T, int E, int k, int H, int e0, int n_local, const void* pro_y, void* pro_res,
                              const void* pro_w, float pro_eps, void* pro_xn, hipStream_t st);

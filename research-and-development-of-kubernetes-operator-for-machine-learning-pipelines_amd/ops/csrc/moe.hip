@@ -308,7 +308,7 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
 }
 
 // ---------------------------------------------------------------------------
-// Mid-size MoE dispatch (16 < T <= kMidT tokens) in ONE launch.  At batch 64 the separate
+// MoE dispatch for 16 < T <= kMidT tokens (decode batches and prefill chunks) in ONE launch.  At batch 64 the separate
 // route is five ~5 us graph nodes per layer (router GEMM + its split-K reduce, top-k, sort,
 // gather: profiles/r05_windows.md), each a few us of work at most.  Here:
 //   workgroup w (tokens kMidTok w ..): the optional add + RMSNorm prologue, router logits
@@ -320,7 +320,12 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
 // There is no gathered copy: the grouped gate_up GEMM reads x rows through arow.  Rows inside
 // an expert come in ticket order (LDS atomics), which changes no value: each row's product is
 // independent of its position and the combine gathers by inv.
-constexpr int kMidT = 1024, kMidTok = 2;
+constexpr int kMidT = 16384, kMidTok = 2;
+static int g_mid_max_t = kMidT;  // moe_mid_max_tokens op: in-process A/B of the range
+int moe_mid_max_tokens(int set) {
+  if (set >= 0) g_mid_max_t = set < kMidT ? set : kMidT;
+  return g_mid_max_t;
+}
 
 template <int CH>
 __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
@@ -465,7 +470,7 @@ __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
 }
 
 bool moe_dispatch_mid_takes(int T, int E, int k, int H) {
-  return T > kSmallT && T <= kMidT && E <= kMaxE && k <= 8 && (H == 1024 || H == 2048 || H == 4096 || H == 8192);
+  return T > kSmallT && T <= g_mid_max_t && E <= kMaxE && k <= 8 && (H == 1024 || H == 2048 || H == 4096 || H == 8192);
 }
 
 void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, int* inv, const void* x, const void* wr,

@@ -59,7 +59,7 @@ def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int
                          pre=None):
     """Single-rank MoE block followed by the decoder's residual add + RMSNorm.  At decode
     sizes the router GEMV, routing, sort and gather are ONE launch (moe_dispatch_small; at
-    16 < T <= 1024 moe_dispatch_mid, whose experts read x in place) and the weighted combine
+    16 < T <= 16384 moe_dispatch_mid, whose experts read x in place) and the weighted combine
     rides in the add + RMSNorm launch: 6 MoE glue launches -> 2.
     ``pre=(o, pre_norm_w)``: x is not formed yet; the block's own input add + RMSNorm
     (residual += o, x = rmsnorm(residual)) becomes the dispatch launch's prologue."""
@@ -75,7 +75,7 @@ def moe_forward_add_norm(x, router_w, w13, w2, top_k: int, e0: int, n_local: int
         d = ops.moe_dispatch_small(x, router_w, top_k, e0, n_local)
         if d is None:
             mid = ops.moe_dispatch_mid(x, router_w, top_k, e0, n_local)
-    if mid is not None:  # 16 < T <= 1024: one dispatch launch, the experts read x through arow
+    if mid is not None:  # 16 < T <= 16384: one dispatch launch, the experts read x through arow
         topw, topi, xs, offsets, arow, inv = mid
         return local_experts(xs, topw, topi, w13, w2, e0, n_local, dispatched=(xs, offsets, inv, arow),
                              combine=(residual, norm_w, eps))

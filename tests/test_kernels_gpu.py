@@ -806,7 +806,7 @@ def _check_mid_layout(topi, off, arow, inv, T, k, e0, nl):
     assert torch.equal(arow.cpu().long()[rows], slots // k)
 
 
-@pytest.mark.parametrize("T,E,k,H", [(17, 8, 2, 4096), (64, 8, 2, 4096), (130, 8, 2, 1024), (1024, 8, 2, 4096),
+@pytest.mark.parametrize("T,E,k,H", [(17, 8, 2, 4096), (64, 8, 2, 4096), (130, 8, 2, 1024), (1024, 8, 2, 4096), (5000, 8, 2, 4096),
                                      (40, 16, 4, 2048), (300, 8, 2, 8192)])
 def test_moe_dispatch_mid(gpu, T, E, k, H):
     """Multi-workgroup dispatch (router GEMV + route per workgroup, last-workgroup sort, no
