@@ -439,6 +439,12 @@ int gemm_big_variant(int set) {
   if (set >= 0) g_big_variant = set;
   return g_big_variant;
 }
+// the grouped <= 32-rows-per-expert rule (plan() below) on / off (gemm_grouped_narrow op)
+static int g_grouped_narrow = 1;
+int gemm_grouped_narrow(int set) {
+  if (set >= 0) g_grouped_narrow = set;
+  return g_grouped_narrow;
+}
 // the planner's half-height four-wave tile (variant 6) on / off (gemm_half_tile op, A/B runs)
 static int g_half_tile = 1;
 int gemm_half_tile(int set) {
@@ -1025,6 +1031,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
 struct Plan {
   int BM, BN, splits, k_chunk, m_tiles, variant;
   int stages;  // LDS-DMA ring depth of the small-M tiles (0: g_small_stages)
+  bool nosplit;  // grouped: one K range (the mid-size MoE split-K below is skipped)
 };
 
 
@@ -1080,6 +1087,14 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
     p.BN = 64;
     // grouped (MoE at a few dozen rows per expert), narrow down projection: ring depth knob
     if (grouped && N < 16384) p.stages = g_grouped_small_stages;
+    // grouped at <= 32 rows per expert (Mixtral batch 16-64): down on 32 x 64 tiles with a
+    // 6-deep ring and ONE K range, gate_up on a 4-deep ring (scripts/bench_moe_decode.py, cold
+    // expert weights, profiles/r05_moe_decode.md: down at 128 routed rows 172.4 -> 160.4 us,
+    // 5.45 -> 5.86 TB/s; gate_up 318.2 -> 315.9)
+    if (grouped && g_grouped_narrow && mrows <= 32) {
+      if (N < 16384) { p.BM = 32; p.stages = 6; p.nosplit = true; }
+      else p.stages = 4;
+    }
   }
   else if (mrows <= 128) { p.BM = 128; p.BN = 64; }
   else if (mrows <= 256) {
@@ -1401,7 +1416,7 @@ void launch_grouped_gemm(const void* A, const void* B, void* C, const int* offse
   // stream-K slab buffer (same stream, so never in use by another launch), then the reduce
   // kernel applies the epilogue.  Routed tiles are estimated as one m-tile per expert.
   float* ws = nullptr;
-  if (p.variant != 3 && K >= 2048 && g_gp[3] != 1) {
+  if (p.variant != 3 && K >= 2048 && g_gp[3] != 1 && !(p.nosplit && g_gp[0] <= 0)) {
     const SkBuf* b = sk_buf();
     const long t_est = (long)((N + p.BN - 1) / p.BN) * std::max(1, std::min(n_groups, (M + p.BM - 1) / p.BM + n_groups));
     constexpr int target = 1024;

@@ -66,6 +66,7 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 // 8-wave, 3 ping-pong, 5 four-wave asm K-loop); set >= 0 overrides (in-process A/B), returns the current value
 int gemm_big_variant(int set);
 int gemm_half_tile(int set);
+int gemm_grouped_narrow(int set);
 void gemm_grouped_plan(int bm, int bn, int stages, int splits);
 void gemm_dense_plan(int variant, int bm, int bn, int splits, int stages = 0);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip), variant 6 its 128x256

@@ -27,9 +27,12 @@ from mlopamd import ops  # noqa: E402
 E = 8
 # (label, BM, BN, stages, splits); -1 = planner default
 CANDIDATES = {
-    "small": [("auto", -1, -1, -1, -1), ("16x64/s6", 16, 64, 6, -1), ("32x64/s6", 32, 64, 6, -1),
-              ("32x32/s8", 32, 32, 8, -1), ("64x64/s6", 64, 64, 6, -1), ("64x64/s3", 64, 64, 3, -1),
-              ("32x64/s6/k1", 32, 64, 6, 1), ("32x64/s6/k4", 32, 64, 6, 4)],
+    "small": [("auto", -1, -1, -1, -1), ("16x64/s6", 16, 64, 6, -1), ("16x64/s8", 16, 64, 8, -1),
+              ("32x64/s6", 32, 64, 6, -1), ("32x32/s8", 32, 32, 8, -1), ("64x64/s6", 64, 64, 6, -1),
+              ("64x64/s4", 64, 64, 4, -1), ("64x64/s3", 64, 64, 3, -1), ("64x32/s4", 64, 32, 4, -1),
+              ("32x64/s6/k1", 32, 64, 6, 1), ("32x64/s6/k4", 32, 64, 6, 4), ("64x64/s3/k1", 64, 64, 3, 1),
+              ("64x64/s3/k2", 64, 64, 3, 2), ("64x64/s3/k4", 64, 64, 3, 4), ("64x64/s6/k4", 64, 64, 6, 4),
+              ("16x64/s8/k2", 16, 64, 8, 2), ("16x64/s8/k4", 16, 64, 8, 4)],
     "mid": [("auto", -1, -1, -1, -1), ("128x64", 128, 64, -1, -1), ("64x64/s6", 64, 64, 6, -1),
             ("64x64/s3", 64, 64, 3, -1), ("256x128", 256, 128, -1, 1), ("256x64", 256, 64, -1, 1),
             ("256x256", 256, 256, -1, 1)],
