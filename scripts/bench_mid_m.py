@@ -20,7 +20,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mlopamd import ops  # noqa: E402
 
-PROJ = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+PROJ = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+        "lm_head": (128256, 4096)}
 # (label, variant, BM, BN, splits): -1 = planner default
 CANDS = [("auto", -1, -1, -1, -1), ("w4", 5, 256, 256, -1), ("w4h", 6, 128, 256, -1), ("pp", 3, 256, 256, -1),
          ("256x128", 0, 256, 128, 1), ("256x128/k2", 0, 256, 128, 2), ("256x64", 0, 256, 64, 1),
