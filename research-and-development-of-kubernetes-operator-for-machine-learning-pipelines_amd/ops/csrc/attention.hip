@@ -82,7 +82,7 @@ __device__ __forceinline__ bf16x8 vt_frag(uint32_t b, int d) {
 
 __device__ __forceinline__ int wid_of(unsigned t) { return __builtin_amdgcn_readfirstlane((int)(t >> 6)); }
 
-template <int G>
+template <int G, bool NT>
 __global__ void __launch_bounds__(256) paged_attn_kernel(
     uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
@@ -170,7 +170,8 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     for (int i = 0; i < 8; ++i) {
       const int trow = (4 * i + g4) & 15;
       const uint16_t* src = (i < 4 ? vA : vB) + trow * kD + ((r ^ vswz(trow)) << 3);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(dst + 1024u * i), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(dst + 1024u * i), 16, 0,
+                                       NT ? 2 /* nt */ : 0);
     }
   };
   // page ids one pair ahead: the block-table loads of pair pp + 4 run under pair pp
@@ -188,8 +189,13 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     bf16x8 ka[4], kb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      ka[kk] = *reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8);
-      kb[kk] = *reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8);
+      if constexpr (NT) {
+        ka[kk] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8));
+        kb[kk] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8));
+      } else {
+        ka[kk] = *reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8);
+        kb[kk] = *reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8);
+      }
     }
     // this pair's V image, issued behind the K loads (the S MFMAs wait for those only; the
     // previous pair's transposed reads are complete: their MFMAs consumed them)
@@ -388,6 +394,14 @@ __global__ void __launch_bounds__(256) attn_reduce_kernel(
   *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi) * Hq + head) * kD + c) = ov;
 }
 
+// K / V pages of the decode kernel non-temporal (read once per step by one workgroup; the
+// headline step reads ~100 GB of them): headline +2.2 / +3.2 % interleaved (attn_kv_nt op)
+static int g_attn_kv_nt = 1;
+int attn_kv_nt(int set) {
+  if (set >= 0) g_attn_kv_nt = set;
+  return g_attn_kv_nt;
+}
+
 template <int G>
 static void launch_g(void* out, float* part_o, float* part_ml, const void* q, const void* kc,
                      const void* vc, const int* bt, int bt_stride, const int* tile_seq,
@@ -395,10 +409,11 @@ static void launch_g(void* out, float* part_o, float* part_ml, const void* q, co
                      int num_tiles, int Hq, int Hkv, float scale_log2, int part_tokens, int nparts,
                      int num_blocks, int* sem, hipStream_t st) {
   dim3 grid(num_tiles, Hkv, nparts);
-  paged_attn_kernel<G><<<grid, 256, 0, st>>>((uint16_t*)out, part_o, part_ml, (const uint16_t*)q,
-                                             (const uint16_t*)kc, (const uint16_t*)vc, bt,
-                                             bt_stride, tile_seq, tile_q0, q_start, q_len, ctx_len,
-                                             Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, sem);
+  // K / V pages non-temporal (attn_kv_nt op): each is read once per step by one workgroup
+  auto kern = g_attn_kv_nt ? paged_attn_kernel<G, true> : paged_attn_kernel<G, false>;
+  kern<<<grid, 256, 0, st>>>((uint16_t*)out, part_o, part_ml, (const uint16_t*)q, (const uint16_t*)kc,
+                             (const uint16_t*)vc, bt, bt_stride, tile_seq, tile_q0, q_start, q_len, ctx_len,
+                             Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, sem);
   if (nparts > 1 && sem == nullptr) {
     attn_reduce_kernel<G><<<dim3(num_tiles, Hkv), 256, 0, st>>>(
         (uint16_t*)out, part_o, part_ml, tile_seq, tile_q0, q_start, q_len, ctx_len, Hq, Hkv,

@@ -120,13 +120,19 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
       src[i] = Bg + (size_t)gn * ldb + kbeg + pchunk * 8;
     }
   }
+  // weight pieces non-temporal when re.b_nt (wave-uniform: a piece is A or B by its index)
+  const bool b_nt = re.b_nt != 0;
   auto issue = [&](int buf, int kt) {
     uint16_t* base = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int p = wid + i * NW;
-      __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * kBK),
-                                       (lds_void_t*)(base + p * 512), 16, 0, 0);
+      if (b_nt && p >= BM / 8)
+        __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * kBK),
+                                         (lds_void_t*)(base + p * 512), 16, 0, 2 /* nt */);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * kBK),
+                                         (lds_void_t*)(base + p * 512), 16, 0, 0);
     }
   };
 
@@ -360,6 +366,17 @@ constexpr size_t lds_bytes() {
   return ring > epi ? ring : epi;
 }
 
+// non-temporal weight stream of the decode-shaped GEMMs (gemm_small_nt op; MI355X_MICROARCH.md
+// "nt-weights": serving streams 16 GB of other weights between two reads of one matrix, so the
+// default policy's L2 / MALL fills are pure cost).  Interleaved on one box: Llama batch 16 +4.4 %,
+// batch 64 +2.6 %, Mixtral batch 64 +6.3 % (gate_up at M = 16 / 64 46.1 -> 41.3 / 52.1 -> 47.7 us);
+// bit 0 dense one-m-tile launches, bit 1 grouped small tiles, bit 2 grouped ping-pong
+static int g_small_nt_flags = 7;
+int gemm_small_nt(int set) {
+  if (set >= 0) g_small_nt_flags = set;
+  return g_small_nt_flags;
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES, bool SETPRIO>
 static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc,
                     float* ws, int M, int N, int K, int splits, int k_chunk, const int* offsets,
@@ -375,8 +392,12 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
   }
   const int gx = (N + BN - 1) / BN;
   const int blocks = gx * m_tiles * splits;
+  // non-temporal weights where each weight byte is streamed by ONE workgroup: one m-tile
+  // (dense), or the grouped decode tiles (an expert's few routed rows)
+  RopeEpi r = re;
+  r.b_nt = GROUPED ? (g_small_nt_flags & 2) != 0 && BM <= 64 : (g_small_nt_flags & 1) != 0 && m_tiles == 1;
   kern<<<blocks, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups, gx,
-                               m_tiles, splits, re);
+                               m_tiles, splits, r);
 }
 
 static int g_small_stages = 3;
@@ -660,7 +681,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       for (int i = 0; i < 2; ++i) {
         const int r0 = h < 2 ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
         uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + r0 * kBK;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
+        if (GROUPED && h >= 2 && re.b_nt)  // expert weights, streamed once (run_pp)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 2 /* nt */);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
       }
     };
     auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
@@ -1001,6 +1025,11 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   const int gm = std::max(1, std::min(group_m, gy));
   int n_sk = 0;
   SkArgs sk = sk_plan(gx * gy, K / kBK, n_sk);
+  // expert weights non-temporal while an expert's rows mostly fit one 256-row m-tile (each
+  // weight byte streamed once): Mixtral batch 256 (64 rows per expert on average) +3.9 %; at
+  // 256 per expert the spill m-tiles re-read the weights and nt lost 1.5 % (batch 1024)
+  RopeEpi r = re;
+  r.b_nt = GROUPED && (g_small_nt_flags & 4) != 0 && M <= 128 * std::max(1, n_groups);
   if constexpr (GROUPED) {
     // the routed tile count is only known on device: the grid is the worst case (every
     // expert's last m-tile partial) plus one stream-K block per CU; the kernel plans the
@@ -1022,10 +1051,10 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
       hipFuncSetAttribute((const void*)ksk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_sk = true;
     }
-    ksk<<<sk.n_base + n_sk, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
+    ksk<<<sk.n_base + n_sk, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, r, offsets, n_groups, sk);
     return;
   }
-  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, re, offsets, n_groups, sk);
+  kern<<<gx * gy, 512, lds, st>>>(A, lda, B, ldb, C, ldc, M, N, K, gx, gy, gm, r, offsets, n_groups, sk);
 }
 
 struct Plan {

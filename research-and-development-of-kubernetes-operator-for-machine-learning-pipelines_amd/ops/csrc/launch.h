@@ -57,6 +57,9 @@ struct RopeEpi {
   // grouped GEMM: A row of permuted row r is a_rows[r] (moe_dispatch_mid: the experts read the
   // token rows in place, no gathered copy); nullptr = row r
   const int* a_rows = nullptr;
+  // gemm_kernel: the weight (B) pieces of the LDS-DMA ring load non-temporal (read once by one
+  // workgroup: MI355X_MICROARCH.md "nt-weights"); set by run_cfg (gemm_small_nt)
+  int b_nt = 0;
 };
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
@@ -85,6 +88,11 @@ bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, in
                      const RopeEpi& re, hipStream_t st);
 int gemm_small_stages(int set);  // LDS-DMA ring depth of the M <= 128 tiles (3, or 5/6)
 int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fitted BM x BN
+// non-temporal weight loads of the one-m-tile gemm_kernel launches: bit 0 dense, bit 1 grouped,
+// bit 2 the grouped ping-pong kernel
+int gemm_small_nt(int set);
+// non-temporal K / V page loads of the decode attention kernel
+int attn_kv_nt(int set);
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the
 // per-device partial / counter buffers (allocate once, outside graph capture)
 int gemm_sk_mode(int set);

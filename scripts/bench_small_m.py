@@ -6,6 +6,7 @@ of copies, as in serving where 16 GB of other layers pass between two calls of o
 One process, interleaved rounds, random data.
 
 Usage (GPU box): python scripts/bench_small_m.py [--ms 8,16,32,64] [--shapes qkv,o,gate_up,down]
+       --nt: the planner's tile only, default vs non-temporal weight loads (gemm_small_nt), 4 rounds
 """
 from __future__ import annotations
 
@@ -53,6 +54,7 @@ def main():
     ap.add_argument("--ms", default="8,16,32,64")
     ap.add_argument("--shapes", default="qkv,o,gate_up,down")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--nt", action="store_true")
     a = ap.parse_args()
     ops.load()
     dev = torch.device("cuda")
@@ -75,9 +77,16 @@ def main():
                 return ops.gemm(x, ws[cyc[0]], epi=epi)
 
             res, ref = {}, None
-            for _ in range(2):
-                for label, v, bm, bn, sp, st in candidates(M):
+            cands = candidates(M)
+            if a.nt:
+                cands = [("auto", -1, -1, -1, -1, 0, 0), ("auto_nt", -1, -1, -1, -1, 0, 1)]
+            else:
+                cands = [c + (torch.ops.mlop.gemm_small_nt(-1),) for c in cands]
+            for _ in range(4 if a.nt else 2):
+                for label, v, bm, bn, sp, st, nt in cands:
+                    prev_nt = torch.ops.mlop.gemm_small_nt(-1)
                     try:
+                        torch.ops.mlop.gemm_small_nt(nt)
                         torch.ops.mlop.gemm_dense_plan(v, bm, bn, sp, st)
                         ops.GEMM_BACKEND = "mlop"
                         y = ops.gemm(x, w, epi=epi)
@@ -89,6 +98,7 @@ def main():
                     finally:
                         ops.GEMM_BACKEND = ops.GEMM_BACKEND_DEFAULT
                         torch.ops.mlop.gemm_dense_plan(-1, -1, -1, -1, 0)
+                        torch.ops.mlop.gemm_small_nt(prev_nt)
             good = {k: v for k, v in res.items() if v > 0}
             best = min(good, key=good.get)
             wbytes = N * K * 2

@@ -934,3 +934,59 @@ def test_moe_pipeline(gpu, T, E, k, H, I):
         # bf16 rounding noise scales with the output magnitude (large I: |out| ~ 20)
         close(out, exp, atol=3e-2 + 3e-3 * float(exp.abs().max()), rtol=3e-2)
         assert n == int(((idx >= e0) & (idx < e0 + nl)).sum())
+
+
+@pytest.mark.parametrize("M", [16, 64, 200, 600])
+def test_nt_weight_policy_bit_identical(gpu, M):
+    """The non-temporal weight stream (gemm_small_nt: one-m-tile dense tiles, grouped small
+    tiles, grouped ping-pong) changes the cache policy only: outputs are bit-identical to the
+    default policy, dense and grouped."""
+    torch.manual_seed(M)
+    ops._sk_reserve(torch.device(gpu))
+    x = torch.randn(M, 4096, device=gpu, dtype=bf)
+    w = (0.02 * torch.randn(6144, 4096, device=gpu)).to(bf)
+    E = 8
+    counts = [M // E + (1 if e < M % E else 0) for e in range(E)]
+    off = torch.tensor([0] + list(np.cumsum(counts)), device=gpu, dtype=torch.int32)
+    we = (0.02 * torch.randn(E, 1024, 4096, device=gpu)).to(bf)
+    prev_b = ops.GEMM_BACKEND
+    prev = torch.ops.mlop.gemm_small_nt(-1)
+    outs = {}
+    try:
+        ops.GEMM_BACKEND = "mlop"
+        for nt in (0, 7):
+            torch.ops.mlop.gemm_small_nt(nt)
+            outs[nt] = (ops.gemm(x, w), ops.gemm(x, w[:4096], epi=ops.EPI_SILU_MUL),
+                        ops.grouped_gemm(x, we, off, epi=0, avg_rows=max(1, M // E)))
+    finally:
+        torch.ops.mlop.gemm_small_nt(prev)
+        ops.GEMM_BACKEND = prev_b
+    for a, b in zip(outs[0], outs[7]):
+        assert torch.equal(a, b)
+    close(outs[7][0], (x.float() @ w.float().t()).to(bf))
+
+
+@pytest.mark.parametrize("case", ["decode", "split"])
+def test_attention_kv_policy_bit_identical(gpu, case):
+    """Non-temporal K / V page loads in the decode kernel (attn_kv_nt): bit-identical output."""
+    torch.manual_seed(3)
+    np.random.seed(3)
+    Hq, Hkv = 32, 8
+    ctx = [300, 1000, 17, 64] if case == "decode" else [3000, 2500]
+    NB = sum((c + 15) // 16 for c in ctx) + 8
+    kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
+    kw = dict(part_tokens=512, nparts=6) if case == "split" else {}
+    m, T = make_meta(gpu, [1] * len(ctx), ctx, Hkv, Hq // Hkv, NB, **kw)
+    q = torch.randn(T, Hq, 128, device=gpu, dtype=bf)
+    prev = torch.ops.mlop.attn_kv_nt(-1)
+    try:
+        torch.ops.mlop.attn_kv_nt(0)
+        a = ops.paged_attention(q, kc, vc, m).clone()
+        torch.ops.mlop.attn_kv_nt(1)
+        b = ops.paged_attention(q, kc, vc, m).clone()
+    finally:
+        torch.ops.mlop.attn_kv_nt(prev)
+    assert torch.equal(a, b)
+    close(b, ref.paged_attention(q, kc, vc, m))
+
