@@ -599,6 +599,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
   // routed (expert, m-tile) slot is the fast index, rows stop at offsets[e + 1], B = W[e].
   int m_end = M;
   const uint16_t* Bg = B;
+  bool b_once = false;  // grouped: the expert fits one m-tile, its weights are streamed once
   auto tile_origin = [&](int lid, int& m0, int& n0) {
     if constexpr (GROUPED) {
       const int slot = lid % S;
@@ -612,6 +613,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       n0 = (lid / S) * BN;
       m_end = offsets[e + 1];
       Bg = B + (size_t)e * N * ldb;
+      b_once = offsets[e + 1] - offsets[e] <= BM;
     } else {
       const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
       const int gm_here = min(group_m, m_tiles - band * group_m);
@@ -681,7 +683,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       for (int i = 0; i < 2; ++i) {
         const int r0 = h < 2 ? i * 128 + h * 64 + wid * 8 : (h & 1) * 128 + (wid + 8 * i) * 8;
         uint16_t* dst = smem + buf * BUF + (h >= 2 ? BM * kBK : 0) + r0 * kBK;
-        if (GROUPED && h >= 2 && re.b_nt)  // expert weights, streamed once (run_pp)
+        if (GROUPED && h >= 2 && re.b_nt && b_once)  // an expert's weights streamed once
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 2 /* nt */);
         else
           __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
@@ -1025,11 +1027,11 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   const int gm = std::max(1, std::min(group_m, gy));
   int n_sk = 0;
   SkArgs sk = sk_plan(gx * gy, K / kBK, n_sk);
-  // expert weights non-temporal while an expert's rows mostly fit one 256-row m-tile (each
-  // weight byte streamed once): Mixtral batch 256 (64 rows per expert on average) +3.9 %; at
-  // 256 per expert the spill m-tiles re-read the weights and nt lost 1.5 % (batch 1024)
+  // expert weights non-temporal where the expert fits one 256-row m-tile (decided per tile on
+  // device): Mixtral batch 256 (64 rows per expert on average) +3.9 %; nt on every expert lost
+  // 1.5 % at batch 1024, where the spill m-tiles of the > 256-row experts re-read the weights
   RopeEpi r = re;
-  r.b_nt = GROUPED && (g_small_nt_flags & 4) != 0 && M <= 128 * std::max(1, n_groups);
+  r.b_nt = GROUPED && (g_small_nt_flags & 4) != 0;
   if constexpr (GROUPED) {
     // the routed tile count is only known on device: the grid is the worst case (every
     // expert's last m-tile partial) plus one stream-K block per CU; the kernel plans the
