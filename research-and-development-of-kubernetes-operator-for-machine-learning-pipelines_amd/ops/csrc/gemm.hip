@@ -189,7 +189,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ml = wm * WTM + i * 16 + 4 * (lane >> 4) + r;
-          if (ml < rows_here && n < N) P[(size_t)(m0 + ml) * N + n] = acc[i][j][r];
+          if (ml < rows_here && n < N) {
+            if (re.ws_nt & 1) __builtin_nontemporal_store(acc[i][j][r], P + (size_t)(m0 + ml) * N + n);
+            else P[(size_t)(m0 + ml) * N + n] = acc[i][j][r];
+          }
         }
       }
     return;
@@ -377,6 +380,16 @@ int gemm_small_nt(int set) {
   return g_small_nt_flags;
 }
 
+// non-temporal stores of GEMM outputs the next launch reads (gemm_slab_nt op; not left dirty in
+// L2 for the kernel boundary's write-back, MI355X_MICROARCH.md "boundary"): bit 0 the split-K
+// slabs (batch 256 +0.6 %, batch 64 neutral), bit 1 the four-wave kernel's C (headline +1.2 %),
+// bit 2 the ping-pong kernel's C (Mixtral batch 256 / 1024 and Llama batch 512 +0.3-0.4 %)
+static int g_slab_nt = 7;
+int gemm_slab_nt(int set) {
+  if (set >= 0) g_slab_nt = set;
+  return g_slab_nt;
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES, bool SETPRIO>
 static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc,
                     float* ws, int M, int N, int K, int splits, int k_chunk, const int* offsets,
@@ -396,6 +409,7 @@ static void run_cfg(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint
   // (dense), or the grouped decode tiles (an expert's few routed rows)
   RopeEpi r = re;
   r.b_nt = GROUPED ? (g_small_nt_flags & 2) != 0 && BM <= 64 : (g_small_nt_flags & 1) != 0 && m_tiles == 1;
+  r.ws_nt = g_slab_nt;
   kern<<<blocks, T, lds, st>>>(A, lda, B, ldb, C, ldc, ws, M, N, K, k_chunk, offsets, n_groups, gx,
                                m_tiles, splits, r);
 }
@@ -900,8 +914,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       const int c = i2 * 64 + lane;
       const int row = c / CPR, cc = (c % CPR) * 8;
       const int gm = m0 + grp * 128 + row, gn = out_col0 + cc;
-      if (gm < m_end && gn < out_n)
-        *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
+      if (gm < m_end && gn < out_n) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sC + row * LD + cc);
+        if (re.ws_nt & 4) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn));
+        else *reinterpret_cast<u32x4*>(C + (size_t)gm * ldc + gn) = v;
+      }
     }
   } while (SK && it < it_end);
 }
@@ -1032,6 +1049,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
   // 1.5 % at batch 1024, where the spill m-tiles of the > 256-row experts re-read the weights
   RopeEpi r = re;
   r.b_nt = GROUPED && (g_small_nt_flags & 4) != 0;
+  r.ws_nt = g_slab_nt;
   if constexpr (GROUPED) {
     // the routed tile count is only known on device: the grid is the worst case (every
     // expert's last m-tile partial) plus one stream-K block per CU; the kernel plans the

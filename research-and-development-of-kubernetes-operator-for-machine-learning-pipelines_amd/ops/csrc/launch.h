@@ -60,6 +60,9 @@ struct RopeEpi {
   // gemm_kernel: the weight (B) pieces of the LDS-DMA ring load non-temporal (read once by one
   // workgroup: MI355X_MICROARCH.md "nt-weights"); set by run_cfg (gemm_small_nt)
   int b_nt = 0;
+  // gemm_kernel: split-K slabs stored non-temporal (not left dirty in L2 for the kernel boundary's
+  // write-back; MI355X_MICROARCH.md "boundary"); set by run_cfg (gemm_slab_nt)
+  int ws_nt = 0;
 };
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
@@ -93,6 +96,7 @@ int gemm_small_tile(int set);    // M <= 64 tiles: 0 = 64 x 64, 32 / 64 = row-fi
 int gemm_small_nt(int set);
 // non-temporal K / V page loads of the decode attention kernel
 int attn_kv_nt(int set);
+int gemm_slab_nt(int set);
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the
 // per-device partial / counter buffers (allocate once, outside graph capture)
 int gemm_sk_mode(int set);
