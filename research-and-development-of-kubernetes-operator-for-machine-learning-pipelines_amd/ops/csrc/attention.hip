@@ -82,7 +82,7 @@ __device__ __forceinline__ bf16x8 vt_frag(uint32_t b, int d) {
 
 __device__ __forceinline__ int wid_of(unsigned t) { return __builtin_amdgcn_readfirstlane((int)(t >> 6)); }
 
-template <int G, bool NT>
+template <int G, int NT>  // NT bit 0: K / V loads non-temporal, bit 1: the output stores
 __global__ void __launch_bounds__(256) paged_attn_kernel(
     uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
       const int trow = (4 * i + g4) & 15;
       const uint16_t* src = (i < 4 ? vA : vB) + trow * kD + ((r ^ vswz(trow)) << 3);
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(uintptr_t)(dst + 1024u * i), 16, 0,
-                                       NT ? 2 /* nt */ : 0);
+                                       (NT & 1) ? 2 /* nt */ : 0);
     }
   };
   // page ids one pair ahead: the block-table loads of pair pp + 4 run under pair pp
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     bf16x8 ka[4], kb[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      if constexpr (NT) {
+      if constexpr ((NT & 1) != 0) {
         ka[kk] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kR + kk * 32 + g4 * 8));
         kb[kk] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kR + 4 * kD + kk * 32 + g4 * 8));
       } else {
@@ -288,7 +288,9 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     u32x4 ov;
 #pragma unroll
     for (int j = 0; j < 4; ++j) ov[j] = pack2(acc[2 * j] * inv, acc[2 * j + 1] * inv);
-    *reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + head2) * kD + c) = ov;
+    u32x4* dst = reinterpret_cast<u32x4*>(out + ((size_t)(qs + qi2) * Hq + head2) * kD + c);
+    if constexpr ((NT & 2) != 0) __builtin_nontemporal_store(ov, dst);
+    else *dst = ov;
     return;
   }
   if (row_valid) {
@@ -395,8 +397,9 @@ __global__ void __launch_bounds__(256) attn_reduce_kernel(
 }
 
 // K / V pages of the decode kernel non-temporal (read once per step by one workgroup; the
-// headline step reads ~100 GB of them): headline +2.2 / +3.2 % interleaved (attn_kv_nt op)
-static int g_attn_kv_nt = 1;
+// headline step reads ~100 GB of them): headline +2.2 / +3.2 % interleaved (attn_kv_nt op, bit
+// 0); bit 1 the output stores too (with gemm_slab_nt bit 3: +0.5 %)
+static int g_attn_kv_nt = 3;
 int attn_kv_nt(int set) {
   if (set >= 0) g_attn_kv_nt = set;
   return g_attn_kv_nt;
@@ -410,7 +413,7 @@ static void launch_g(void* out, float* part_o, float* part_ml, const void* q, co
                      int num_blocks, int* sem, hipStream_t st) {
   dim3 grid(num_tiles, Hkv, nparts);
   // K / V pages non-temporal (attn_kv_nt op): each is read once per step by one workgroup
-  auto kern = g_attn_kv_nt ? paged_attn_kernel<G, true> : paged_attn_kernel<G, false>;
+  auto kern = g_attn_kv_nt == 3 ? paged_attn_kernel<G, 3> : g_attn_kv_nt ? paged_attn_kernel<G, 1> : paged_attn_kernel<G, 0>;
   kern<<<grid, 256, 0, st>>>((uint16_t*)out, part_o, part_ml, (const uint16_t*)q, (const uint16_t*)kc,
                              (const uint16_t*)vc, bt, bt_stride, tile_seq, tile_q0, q_start, q_len, ctx_len,
                              Hq, Hkv, scale_log2, part_tokens, nparts, num_blocks, sem);

@@ -383,8 +383,9 @@ int gemm_small_nt(int set) {
 // non-temporal stores of GEMM outputs the next launch reads (gemm_slab_nt op; not left dirty in
 // L2 for the kernel boundary's write-back, MI355X_MICROARCH.md "boundary"): bit 0 the split-K
 // slabs (batch 256 +0.6 %, batch 64 neutral), bit 1 the four-wave kernel's C (headline +1.2 %),
-// bit 2 the ping-pong kernel's C (Mixtral batch 256 / 1024 and Llama batch 512 +0.3-0.4 %)
-static int g_slab_nt = 7;
+// bit 2 the ping-pong kernel's C (Mixtral batch 256 / 1024 and Llama batch 512 +0.3-0.4 %),
+// bit 3 the four-wave RoPE epilogue's q / K / V (with attn_kv_nt 3: headline +0.5 % over 5 pairs)
+static int g_slab_nt = 15;
 int gemm_slab_nt(int set) {
   if (set >= 0) g_slab_nt = set;
   return g_slab_nt;

@@ -968,7 +968,8 @@ def test_nt_weight_policy_bit_identical(gpu, M):
 
 @pytest.mark.parametrize("case", ["decode", "split"])
 def test_attention_kv_policy_bit_identical(gpu, case):
-    """Non-temporal K / V page loads in the decode kernel (attn_kv_nt): bit-identical output."""
+    """Non-temporal K / V page loads and output stores in the decode kernel (attn_kv_nt):
+    bit-identical output."""
     torch.manual_seed(3)
     np.random.seed(3)
     Hq, Hkv = 32, 8
@@ -983,7 +984,7 @@ def test_attention_kv_policy_bit_identical(gpu, case):
     try:
         torch.ops.mlop.attn_kv_nt(0)
         a = ops.paged_attention(q, kc, vc, m).clone()
-        torch.ops.mlop.attn_kv_nt(1)
+        torch.ops.mlop.attn_kv_nt(3)
         b = ops.paged_attention(q, kc, vc, m).clone()
     finally:
         torch.ops.mlop.attn_kv_nt(prev)
