@@ -973,7 +973,8 @@ def test_attention_kv_policy_bit_identical(gpu, case):
     torch.manual_seed(3)
     np.random.seed(3)
     Hq, Hkv = 32, 8
-    ctx = [300, 1000, 17, 64] if case == "decode" else [3000, 2500]
+    # >= 8 query tiles: the policy applies from 8 (below, the default policy always)
+    ctx = [300, 1000, 17, 64, 900, 33, 512, 700] if case == "decode" else [3000, 2500] * 4
     NB = sum((c + 15) // 16 for c in ctx) + 8
     kc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
     vc = torch.randn(NB, Hkv, 16, 128, device=gpu, dtype=bf)
