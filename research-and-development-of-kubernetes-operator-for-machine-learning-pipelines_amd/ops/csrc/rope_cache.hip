@@ -54,7 +54,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   const int n_v = Hkv * (D >> 3);
   const int blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
-  for (int it = threadIdx.x; it < n_rope + n_v; it += blockDim.x) {
+  // gridDim.y blocks per token share its items (one item per thread at the decoder's head
+  // counts: one dependent load chain each instead of two in a row)
+  for (int it = threadIdx.x + blockIdx.y * blockDim.x; it < n_rope + n_v; it += blockDim.x * gridDim.y) {
     if (it < n_rope) {
       const int h = it / vph, c = (it % vph) * 8;
       // q heads then k heads are contiguous
@@ -103,7 +105,11 @@ void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qk
 
 void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int T, int N, hipStream_t st) {
   if (T == 0) return;
-  rope_cache_kernel<true><<<T, 256, 0, st>>>(re.q_out, re.k_cache, re.v_cache, nullptr, re.pos, re.cos_sin,
+  const int items = (re.Hq + re.Hkv) * 8 + re.Hkv * 16;  // 16-B vectors per token (head_dim 128)
+  // two blocks per token when the items exceed one block (batch 16 / 64 +0.4 %, interleaved,
+  // scripts/r5_ropesplit.sh)
+  const int by = std::min(2, (items + 255) / 256);
+  rope_cache_kernel<true><<<dim3(T, by), 256, 0, st>>>(re.q_out, re.k_cache, re.v_cache, nullptr, re.pos, re.cos_sin,
                                              re.slots, re.Hq, re.Hkv, 128, N, re.BS, ws, splits);
 }
 
