@@ -1,5 +1,6 @@
 #!/bin/bash
-# RoPE slab kernel over 2 blocks per token (rope_split) A/B at batch 16 / 64, after the GPU suite,
+# RoPE slab kernel over 2 blocks per token A/B at batch 16 / 64 (the rope_split op it flipped was removed
+# after this run: two blocks are now fixed), after the GPU suite, smoke() and the driver's command
 # smoke() and the driver's command on this tree
 source scripts/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
