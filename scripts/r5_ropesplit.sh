@@ -1,7 +1,6 @@
 #!/bin/bash
 # RoPE slab kernel over 2 blocks per token A/B at batch 16 / 64 (the rope_split op it flipped was removed
 # after this run: two blocks are now fixed), after the GPU suite, smoke() and the driver's command
-# smoke() and the driver's command on this tree
 source scripts/gpu_check.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step gpu_suite 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
