@@ -98,7 +98,9 @@ void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qk
                        const float* cos_sin, const int* slots, int T, int Hq, int Hkv, int D,
                        int qkv_stride, int BS, hipStream_t st) {
   if (T == 0) return;
-  rope_cache_kernel<false><<<T, 256, 0, st>>>((uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)v_cache,
+  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);  // 16-B vectors per token
+  const int by = std::min(2, (items + 255) / 256);               // as launch_rope_cache_slabs
+  rope_cache_kernel<false><<<dim3(T, by), 256, 0, st>>>((uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)v_cache,
                                               (const uint16_t*)qkv, pos, cos_sin, slots, Hq, Hkv, D,
                                               qkv_stride, BS);
 }
