@@ -126,6 +126,7 @@ class LLMBackend:
                 self.metrics.engine_steps.labels(**self.metrics.labels).inc()
                 if len(outs):
                     self.metrics.engine_tokens.labels(**self.metrics.labels).inc(len(outs))
+                self.metrics.engine_clock.labels(**self.metrics.labels).set(now)
             for o in outs:
                 r = self._active.get(o.seq_id)
                 if r is None:

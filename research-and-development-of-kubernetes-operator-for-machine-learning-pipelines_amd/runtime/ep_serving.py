@@ -231,6 +231,7 @@ class EPBackend(LLMBackend):
                 self.metrics.engine_steps.labels(**self.metrics.labels).inc()
                 if n_tok:
                     self.metrics.engine_tokens.labels(**self.metrics.labels).inc(n_tok)
+                self.metrics.engine_clock.labels(**self.metrics.labels).set(time.perf_counter())
                 m = self.metrics
                 m.running.labels(**m.labels).set(sum(self.load))
         self.stopped.set()

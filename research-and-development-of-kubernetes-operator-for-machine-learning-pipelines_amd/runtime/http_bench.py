@@ -32,7 +32,7 @@ async def _scrape(session, url) -> dict:
         txt = await r.text()
     out = {}
     for name in ("mlop_engine_steps_total", "mlop_engine_tokens_total", "mlop_prompt_tokens_total",
-                 "mlop_num_requests_waiting", "mlop_num_requests_running"):
+                 "mlop_num_requests_waiting", "mlop_num_requests_running", "mlop_engine_clock_seconds"):
         m = re.search(rf"^{name}\{{[^}}]*\}} ([0-9.e+]+)$", txt, re.M)
         out[name] = float(m.group(1)) if m else 0.0
     return out
@@ -197,8 +197,14 @@ async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256
             await asyncio.gather(*tasks, return_exceptions=True)
         n_steps = b["mlop_engine_steps_total"] - a["mlop_engine_steps_total"]
         toks = b["mlop_engine_tokens_total"] - a["mlop_engine_tokens_total"]
-        out.update(served_tokens_per_sec_http=round(toks / (t_b - t_a), 2), http_window_steps=int(n_steps),
-                   http_ms_per_step=round(1e3 * (t_b - t_a) / max(n_steps, 1), 3),
+        # the window's time on the predictor's engine clock (end of the first / last counted
+        # step), not between the two scrape responses: a scrape answered late by the busy event
+        # loop lengthened the client-side window by up to ~12 % (two 33.7k vs 38.5k samples)
+        ck = b["mlop_engine_clock_seconds"] - a["mlop_engine_clock_seconds"]
+        dt = ck if a["mlop_engine_clock_seconds"] > 0 and ck > 0 else t_b - t_a
+        out.update(served_tokens_per_sec_http=round(toks / dt, 2), http_window_steps=int(n_steps),
+                   http_ms_per_step=round(1e3 * dt / max(n_steps, 1), 3),
+                   http_window_client_s=round(t_b - t_a, 3), http_window_engine_s=round(ck, 3),
                    http_requests=stats["requests"], http_errors=stats["errors"],
                    http_running_at_end=int(b["mlop_num_requests_running"]))
     finally:

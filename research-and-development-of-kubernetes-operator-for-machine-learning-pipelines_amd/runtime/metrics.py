@@ -61,6 +61,11 @@ class RuntimeMetrics:
         self.gpu_power = Gauge("mlop_gpu_power_watts", "Socket power", base + ["gpu"], registry=r)
         self.engine_steps = Counter("mlop_engine_steps", "Engine steps executed", base, registry=r)
         self.engine_tokens = Counter("mlop_engine_tokens", "Tokens emitted by engine steps", base, registry=r)
+        # the engine thread's perf_counter at the end of its last step, set right after the two
+        # counters above: a rate over two scrapes then needs no client-side clock (the scrape's
+        # own latency on a busy event loop skewed a 2-3 s window by up to ~12 %)
+        self.engine_clock = Gauge("mlop_engine_clock_seconds", "Engine-thread clock at the end of the last step",
+                                  base, registry=r)
         self.kernel_time = Gauge("mlop_kernel_time_fraction", "rocprof kernel-time share per kernel class",
                                  base + ["kernel"], registry=r)
 
