@@ -1333,10 +1333,31 @@ static bool rope_slabs_ok(const Plan& p, int M, int N) {
          (size_t)p.splits * M * N <= (size_t)2 * kSkMaxWg * 256 * 256;
 }
 
+// Small-M QKV: K split even where the plain plan keeps one K range (M <= 16: 192 tiles of 16 x
+// 32): the slabs' reduce rides in the RoPE + cache kernel that runs anyway, so a second K range
+// costs one fp32 slab and doubles the workgroups streaming the weights (gemm_rope_split op:
+// the K ranges, 1 = the plain plan).  Interleaved, scripts/r5_ropesplitk.sh: batch 16 +1.9 %,
+// batch 12 +3.0 % (4 ranges: +2.2 / +2.6 %)
+static int g_rope_split_k = 2;
+int gemm_rope_split(int set) {
+  if (set >= 1) g_rope_split_k = set;
+  return g_rope_split_k;
+}
+
+static Plan rope_plan(int M, int N, int K) {
+  Plan p = plan(M, N, K, false, 0, 0);
+  if (g_rope_split_k > 1 && p.splits == 1 && p.variant == 0 && p.BM <= 64 && K >= 2048) {
+    const int kc = ((K / g_rope_split_k + kBK - 1) / kBK) * kBK;
+    p.splits = (K + kc - 1) / kc;
+    p.k_chunk = kc;
+  }
+  return p;
+}
+
 bool gemm_rope_supported(int M, int N, int K) {
   if (M <= 0 || N % 128 || K % kBK) return false;
   if (gemv_takes(M, N, K, EPI_ROPE)) return true;  // decode M <= 8: gemv.hip
-  const Plan p = plan(M, N, K, false, 0, 0);
+  const Plan p = rope_plan(M, N, K);
   return ((p.BM == 256 || p.variant == 6) && p.BN >= 128) || rope_slabs_ok(p, M, N);
 }
 
@@ -1348,7 +1369,7 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     launch_gemv_rope(A, lda, B, M, N, K, re, st);
     return true;
   }
-  Plan p = plan(M, N, K, false, 0, 0);
+  Plan p = rope_plan(M, N, K);
   if (!((p.BM == 256 || p.variant == 6) && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
     float* ws = sk_buf()->ws;
     launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, nullptr, N, ws,
