@@ -231,6 +231,7 @@ int64_t gemm_small_nt(int64_t set) { return mlop::gemm_small_nt((int)set); }
 int64_t attn_kv_nt(int64_t set) { return mlop::attn_kv_nt((int)set); }
 int64_t gemm_slab_nt(int64_t set) { return mlop::gemm_slab_nt((int)set); }
 int64_t gemm_rope_split(int64_t set) { return mlop::gemm_rope_split((int)set); }
+int64_t gemm_split_target(int64_t set) { return mlop::gemm_split_target((int)set); }
 int64_t gemm_grouped_narrow(int64_t set) { return mlop::gemm_grouped_narrow((int)set); }
 int64_t moe_mid_max_tokens(int64_t set) { return mlop::moe_mid_max_tokens((int)set); }
 void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits, int64_t stages) {
@@ -809,6 +810,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("attn_kv_nt(int set=-1) -> int", &attn_kv_nt);
   m.def("gemm_slab_nt(int set=-1) -> int", &gemm_slab_nt);
   m.def("gemm_rope_split(int set=-1) -> int", &gemm_rope_split);
+  m.def("gemm_split_target(int set=-1) -> int", &gemm_split_target);
   m.def("gemm_grouped_narrow(int set=-1) -> int", &gemm_grouped_narrow);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);

@@ -386,6 +386,11 @@ int gemm_small_nt(int set) {
 // bit 2 the ping-pong kernel's C (Mixtral batch 256 / 1024 and Llama batch 512 +0.3-0.4 %),
 // bit 3 the four-wave RoPE epilogue's q / K / V (with attn_kv_nt 3: headline +0.5 % over 5 pairs)
 static int g_slab_nt = 15;
+static int g_split_target = 512;  // gemm_split_target op: workgroups the split-K of the 16-row tiles aims at
+int gemm_split_target(int set) {
+  if (set >= 1) g_split_target = set;
+  return g_split_target;
+}
 int gemm_slab_nt(int set) {
   if (set >= 0) g_slab_nt = set;
   return g_slab_nt;
@@ -1246,7 +1251,10 @@ static Plan plan(int M, int N, int K, bool grouped, int n_groups, int rows_per_g
   p.splits = 1;
   p.k_chunk = K;
   const long tiles = (long)n_tiles * real_m_tiles;
-  constexpr int split_target = 256;  // run49: down -5..-15% at M 8-64
+  // run49: down -5..-15% at M 8-64.  The 16-row tiles (M 9-16) aim at 512 workgroups: batch 16
+  // +5.6 / +6.0 % interleaved (scripts/r5_splittarget.sh, r5_splittarget2.sh), while 512 lost
+  // 1.4-1.6 % at batch 24 / 32 (32-row tiles), 5 % at batch 64 and 4 % at 256
+  const int split_target = p.BM <= 16 ? g_split_target : 256;
   constexpr int split_max_tiles = 160;
   if (!grouped && tiles < split_max_tiles && K >= 1024 && p.variant != 3 && p.variant < 5) {
     int s = (int)std::min<long>(8, std::max<long>(1, split_target / tiles));

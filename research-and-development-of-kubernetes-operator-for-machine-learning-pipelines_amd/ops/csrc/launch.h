@@ -97,7 +97,8 @@ int gemm_small_nt(int set);
 // non-temporal K / V page loads of the decode attention kernel
 int attn_kv_nt(int set);
 int gemm_slab_nt(int set);
-int gemm_rope_split(int set);  // K ranges of the small-M QKV + RoPE launch (A/B)
+int gemm_rope_split(int set);
+int gemm_split_target(int set);  // K ranges of the small-M QKV + RoPE launch (A/B)
 // stream-K tail of the ping-pong GEMM: mode (1 on, 0 off; set >= 0 changes it) and the
 // per-device partial / counter buffers (allocate once, outside graph capture)
 int gemm_sk_mode(int set);
