@@ -101,6 +101,17 @@ def parse(argv=None):
     ap.add_argument("--ab-ops", default="",
                     help="A/B runs: comma list of op=value set through torch.ops.mlop before the engine "
                          "is built, e.g. gemm_half_tile=0 (in-process switches, scripts/ab.sh)")
+    ap.add_argument("--tp-phase", choices=("auto", "on", "off"), default="auto",
+                    help="after the DP replicas (the line's value), run a short TP = world phase of the same "
+                         "model on the same ranks: RCCL process group + the K15 IPC all-reduce across the "
+                         "devices (xGMI), with K15's start-up self-check and a greedy-token check against a "
+                         "dense TP = 1 recompute, reported as the 'tp' block.  auto: on when world > 1")
+    ap.add_argument("--tp-batch", type=int, default=256, help="concurrent requests of the TP phase")
+    ap.add_argument("--tp-steps", type=int, default=10, help="timed engine steps of the TP phase")
+    ap.add_argument("--tp-warmup", type=int, default=3)
+    ap.add_argument("--tp-timeout", type=float, default=240.0,
+                    help="watchdog of the TP phase (seconds): past it rank 0 prints the line with "
+                         "tp.error and every rank exits, so a first-contact hang cannot eat the DP result")
     ap.add_argument("--cr-ready-samples", type=int, default=3,
                     help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
                          "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
@@ -295,14 +306,67 @@ def main(argv=None):
     if not leader:  # TP worker: replay the leader's steps (and join its barriers) until STOP
         engine.worker_loop()
         _report(a, rank, world, dev, 0.0, 0.0, ready_s, {}, deploy_info, engine, None)
+        dist.barrier()
+        dist.destroy_process_group()
         return
-    from mlopamd.runtime.sampler import SamplingParams
-
     # steady-state serving is what the timed steps measure: let a lazily backed KV pool
     # finish its background fill first (CR->ready above is taken BEFORE this, when only
     # the first chunk is backed).  A partly backed pool admits fewer prompts, which turns
     # mixed steps into decode-only ones (29.9k vs 32.1k tok/s right after the GPU test suite)
     deploy_info.update(engine.kv.wait_ready())
+    gen, elapsed, stats, ramp = serve_closed_loop(
+        engine, a, a.batch, a.steps, a.warmup, rank,
+        ep_group=engine.model.ps.ep_cpu if a.ep > 1 else None)
+    deploy_info["ramp_steps"] = ramp
+    if a.tp > 1:
+        engine.shutdown()  # release the TP workers before the result gather
+    res = _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine, proc_ready)
+    if a.tp == 1:
+        engine.shutdown()
+    if _tp_phase_on(a, world):
+        # the driver's N-GPU command is DP replicas; on the same ranks, a short TP = N phase then
+        # carries Llama-3 over RCCL + the K15 IPC all-reduce across the N devices (xGMI), with
+        # its own first-contact checks (runtime/bench_tp.py), reported as the line's "tp" block
+        del engine
+        from mlopamd.runtime.bench_tp import tp_phase
+
+        tp = tp_phase(a, rank, world, dev, serve_closed_loop, res, _emit)
+        if res is not None:
+            res["tp"] = tp
+    _emit(res)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _tp_phase_on(a, world: int) -> bool:
+    if a.tp_phase == "off" or a.tp > 1 or a.ep > 1:
+        return False
+    return world > 1 or a.tp_phase == "on"
+
+
+_EMITTED = []
+
+
+def _emit(res) -> None:
+    """Rank 0 prints THE one JSON line (once, whichever of the normal end / the TP phase's
+    watchdog gets there first)."""
+    if res is None or _EMITTED:
+        return
+    _EMITTED.append(True)
+    print(json.dumps(res), flush=True)
+
+
+def serve_closed_loop(engine, a, batch, steps, warmup, rank, ep_group=None):
+    """Closed-loop load: ``batch`` concurrent requests of ``--prompt-len`` random tokens and
+    ``--output-len`` generated ones, the first cohort at staggered remaining lengths (steady-state
+    age mix), each finished request replaced at once.  An untimed ramp admits and prefills the
+    first cohort, then ``warmup`` untimed and ``steps`` timed engine steps bracketed by
+    ``sync_point`` (device sync + world barrier, TP workers included).  Returns
+    (generated tokens, seconds, step-stat deltas, ramp steps).  ``ep_group``: EP ranks step in
+    lock-step, so the ramp continues while ANY rank still ramps."""
+    from mlopamd.runtime.sampler import SamplingParams
+
     rng = np.random.default_rng(1234 + rank)
     V = engine.model.cfg.vocab_size
     P, O = a.prompt_len, a.output_len
@@ -315,9 +379,8 @@ def main(argv=None):
         engine.add_request(prompt, SamplingParams(max_tokens=int(max_tokens), temperature=a.temperature,
                                                   top_k=50 if a.temperature > 0 else 0, ignore_eos=True))
 
-    # first cohort at uniformly staggered remaining lengths (steady-state age mix)
-    for i in range(a.batch):
-        new_request(1 + (i * O) // a.batch)
+    for i in range(batch):
+        new_request(1 + (i * O) // batch)
 
     def run_steps(n):
         gen = 0
@@ -332,14 +395,17 @@ def main(argv=None):
     # admitted and prefilled, so the W warmup + K timed steps see the steady-state
     # mix (each step: every running sequence's decode token + the prompt chunks of
     # the requests that replaced the ones that finished) whatever W the caller picks
-    ramp_cap = 4 * (a.batch * P) // max(1, a.max_batched_tokens) + 64
+    ramp_cap = 4 * (batch * P) // max(1, a.max_batched_tokens) + 64
     ramp = 0
-    backlog = max(a.prefill_min_batch, 2 * a.batch // max(1, O))  # ~2 steps of arrivals
+    backlog = max(a.prefill_min_batch, 2 * batch // max(1, O))  # ~2 steps of arrivals
+
     def ramp_more() -> bool:
-        more = ramp < ramp_cap and (engine.stats["prefill_tokens"] < a.batch * P or len(engine.waiting) > backlog)
-        if a.ep > 1:  # EP ranks step in lock-step: continue while ANY rank still ramps
+        import torch.distributed as dist
+
+        more = ramp < ramp_cap and (engine.stats["prefill_tokens"] < batch * P or len(engine.waiting) > backlog)
+        if ep_group is not None:
             t = torch.tensor([int(more)], dtype=torch.int64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=engine.model.ps.ep_cpu)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ep_group)
             more = bool(t.item())
         return more
 
@@ -351,9 +417,8 @@ def main(argv=None):
             t_log = time.perf_counter()
             _progress(rank, f"ramp step {ramp}: {engine.stats['prefill_tokens']} prompt tokens in, "
                             f"{len(engine.running)} running")
-    deploy_info["ramp_steps"] = ramp
-    _progress(rank, f"ramp done ({ramp} steps); {a.warmup} warmup + {a.steps} timed steps")
-    run_steps(a.warmup)
+    _progress(rank, f"ramp done ({ramp} steps); {warmup} warmup + {steps} timed steps")
+    run_steps(warmup)
     if not a.tune_in_timed:
         # shapes first seen from here on take the nearest tuned row count's GEMM backend
         # instead of being timed inside the measured steps
@@ -363,13 +428,11 @@ def main(argv=None):
     engine.sync_point()  # device sync + world barrier (TP workers join it)
     s0 = dict(engine.stats)
     t_start = time.perf_counter()
-    gen = run_steps(a.steps)
+    gen = run_steps(steps)
     engine.sync_point()
     elapsed = time.perf_counter() - t_start
     stats = {k: engine.stats[k] - s0.get(k, 0) for k in engine.stats}
-    if a.tp > 1:
-        engine.shutdown()  # release the TP workers before the result gather
-    _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine, proc_ready)
+    return gen, elapsed, stats, ramp
 
 
 def http_main(a):
@@ -395,6 +458,7 @@ def _progress(rank: int, msg: str) -> None:
 
 
 def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engine, proc_ready=None):
+    """Gather every rank's counts; rank 0 returns the result dict (the caller prints it)."""
     import torch.distributed as dist
 
     tot = torch.tensor([float(gen), elapsed, ready_s, float(stats.get("prefill_tokens", 0))], dtype=torch.float64)
@@ -465,16 +529,12 @@ def _report(a, rank, world, dev, gen, elapsed, ready_s, stats, deploy_info, engi
             res["gemm_mode"] = ops.GEMM_BACKEND
         except Exception:  # noqa: BLE001
             pass
-        print(json.dumps(res), flush=True)
         if a.save_gemm_table:
             from mlopamd import ops
 
             ops.save_gemm_table(a.save_gemm_table)
-    if a.tp == 1:
-        engine.shutdown()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        return res
+    return None
 
 
 if __name__ == "__main__":

@@ -49,6 +49,8 @@ class Group:
     handle: object = None
     car: object = None  # CustomAllReduce (K15) for small bf16 messages on GPU
     ex: object = None   # EPExchange (ep_ipc.py): the DP-attention + EP MoE exchange on GPU
+    car_status: str = "off"  # K15: "ok" (self-check passed), "fallback" (failed: RCCL / gloo), "off"
+    car_check: dict = None   # this rank's K15 start-up self-check verdict (custom_ar.self_check)
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -161,8 +163,23 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
     if custom_ar and tp_size in (2, 4, 8) and torch.cuda.is_available() and backend_ok and car_env != "0":
         from .custom_ar import CustomAllReduce
 
-        tp.car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
-                                 group=tp_handle)
+        car = CustomAllReduce(tp.rank, tp_size, torch.device("cuda", torch.cuda.current_device()),
+                              group=tp_handle)
+        # first contact: K15 must reproduce the exact rank-order sum of seeded inputs on EVERY
+        # rank before it carries a single real message; otherwise the whole group stays on the
+        # process-group collectives (custom_ar.py self_check / agree)
+        inj = os.environ.get("MLOP_INJECT_CAR_CORRUPT", "")
+        verdict = car.self_check(inject_rank=int(inj) if inj.strip() else None)
+        tp.car_check = verdict
+        if car.agree(verdict):
+            tp.car, tp.car_status = car, "ok"
+        else:
+            import sys
+
+            print(f"[comm] K15 self-check failed on the TP group (rank {tp.rank}: {verdict}): "
+                  "falling back to the process-group collectives", file=sys.stderr, flush=True)
+            car.close()
+            tp.car_status = "fallback"
     return ParallelState(tp=tp, ep=ep, ep_cpu=ep_cpu, tp_cpu=tp_cpu)
 
 

@@ -124,3 +124,86 @@ class CustomAllReduce:
         if self.h:
             torch.ops.mlop.car_destroy(self.h)
             self.h = 0
+
+    # ------------------------------------------------------------ first contact --
+    def self_check(self, hidden: int = 4096, inject_rank: int | None = None) -> dict:
+        """Start-up agreement test of the IPC peers, run by EVERY rank of the group before the
+        first real call: a peer mapping that reads stale / wrong memory (a cross-device
+        coherence or dmabuf bug) would otherwise serve garbage at full speed, since the only
+        runtime guard (``error``) catches a dead peer, not a wrong sum.
+
+        Every rank generates every rank's input from a seed (rank r: seed 0x5EED + r), so the
+        exact expected result is known locally without trusting any collective: the fp32 sum
+        in rank order rounded to bf16 -- what the kernels compute, bit for bit.  Checked:
+        one-shot (16 rows), two-shot (256 rows, above TWO_SHOT_MIN_BYTES), the one-shot
+        all-reduce + residual add, the broadcast and the all-gather; plus the process-group
+        all-reduce of the same inputs (fp32, within its own rounding) as a cross-check of the
+        fallback path itself.  ``inject_rank``: that rank perturbs its one-shot output (the
+        forced-corruption test, env ``MLOP_INJECT_CAR_CORRUPT``).  Returns this rank's
+        verdict; ``agree`` makes it the group's."""
+        dev, W = self.device, self.world
+        rows = {"one_shot": 16, "two_shot": max(16, (TWO_SHOT_MIN_BYTES // (2 * hidden)) * 2)}
+
+        def inputs(n, salt):
+            xs = []
+            for p in range(W):
+                g = torch.Generator(device=dev).manual_seed(0x5EED + 7919 * salt + p)
+                xs.append(torch.randn(n, hidden, device=dev, generator=g).to(torch.bfloat16))
+            return xs
+
+        def oracle(xs):
+            acc = torch.zeros(xs[0].shape, dtype=torch.float32, device=dev)
+            for x in xs:  # rank order, fp32: the kernels' accumulation
+                acc += x.float()
+            return acc
+
+        res = {"ok": True, "checks": {}}
+        try:
+            for salt, (name, n) in enumerate(rows.items()):
+                xs = inputs(n, salt)
+                out = torch.empty_like(xs[self.rank])
+                self.all_reduce(xs[self.rank].clone(), out, two_shot=(name == "two_shot"))
+                if inject_rank == self.rank and name == "one_shot":
+                    out.view(-1)[0] += 1.0
+                exp = oracle(xs)
+                res["checks"][name] = bool(torch.equal(out, exp.to(torch.bfloat16)))
+                if name == "one_shot":
+                    resid = xs[(self.rank + 1) % W].clone()  # any residual both sides know
+                    want = (resid.float() + exp.to(torch.bfloat16).float()).to(torch.bfloat16)
+                    self.all_reduce_add(xs[self.rank].clone(), resid)
+                    res["checks"]["all_reduce_add"] = bool(torch.equal(resid, want))
+                    b = xs[self.rank].clone()
+                    self.broadcast(b, 0)
+                    res["checks"]["broadcast"] = bool(torch.equal(b, xs[0]))
+                    ga = self.all_gather(xs[self.rank])
+                    res["checks"]["all_gather"] = bool(torch.equal(ga, torch.stack(xs)))
+                    # the process-group path the fallback would use, on the same inputs
+                    pg = xs[self.rank].float()
+                    if dist.is_initialized() and W > 1:
+                        on_cpu = dist.get_backend(self.group) == "gloo"
+                        t = pg.cpu() if on_cpu else pg
+                        dist.all_reduce(t, group=self.group)
+                        pg = t.to(dev)
+                    res["checks"]["process_group"] = bool(
+                        torch.allclose(pg, exp, rtol=1e-5, atol=1e-5 * W))
+            torch.cuda.synchronize(dev)
+            res["error_word"] = self.error()
+        except Exception as e:  # noqa: BLE001 - reported, the group falls back together
+            res["exception"] = f"{type(e).__name__}: {e}"
+            res["error_word"] = -1
+        res["ok"] = (res["error_word"] == 0 and bool(res["checks"])
+                     and all(v for k, v in res["checks"].items() if k != "process_group"))
+        return res
+
+    def agree(self, verdict: dict) -> bool:
+        """Every rank's self-check verdict -> the group's (MIN over ranks, on the host group when
+        the process group is gloo, else a device tensor over RCCL): the whole group keeps K15 or
+        the whole group falls back, never a mix (a rank on K15 would wait forever for a peer
+        that posts nothing)."""
+        if self.world == 1 or not dist.is_initialized():
+            return bool(verdict["ok"])
+        on_cpu = dist.get_backend(self.group) == "gloo"
+        t = torch.tensor([1 if verdict["ok"] else 0], dtype=torch.int64,
+                         device="cpu" if on_cpu else self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))

@@ -28,6 +28,7 @@ def _run(cmd):
 
 
 ARGS = ["--model", "tiny-llama", "--steps", "4", "--warmup", "2", "--batch", "8"]
+TP_ARGS = ["--tp-batch", "16", "--tp-steps", "3", "--tp-warmup", "1"]
 
 
 def test_bench_single_process_json():
@@ -60,20 +61,37 @@ def test_bench_reports_http_served_rate():
 def test_bench_two_ranks_gloo():
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-              os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0", *ARGS])
+              os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0", *ARGS, *TP_ARGS])
     assert d["dist"] == {"world_size": 2, "backend": "gloo", "launcher": "torch.distributed.run"}
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["global_batch"] == 16 and d["value"] > 0
     # whole-job aggregate over ranks = per-GPU value x N
     assert abs(d["served_tokens_per_sec_per_gpu"] * 2 - d["value"]) < 1e-3 * d["value"] + 0.02
+    # after the DP replicas, a TP = world phase on the same ranks (the
+    # xGMI path on a GPU node): its own rate, K15 state (off on CPU) and the greedy tokens of
+    # 8 fixed prompts against the dense TP = 1 recompute
+    tp = d["tp"]
+    assert tp["tp"] == 2 and tp["world"] == 2 and tp["backend"] == "gloo" and tp["k15"] == "off"
+    assert tp["tokens_per_sec"] > 0 and tp["steps"] == 3 and tp["batch"] == 16
+    assert tp["first_token_match"] and tp["tokens_match"] and tp["tokens_checked"] == 32
+
+
+def test_bench_tp_phase_watchdog_keeps_the_dp_result():
+    """A TP phase that overruns --tp-timeout (a first-contact hang on real peers) must not cost
+    the DP value: rank 0 prints THE line with tp.error and every rank exits 0."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
+              *ARGS, "--tp-batch", "64", "--tp-steps", "200", "--tp-timeout", "3"])
+    assert d["value"] > 0 and d["n_gpus"] == 2
+    assert "tp-timeout" in d["tp"]["error"]
 
 
 def test_bench_self_launches_n_ranks():
     """``python bench.py --gpus 2`` with no torchrun around it (the driver's plain command):
     bench.py launches the 2 rank processes itself, both replicas' tokens are counted, and
     the line says which world actually ran."""
-    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS])
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS, *TP_ARGS])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["tp"]["tokens_per_sec"] > 0 and d["tp"]["first_token_match"]
     assert d["dist"] == {"world_size": 2, "backend": "gloo", "launcher": "bench.py"}
     assert len(d["per_rank_tokens_per_sec"]) == 2 and min(d["per_rank_tokens_per_sec"]) > 0
     assert d["cr_ready_path"] == "fresh predictor process"  # probed once by the launcher parent

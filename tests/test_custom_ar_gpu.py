@@ -211,3 +211,55 @@ def test_custom_all_reduce_two_processes_one_gpu(world, split):
         assert all(res["gather"]), (r, res["gather"])
         assert all(res["contention"]), (r, res["contention"])
         assert all(res["add"]), (r, res["add"])
+
+
+def _selfcheck_worker(rank, world, port, out_dir, inject):
+    """make_parallel_state's first-contact check (custom_ar.py self_check / agree) on the gloo
+    group: clean -> every rank keeps K15 ("ok"); one rank's K15 output perturbed
+    (MLOP_INJECT_CAR_CORRUPT) -> EVERY rank falls back to the process-group path, and the
+    fallback all-reduce still gives the right sum."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MLOP_CUSTOM_AR="force")
+    if inject is not None:
+        os.environ["MLOP_INJECT_CAR_CORRUPT"] = str(inject)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mlopamd.parallel.comm import make_parallel_state
+
+    ps = make_parallel_state(tp_size=world)
+    res = {"status": ps.tp.car_status, "has_car": ps.tp.car is not None, "check": ps.tp.car_check}
+    xs = _inputs(7, 4096, world)
+    x = xs[rank].cuda()
+    if ps.tp.car is None:  # gloo fallback carries CPU tensors in this rehearsal
+        xc = x.float().cpu()
+        dist.all_reduce(xc)
+        res["sum_ok"] = bool(torch.allclose(xc, sum(t.float() for t in xs), atol=1e-2))
+    else:
+        ps.tp.all_reduce(x)
+        torch.cuda.synchronize()
+        res["sum_ok"] = bool(torch.equal(x.cpu(), _oracle(xs)))
+        ps.tp.car.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+
+
+@pytest.mark.parametrize("inject", [None, 1])
+def test_custom_all_reduce_self_check_and_group_fallback(inject):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = tempfile.mkdtemp()
+    world = 2
+    mp.start_processes(_selfcheck_worker, args=(world, _free_port(), d, inject), nprocs=world, join=True,
+                       start_method="spawn")
+    rs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]
+    for r, res in enumerate(rs):
+        assert res["sum_ok"], (r, res)
+        if inject is None:
+            assert res["status"] == "ok" and res["has_car"], (r, res)
+            assert res["check"]["ok"] and all(res["check"]["checks"].values()), (r, res)
+        else:
+            # only rank 1's own one-shot check failed, yet the whole group fell back
+            assert res["status"] == "fallback" and not res["has_car"], (r, res)
+            assert res["check"]["checks"]["one_shot"] == (r != inject), (r, res)
