@@ -34,9 +34,10 @@ from .kube import ApiError
 from .mlflow import NotFound, RegistryError, RegistryUnavailable
 from .placement import plan
 
+from .prometheus import MetricsUnavailable, get_model_metrics, gpu_guard_queries, should_promote
+
 ANN = seldon.ANN_PREFIX
 SELDON_POD_LABEL = seldon.POD_LABEL
-from .prometheus import MetricsUnavailable, get_model_metrics, gpu_guard_queries, should_promote
 
 PH_DEPLOYING, PH_READY, PH_CANARY = "Deploying", "Ready", "Canary"
 PH_PROMOTED, PH_ROLLED_BACK, PH_FAILED, PH_NO_ALIAS = "Promoted", "RolledBack", "PromotionFailed", "AliasNotFound"
@@ -227,6 +228,11 @@ class MlflowModelReconciler:
         node = None
         existing = None
         notes = {}
+        # GPUs of this SD's predictors placed earlier in this pass while no node had been read
+        # yet (a reused placement skips the node read).  node_capacity excludes the SD's OWN
+        # pods, so a later predictor's free count must be charged with them explicitly: a canary
+        # never plans onto the GPUs the running version still holds
+        held_before_node = 0
         for v, traffic in versions:
             uri, mv = await self._uri(spec, v)
             runtime, arch = self._runtime_of(spec, mv)
@@ -244,6 +250,8 @@ class MlflowModelReconciler:
                 else:
                     if node is None:
                         node = await self.node_capacity(exclude=(md["namespace"], md["name"]))
+                        if node.get("free_gpus") is not None and held_before_node:
+                            node = dict(node, free_gpus=max(0, node["free_gpus"] - held_before_node))
                     p = plan(arch, max_model_len=spec.max_model_len or 4096, max_num_seqs=spec.max_num_seqs or 256,
                              hbm_gb=node.get("hbm_gb", self.settings.hbm_per_gpu_gb),
                              gpus_per_node=node.get("gpus", self.settings.gpus_per_node),
@@ -259,7 +267,9 @@ class MlflowModelReconciler:
                         notes[seldon.predictor_name(v)] = p.reason + (
                             f" [GPU accounting: {node['accounting']}]" if node.get("accounting") else "")
                     gpus_held = p.gpus
-                if node is not None and node.get("free_gpus") is not None:
+                if node is None:
+                    held_before_node += gpus_held * spec.replicas
+                elif node.get("free_gpus") is not None:
                     # the canary's second predictor needs its own GPUs beside this one's
                     node = dict(node, free_gpus=max(0, node["free_gpus"] - gpus_held * spec.replicas))
             elif runtime == seldon.RUNTIME_LLM and (spec.tensor_parallel or spec.expert_parallel):
@@ -388,7 +398,7 @@ class MlflowModelReconciler:
 
         # ---- level-triggered apply of the desired deployment
         desired = await self.desired_sd(body, spec, status)
-        notes = self.placement_notes.get((ns, name)) or None
+        notes = self.placement_notes.pop((ns, name), None) or None  # consumed: no stale entries
         if desired is not None and status.get("placement") != notes:  # why a predictor cannot be placed
             body = await self._patch_status(ns, name, {"placement": notes})
             status["placement"] = notes

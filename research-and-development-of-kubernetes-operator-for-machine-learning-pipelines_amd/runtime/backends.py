@@ -123,10 +123,7 @@ class LLMBackend:
             now = time.perf_counter()
             self.ktime.after_step(now)
             if self.metrics:
-                self.metrics.engine_steps.labels(**self.metrics.labels).inc()
-                if len(outs):
-                    self.metrics.engine_tokens.labels(**self.metrics.labels).inc(len(outs))
-                self.metrics.engine_clock.labels(**self.metrics.labels).set(now)
+                self.metrics.mark_step(len(outs), now)
             for o in outs:
                 r = self._active.get(o.seq_id)
                 if r is None:

@@ -108,7 +108,11 @@ class EPGroupLoop:
         self.local: dict[int, int] = {}  # local seq_id -> global request id
         self.iterations = 0
         # one slot holds a longest prompt's record, and every output row of a full engine
-        self.max_words = max(32768, engine.max_model_len + 64, 8 * engine.cfg.max_num_seqs + 64)
+        # one slot must hold the largest request any backend accepts (packed_words: a prompt of
+        # max_model_len ids + MAX_STOP_IDS stop ids + the header) and a step's output records
+        from .sampler import MAX_STOP_IDS
+
+        self.max_words = max(32768, engine.max_model_len + MAX_STOP_IDS + 64, 8 * engine.cfg.max_num_seqs + 64)
         self.xg = make_host_allgather(self.group, self.max_words)
         self._none = torch.zeros(0, dtype=torch.int64)
 
@@ -228,10 +232,7 @@ class EPBackend(LLMBackend):
                     n_tok += 1
                     self._deliver(_Out(rid, tok, bool(fin), REASON_NAMES.get(code)), now)
             if self.metrics:
-                self.metrics.engine_steps.labels(**self.metrics.labels).inc()
-                if n_tok:
-                    self.metrics.engine_tokens.labels(**self.metrics.labels).inc(n_tok)
-                self.metrics.engine_clock.labels(**self.metrics.labels).set(time.perf_counter())
+                self.metrics.mark_step(n_tok, time.perf_counter())
                 m = self.metrics
                 m.running.labels(**m.labels).set(sum(self.load))
         self.stopped.set()

@@ -32,7 +32,8 @@ async def _scrape(session, url) -> dict:
         txt = await r.text()
     out = {}
     for name in ("mlop_engine_steps_total", "mlop_engine_tokens_total", "mlop_prompt_tokens_total",
-                 "mlop_num_requests_waiting", "mlop_num_requests_running", "mlop_engine_clock_seconds"):
+                 "mlop_num_requests_waiting", "mlop_num_requests_running", "mlop_engine_clock_seconds",
+                 "mlop_engine_tokens_at_clock"):
         m = re.search(rf"^{name}\{{[^}}]*\}} ([0-9.e+]+)$", txt, re.M)
         out[name] = float(m.group(1)) if m else 0.0
     return out
@@ -196,12 +197,17 @@ async def run(model: str = "llama3-8b", batch: int = 2048, prompt_len: int = 256
                 t.cancel()
             await asyncio.gather(*tasks, return_exceptions=True)
         n_steps = b["mlop_engine_steps_total"] - a["mlop_engine_steps_total"]
-        toks = b["mlop_engine_tokens_total"] - a["mlop_engine_tokens_total"]
         # the window's time on the predictor's engine clock (end of the first / last counted
         # step), not between the two scrape responses: a scrape answered late by the busy event
-        # loop lengthened the client-side window by up to ~12 % (two 33.7k vs 38.5k samples)
+        # loop lengthened the client-side window by up to ~12 % (two 33.7k vs 38.5k samples).
+        # Tokens from the SAME snapshot as each clock reading (metrics.mark_step)
         ck = b["mlop_engine_clock_seconds"] - a["mlop_engine_clock_seconds"]
-        dt = ck if a["mlop_engine_clock_seconds"] > 0 and ck > 0 else t_b - t_a
+        if a["mlop_engine_clock_seconds"] > 0 and ck > 0:
+            dt = ck
+            toks = b["mlop_engine_tokens_at_clock"] - a["mlop_engine_tokens_at_clock"]
+        else:
+            dt = t_b - t_a
+            toks = b["mlop_engine_tokens_total"] - a["mlop_engine_tokens_total"]
         out.update(served_tokens_per_sec_http=round(toks / dt, 2), http_window_steps=int(n_steps),
                    http_ms_per_step=round(1e3 * dt / max(n_steps, 1), 3),
                    http_window_client_s=round(t_b - t_a, 3), http_window_engine_s=round(ck, 3),

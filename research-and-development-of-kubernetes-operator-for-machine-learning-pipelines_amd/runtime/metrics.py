@@ -17,8 +17,31 @@ from __future__ import annotations
 import os
 
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+from prometheus_client.core import GaugeMetricFamily
 
 LAT_BUCKETS = (0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0, 30.0, 60.0, 120.0)
+
+
+class _EngineClock:
+    """Collector of ``mlop_engine_clock_seconds`` + ``mlop_engine_tokens_at_clock`` from one
+    tuple the engine thread replaces atomically (``RuntimeMetrics.mark_step``)."""
+
+    def __init__(self, labels: dict):
+        self.names = list(labels)
+        self.values = [str(labels[k]) for k in self.names]
+        self.snap = (0.0, 0.0)
+
+    def collect(self):
+        tokens, clock = self.snap
+        g = GaugeMetricFamily("mlop_engine_clock_seconds", "Engine-thread clock at the end of the last step",
+                              labels=self.names)
+        g.add_metric(self.values, clock)
+        yield g
+        t = GaugeMetricFamily("mlop_engine_tokens_at_clock",
+                              "Engine tokens emitted up to mlop_engine_clock_seconds (same snapshot)",
+                              labels=self.names)
+        t.add_metric(self.values, tokens)
+        yield t
 
 
 class RuntimeMetrics:
@@ -61,13 +84,24 @@ class RuntimeMetrics:
         self.gpu_power = Gauge("mlop_gpu_power_watts", "Socket power", base + ["gpu"], registry=r)
         self.engine_steps = Counter("mlop_engine_steps", "Engine steps executed", base, registry=r)
         self.engine_tokens = Counter("mlop_engine_tokens", "Tokens emitted by engine steps", base, registry=r)
-        # the engine thread's perf_counter at the end of its last step, set right after the two
-        # counters above: a rate over two scrapes then needs no client-side clock (the scrape's
-        # own latency on a busy event loop skewed a 2-3 s window by up to ~12 %)
-        self.engine_clock = Gauge("mlop_engine_clock_seconds", "Engine-thread clock at the end of the last step",
-                                  base, registry=r)
+        # the engine thread's perf_counter at the end of its last step AND the token total at that
+        # instant, exported from ONE snapshot (``mark_step``): a rate over two scrapes then needs
+        # no client-side clock (the scrape's own latency on a busy event loop skewed a 2-3 s
+        # window by up to ~12 %), and a scrape can never pair a new token count with an old clock
+        # (two separately collected series could, by up to one step's tokens at each end)
+        self._tok_total = 0.0
+        self._clock = _EngineClock(self.labels)
+        r.register(self._clock)
         self.kernel_time = Gauge("mlop_kernel_time_fraction", "rocprof kernel-time share per kernel class",
                                  base + ["kernel"], registry=r)
+
+    def mark_step(self, tokens: int, now: float) -> None:
+        """Engine thread, once per step: the step counters and the (token total, clock) pair."""
+        self.engine_steps.labels(**self.labels).inc()
+        if tokens:
+            self.engine_tokens.labels(**self.labels).inc(tokens)
+        self._tok_total += tokens
+        self._clock.snap = (self._tok_total, now)  # one reference store: scrapes see a consistent pair
 
     def lv(self, **extra):
         return dict(self.labels, **extra)

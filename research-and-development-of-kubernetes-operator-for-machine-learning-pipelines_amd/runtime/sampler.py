@@ -13,6 +13,9 @@ import torch
 from .. import ops
 
 I32_MAX = 2**31 - 1
+# stop ids per request: bounded so every backend (single GPU, TP, the EP group's fixed control
+# slot, ep_serving.py) accepts and rejects the same requests
+MAX_STOP_IDS = 256
 
 
 @dataclass
@@ -46,6 +49,8 @@ class SamplingParams:
             self.top_k = 0  # beyond any vocabulary: the same as no top-k bound (full vocabulary)
         if not (0.0 < float(self.top_p) <= 1.0):
             raise ValueError(f"top_p must be in (0, 1], got {self.top_p}")
+        if len(self.stop_token_ids) > MAX_STOP_IDS:
+            raise ValueError(f"at most {MAX_STOP_IDS} stop_token_ids, got {len(self.stop_token_ids)}")
         if any(not isinstance(t, int) or not 0 <= t <= I32_MAX for t in self.stop_token_ids):
             raise ValueError(f"stop_token_ids must be ints in [0, {I32_MAX}]")
         if self.seed is not None and (not isinstance(self.seed, int) or not 0 <= self.seed < 2**63):

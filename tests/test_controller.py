@@ -563,6 +563,42 @@ def test_own_predictor_pods_do_not_move_the_placement():
     run(go())
 
 
+def test_canary_is_planned_with_the_running_versions_gpus_charged():
+    """v1's placement is REUSED from its annotations (no node read for
+    it), and node_capacity excludes the model's own pods, so the canary's v2 must be charged
+    with v1's GPUs explicitly.  8-GPU node: v1 (TP=4) holds 4 through its own pod, another
+    team 2 -> 2 left, so a TP=4 v2 does not fit (before the fix it was planned onto 6)."""
+    async def go():
+        env = Env()
+        await env.kube.create("", "v1", None, "nodes", _gpu_node("mi355x-0", 8))
+        v1 = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v1)
+        await env.start()
+        await env.create_cr(tensorParallel=4, maxModelLen=8192, maxNumSeqs=64)
+        assert await env.run_until(lambda: _ready(env))
+        own = _gpu_pod("m-v1-0", "mi355x-0", 4)
+        own["metadata"].update(namespace=NS, labels={"seldon-deployment-id": "m"})
+        await env.kube.create("", "v1", NS, "pods", own)
+        await env.kube.create("", "v1", "team", "pods", _gpu_pod("x", "mi355x-0", 2))
+        v2 = env.version(tags={"mlop.architecture": "llama3-70b"})
+        env.reg.set_alias("m", "champion", v2)
+
+        async def split():
+            sd = await env.sd()
+            return sd is not None and len(sd["spec"]["predictors"]) == 2
+
+        assert await env.run_until(split)
+        preds = {p["name"]: p for p in (await env.sd())["spec"]["predictors"]}
+        assert preds["v1"]["annotations"]["mlop.amd.com/fits"] == "True"  # v1 keeps its placement
+        assert preds["v2"]["annotations"]["mlop.amd.com/fits"] == "False", preds["v2"]["annotations"]
+        why = (await env.status())["placement"]["v2"]
+        assert "2 of 8" in why, why
+        # the planner's notes are consumed by the pass that wrote them (no stale entries)
+        assert (NS, "m") not in env.rec.placement_notes
+        await env.stop()
+    run(go())
+
+
 def test_placement_uses_node_vram_label():
     from mlopamd.controller import placement
 

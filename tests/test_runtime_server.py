@@ -289,3 +289,29 @@ def test_hip_warmup_loads_torchs_own_runtime():
     maps = ast.literal_eval(out.stdout.strip().splitlines()[-1])
     torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
     assert len(maps) == 1 and maps[0].startswith(torch_lib), maps
+
+
+def test_engine_clock_and_tokens_come_from_one_snapshot():
+    """the HTTP served rate pairs the engine clock with the token total taken
+    at that same instant (one collector over one tuple), never a token count from another step."""
+    from mlopamd.runtime.metrics import RuntimeMetrics
+    from prometheus_client import generate_latest
+
+    m = RuntimeMetrics(deployment="d", predictor="v1", namespace="ns")
+    m.mark_step(7, 10.5)
+    m.mark_step(0, 11.0)
+    m.mark_step(5, 12.25)
+    txt = generate_latest(m.registry).decode()
+    vals = {ln.split("{")[0]: float(ln.rsplit(" ", 1)[1]) for ln in txt.splitlines()
+            if ln.startswith("mlop_engine_") and "{" in ln}
+    assert vals["mlop_engine_clock_seconds"] == 12.25 and vals["mlop_engine_tokens_at_clock"] == 12
+    assert vals["mlop_engine_tokens_total"] == 12 and vals["mlop_engine_steps_total"] == 3
+
+
+def test_stop_token_ids_are_bounded_for_every_backend():
+    import pytest as _pytest
+    from mlopamd.runtime.sampler import MAX_STOP_IDS, SamplingParams
+
+    SamplingParams(stop_token_ids=list(range(MAX_STOP_IDS))).validate()
+    with _pytest.raises(ValueError, match="stop_token_ids"):
+        SamplingParams(stop_token_ids=list(range(MAX_STOP_IDS + 1))).validate()
