@@ -13,7 +13,9 @@ Every predictor here is an OS process on the same GPU (two 8B models = 32 GB,
 two Mixtral-8x7B = 187 GB: both fit one 288 GB MI355X), which is how one box
 stands in for the two 1-GPU pods of config 3.  ``regress`` injects a fault into
 the NEW version's pods only (per-predictor env of the launcher): ``latency``
-(+ s per request), ``errors`` (HTTP 500 share) — the gate must roll it back.
+(+ s per request), ``errors`` (HTTP 500 share), ``tpot`` (a device delay kernel in every
+engine step: slower on the GPU only, with the latency thresholds loosened so that only the
+GPU-side TPOT guard can decide) — the gate must roll it back.
 """
 from __future__ import annotations
 
@@ -28,6 +30,16 @@ FAULTS = {
     None: {},
     "latency": {"MLOP_INJECT_LATENCY_S": "0.25"},
     "errors": {"MLOP_INJECT_ERROR_RATE": "0.3"},
+    # device-only slowdown: every engine step of v2 also runs a 1.5 ms device delay kernel, so its
+    # TPOT rises while the HTTP layer is untouched; the gate's latency thresholds are loosened
+    # for this case (GATES) so that only the GPU-side TPOT guard can reject it
+    "tpot": {"MLOP_INJECT_STEP_DEVICE_US": "1500"},
+}
+
+# per-regression gate overrides: "tpot" keeps the TPOT guard at its 1.10 default and lets p95 /
+# mean latency rise 5x, i.e. the Seldon-executor latency gate alone would promote v2
+GATES = {
+    "tpot": {"thresholds": {"latency_95th": 4.0, "latency_avg": 4.0}, "gpuGuards": {"tpot_avg": 1.10}},
 }
 
 
@@ -79,12 +91,13 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
     router = Router(ctl)
     scraper.start()
     await op.start()
-    cr = mlflow_model_cr(name, namespace, name, "champion", interval=2,
-                         canary={"step": 30, "intervalSeconds": 3, "attemptDelaySeconds": 1,
-                                 "maxAttempts": 6, "windowSeconds": 8, "errorRateFloor": 0.01,
-                                 "latencyFloorSeconds": 0.02,
-                                 # shared-GPU pods: power / HBM of the card are common to both
-                                 "gpuGuards": {"tpot_avg": 1.5}},
+    canary = {"step": 30, "intervalSeconds": 3, "attemptDelaySeconds": 1,
+              "maxAttempts": 6, "windowSeconds": 8, "errorRateFloor": 0.01,
+              "latencyFloorSeconds": 0.02,
+              # shared-GPU pods: power / HBM of the card are common to both
+              "gpuGuards": {"tpot_avg": 1.5}}
+    canary.update(GATES.get(regress, {}))
+    cr = mlflow_model_cr(name, namespace, name, "champion", interval=2, canary=canary,
                          maxNumSeqs=max(16, 2 * concurrency), maxModelLen=1024)
     t_cr = time.perf_counter()
     await kube.create(GROUP, VERSION, namespace, PLURAL, cr)
@@ -174,7 +187,7 @@ if __name__ == "__main__":
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--arch", default="tiny-llama")
-    ap.add_argument("--regress", choices=["latency", "errors"], default=None)
+    ap.add_argument("--regress", choices=sorted(k for k in FAULTS if k), default=None)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--concurrency", type=int, default=8)
     ap.add_argument("--gpu-slots", type=int, default=None, help="predictors per GPU (default: 2 on a 1-GPU node)")

@@ -86,6 +86,16 @@ void silu_mul(Tensor out, Tensor x, int64_t interleaved) {
                         cur_stream());
 }
 
+// fault injection: a device-side delay of `us` microseconds on the current stream
+void device_delay(int64_t us) {
+  int dev = 0, khz = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "device_delay: hipGetDevice");
+  TORCH_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0,
+              "device_delay: wall clock rate");
+  TORCH_CHECK(us >= 0 && us <= 10000000, "device_delay: 0..10 s");
+  mlop::launch_device_delay((long long)us * khz / 1000, cur_stream());
+}
+
 void embedding(Tensor out, Tensor table, Tensor ids, int64_t vocab_start) {
   check_bf16(out, "out"); check_bf16(table, "table");
   TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids int64");
@@ -774,6 +784,7 @@ std::string src_hash() { return std::string(mlop_src_hash()); }
 
 TORCH_LIBRARY(mlop, m) {
   m.def("src_hash() -> str", &src_hash);
+  m.def("device_delay(int us) -> ()", &device_delay);
   m.def("car_create(int rank, int world, int max_bytes, int device, bool split=False) -> int", &car_create);
   m.def("car_ipc_handle(int h) -> Tensor", &car_ipc_handle);
   m.def("car_open(int h, Tensor handles) -> ()", &car_open);

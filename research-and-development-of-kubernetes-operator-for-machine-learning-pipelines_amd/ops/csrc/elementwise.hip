@@ -65,4 +65,17 @@ void launch_embedding(void* out, const void* table, const long* ids, int T, int 
                                       vocab_end);
 }
 
+// Fault injection only (MLOP_INJECT_STEP_DEVICE_US, runtime/engine.py): one wave that waits until
+// the constant-rate wall clock has advanced `ticks`, so an engine step gets slower ON THE DEVICE
+// alone (the host stays idle) -- the canary test of the GPU-side TPOT guard.  Always terminates.
+__global__ void __launch_bounds__(64) device_delay_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+void launch_device_delay(long long ticks, hipStream_t st) {
+  if (ticks <= 0) return;
+  device_delay_kernel<<<1, 64, 0, st>>>(ticks);
+}
+
 }  // namespace mlop

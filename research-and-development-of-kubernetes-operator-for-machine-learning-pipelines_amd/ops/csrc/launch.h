@@ -18,6 +18,7 @@ void launch_rope_cache(void* q_out, void* k_cache, void* v_cache, const void* qk
                        const float* cos_sin, const int* slots, int T, int Hq, int Hkv, int D,
                        int qkv_stride, int BS, hipStream_t st);
 void launch_silu_mul(void* out, const void* x, int M, int I, int interleaved, hipStream_t st);
+void launch_device_delay(long long ticks, hipStream_t st);
 void launch_embedding(void* out, const void* table, const long* ids, int T, int H, long vocab_start,
                       long vocab_end, hipStream_t st);
 void launch_paged_attention(void* out, float* part_o, float* part_ml, const void* q,

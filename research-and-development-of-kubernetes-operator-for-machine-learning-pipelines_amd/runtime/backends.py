@@ -93,6 +93,7 @@ class LLMBackend:
         return self._thread.is_alive()
 
     def start(self):
+        self.ktime.warm()  # the tracer's one-time start-up before serving (gpu_metrics.py)
         self._thread.start()
         return self
 

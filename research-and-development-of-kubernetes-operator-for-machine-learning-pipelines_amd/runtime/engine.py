@@ -361,6 +361,16 @@ class Engine:
         self.profile_window = TorchProfileWindow()
         import os
 
+        # fault injection (canary tests of the GPU-side guards): every forward step also runs a
+        # device delay kernel of this many microseconds (ops/csrc/elementwise.hip device_delay)
+        self._inject_device_us = int(os.environ.get("MLOP_INJECT_STEP_DEVICE_US", "0") or 0)
+        if self._inject_device_us and self.device.type != "cuda":
+            self._inject_device_us = 0
+        if self._inject_device_us:
+            from .. import ops as _ops
+
+            _ops.load()
+
         # TP decode graphs capture the row-parallel all-reduces (K15 one-shot kernel, or RCCL
         # inside capture); the vocab gather runs after the replay (``_gather``).
         if cfg.use_graphs and self.device.type == "cuda":
@@ -1187,6 +1197,8 @@ class Engine:
         return kind, b_max, b_max, b_max, part, nparts, b_max
 
     def _execute(self, kind, T, nt, nl, part, nparts, bucket, npt=0, greedy=0):
+        if self._inject_device_us:  # fault injection: this step is slower on the device only
+            torch.ops.mlop.device_delay(self._inject_device_us)
         if kind == KIND_GRAPH:
             graph, logits_buf = self.graphs[bucket]
             graph.replay()

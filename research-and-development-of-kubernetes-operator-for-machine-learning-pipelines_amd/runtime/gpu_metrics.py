@@ -174,20 +174,50 @@ class KernelTimeSampler:
         self._prof = None
         self._done_ev = None
         self.windows = 0
+        # the sampler's own cost ON THE ENGINE THREAD (opening + closing + reducing a window),
+        # per window, and the one-time tracer start-up paid in ``warm``
+        self.host_ms: list = []
+        self._open_ms = 0.0
+        self.warm_ms = None
 
-    def before_step(self, now: float) -> None:
-        if self.period_s <= 0 or now < self._next or self._prof is not None:
+    def warm(self) -> None:
+        """Pay the tracer's one-time start-up (profiler library + HIP activity callbacks) now, at
+        predictor start-up before it reports ready, with a throwaway window around one tiny
+        kernel -- not inside the first served window, where it stalled the step loop."""
+        import time
+
+        if self.period_s <= 0 or self.warm_ms is not None:
             return
         import torch
 
         if not torch.cuda.is_available():
             return
+        t0 = time.perf_counter()
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as p:
+            torch.ones(1, device="cuda").add_(1)
+            torch.cuda.synchronize()
+        p.key_averages()
+        self.warm_ms = round(1e3 * (time.perf_counter() - t0), 3)
+
+    def before_step(self, now: float) -> None:
+        if self.period_s <= 0 or now < self._next or self._prof is not None:
+            return
+        import time
+
+        import torch
+
+        if not torch.cuda.is_available():
+            return
+        t0 = time.perf_counter()
         self._prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA])
         self._prof.__enter__()
+        self._open_ms = 1e3 * (time.perf_counter() - t0)
 
     def after_step(self, now: float) -> dict | None:
         if self._prof is None:
             return None
+        import time
+
         import torch
 
         if self._done_ev is None:  # the profiled step was just launched: mark its end
@@ -196,6 +226,7 @@ class KernelTimeSampler:
             return None
         if not self._done_ev.query():  # still running: look again after the next step
             return None
+        t0 = time.perf_counter()
         self._prof.__exit__(None, None, None)
         ev = [(e.key, float(getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)))
               for e in self._prof.key_averages()]
@@ -203,6 +234,8 @@ class KernelTimeSampler:
         self._next = now + self.period_s
         self.windows += 1
         shares = shares_from_events(ev)
+        self.host_ms.append(round(self._open_ms + 1e3 * (time.perf_counter() - t0), 3))
+        del self.host_ms[:-64]
         if shares:
             self.last = shares
             if self.on_shares is not None:

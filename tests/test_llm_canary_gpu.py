@@ -14,6 +14,9 @@ pytestmark = pytest.mark.gpu
     ("tiny-llama", None, "Promoted"),
     ("tiny-llama", "latency", "RolledBack"),
     ("tiny-mixtral", "errors", "RolledBack"),
+    # v2 slowed on the device only; p95 / mean latency may rise 5x and still
+    # pass, so the rollback must come from the GPU-side TPOT guard at its 1.10 default
+    ("tiny-llama", "tpot", "RolledBack"),
 ])
 def test_llm_canary_on_gpu(gpu, arch, regress, expect):
     from mlopamd.controller.llm_demo import run_llm_canary
@@ -24,5 +27,8 @@ def test_llm_canary_on_gpu(gpu, arch, regress, expect):
     if expect == "RolledBack":
         assert r["final_predictors"] == {"v1": 100} and r["rolled_back_version"] == "2"
         assert r["events"][-1] == "RollbackComplete"
+        if regress == "tpot":  # the guard that decided is named in status.error
+            assert "tpot_avg" in (r["error"] or ""), r
+            assert not any(k in (r["error"] or "") for k in ("latency_95th", "latency_avg", "error_rate")), r
     else:
         assert r["final_predictors"] == {"v2": 100} and r["events"][-1] == "PromotionComplete"
