@@ -30,16 +30,17 @@ FAULTS = {
     None: {},
     "latency": {"MLOP_INJECT_LATENCY_S": "0.25"},
     "errors": {"MLOP_INJECT_ERROR_RATE": "0.3"},
-    # device-only slowdown: every engine step of v2 also runs a 1.5 ms device delay kernel, so its
-    # TPOT rises while the HTTP layer is untouched; the gate's latency thresholds are loosened
-    # for this case (GATES) so that only the GPU-side TPOT guard can reject it
-    "tpot": {"MLOP_INJECT_STEP_DEVICE_US": "1500"},
+    # device-only slowdown: every engine step of v2 also runs a 0.2 ms device delay kernel (a
+    # tiny-llama step is ~0.16 ms: TPOT x ~2), while the HTTP layer is untouched; the gate's
+    # latency thresholds are loosened for this case (GATES) so only the GPU-side TPOT guard can
+    # reject it (1.5 ms made p95 / mean 10x worse than v1: beyond any loosened latency bound)
+    "tpot": {"MLOP_INJECT_STEP_DEVICE_US": "200"},
 }
 
 # per-regression gate overrides: "tpot" keeps the TPOT guard at its 1.10 default and lets p95 /
-# mean latency rise 5x, i.e. the Seldon-executor latency gate alone would promote v2
+# mean latency rise 10x, i.e. the Seldon-executor latency gate alone would promote v2
 GATES = {
-    "tpot": {"thresholds": {"latency_95th": 4.0, "latency_avg": 4.0}, "gpuGuards": {"tpot_avg": 1.10}},
+    "tpot": {"thresholds": {"latency_95th": 9.0, "latency_avg": 9.0}, "gpuGuards": {"tpot_avg": 1.10}},
 }
 
 

@@ -243,6 +243,7 @@ int64_t gemm_slab_nt(int64_t set) { return mlop::gemm_slab_nt((int)set); }
 int64_t gemm_rope_split(int64_t set) { return mlop::gemm_rope_split((int)set); }
 int64_t gemm_split_target(int64_t set) { return mlop::gemm_split_target((int)set); }
 int64_t gemm_grouped_narrow(int64_t set) { return mlop::gemm_grouped_narrow((int)set); }
+int64_t gemm_skip_dead(int64_t set) { return mlop::gemm_skip_dead((int)set); }
 int64_t moe_mid_max_tokens(int64_t set) { return mlop::moe_mid_max_tokens((int)set); }
 void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits, int64_t stages) {
   mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits, (int)stages);
@@ -444,6 +445,27 @@ bool gemm_add_rmsnorm(Tensor out, Tensor residual, Tensor a, Tensor w, Tensor no
 
 // Decode projection with the residual add + RMSNorm feeding it fused in as a prologue
 // (gemv.hip NORM, M <= 4): res_out = bf16(res_in + y); out = epi(rmsnorm(res_out) * norm_w @ w^T).
+// weight-streaming MFMA GEMM (gemm_ws.hip), plain / SiLU-mul / residual-add forms, optionally
+// with the row-scale prologue; false = shape not taken
+bool gemm_ws(Tensor out, Tensor a, Tensor w, int64_t epi, bool rs, double eps) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == at::kBFloat16 && a.dim() == 2 && a.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0, "a must be bf16 [M, K], 16-B aligned rows");
+  check_bf16(w, "w"); check_bf16(out, "out");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.stride(0) == K, "w [N, K] contiguous");
+  TORCH_CHECK(epi == 0 || epi == 1 || epi == 5, "epi 0 / 1 / 5");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N) && out.stride(1) == 1,
+              "out [M, N or N/2]");
+  TORCH_CHECK(!(rs && epi == 5), "residual form has no row scale");
+  if (!mlop::ws_takes((int)M, (int)N, (int)K, (int)epi)) return false;
+  c10::DeviceGuard g(a.device());
+  mlop::launch_ws(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, out.data_ptr(), (int)out.stride(0), (int)M,
+                  (int)N, (int)K, (int)epi, rs, mlop::RopeEpi{}, (float)eps, cur_stream());
+  return true;
+}
+
+int64_t gemm_ws_max_m(int64_t set) { return mlop::gemm_ws_max_m((int)set); }
+
 bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
 }
@@ -823,6 +845,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_rope_split(int set=-1) -> int", &gemm_rope_split);
   m.def("gemm_split_target(int set=-1) -> int", &gemm_split_target);
   m.def("gemm_grouped_narrow(int set=-1) -> int", &gemm_grouped_narrow);
+  m.def("gemm_skip_dead(int set=-1) -> int", &gemm_skip_dead);
+  m.def("gemm_ws_max_m(int set=-1) -> int", &gemm_ws_max_m);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
   m.def("gemm_dense_plan(int variant, int bm, int bn, int splits, int stages=0) -> ()", &gemm_dense_plan);
@@ -875,6 +899,7 @@ TORCH_LIBRARY(mlop, m) {
         "Tensor pos, Tensor cos_sin, Tensor slots) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor x, int interleaved=0) -> ()");
   m.def("embedding(Tensor(a!) out, Tensor table, Tensor ids, int vocab_start) -> ()");
+  m.def("gemm_ws(Tensor(a!) out, Tensor a, Tensor w, int epi, bool rs, float eps) -> bool");
   m.def("flash_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor ptile_seq, Tensor ptile_q0, Tensor q_start, Tensor q_len, Tensor ctx_len, float scale) -> ()");
   m.def("paged_attention(Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, Tensor(d!) part_sem, Tensor q, "
@@ -892,6 +917,7 @@ TORCH_LIBRARY_IMPL(mlop, CUDA, m) {
   m.impl("paged_attention", &paged_attention);
   m.impl("flash_prefill", &flash_prefill);
   m.impl("gemm", &gemm);
+  m.impl("gemm_ws", &gemm_ws);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("gemm_add_rmsnorm", &gemm_add_rmsnorm);
   m.impl("gemm_res_ss", &gemm_res_ss);

@@ -531,7 +531,7 @@ struct SkArgs {
   int n_base;   // first stream-K block (grouped: the worst-case tile count of the grid)
   int cus;      // CUs the split was planned for
   int min_half; // shortest K-range (K-tiles) the planner may cut
-  int skip_dead;  // 1: quadrants past the last row issue no MFMAs (MLOP_GEMM_SKIP_DEAD=0: A/B)
+  int skip_dead;  // 1: quadrants past the last row issue no MFMAs; 2: also 16-row blocks (gemm_skip_dead)
 };
 
 // d for the r = T % cus tail tiles of a T-tile launch: each is cut into d equal K-ranges
@@ -709,6 +709,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
           __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
       }
     };
+    // 16-row blocks of this wave's quadrant holding rows (skip_dead == 2 only; 4 otherwise): a
+    // ragged quadrant (the 1-64 row spill m-tile of an MoE expert with 256 + a few rows)
+    // multiplies only those blocks
+    const int rows_tile = __builtin_amdgcn_readfirstlane(sk.skip_dead ? m_end - m0 : BM);
+    auto live_blocks = [&](int mi) {
+      const int r = rows_tile - (grp * 128 + mi * 64);
+      return sk.skip_dead == 2 ? (r <= 0 ? 0 : r >= 64 ? 4 : (r + 15) >> 4) : 4;
+    };
     auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
       const uint16_t* sA = smem + buf * BUF;
 #pragma unroll
@@ -741,7 +749,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform): the
     // partner group's MFMAs then run alone on the SIMD.  Ragged M, and above all the last
     // m-tile of every expert in the grouped (MoE) GEMM, half empty on average.
-    const int rows_here = sk.skip_dead ? m_end - m0 : BM;
+    const int rows_here = rows_tile;
     // K-loop: two phases per K-tile, 32 MFMAs each.
     //   X(t): read A(mi 0) + B(nj 0, 1) of t | DMA A(mi 1) of t+1 -> buffer (t+1)&1
     //   Y(t): read A(mi 1) of t             | DMA A(mi 0) + B of t+2 -> buffer t&1
@@ -761,9 +769,14 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       __builtin_amdgcn_sched_barrier(0);
       // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform)
       if (grp * 128 + mi * 64 < rows_here) {
+        const int nb = live_blocks(mi);
         __builtin_amdgcn_s_setprio(1);
+        // a ragged quadrant multiplies only its live 16-row blocks (wave-uniform branches; one
+        // code path with every index static: a second, ragged copy of this block pushed the
+        // kernel past 256 VGPRs into scratch)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          if (i >= nb) continue;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -771,6 +784,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
               acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
               acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
             }
+        }
         __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -941,7 +955,13 @@ struct SkBuf {
 static SkBuf g_sk[16];
 static int g_sk_mode = 1;
 static const int g_sk_min_iters = 16;
-static const int g_skip_dead = 1;
+// dead-row skipping of the ping-pong kernel: 1 = whole 64-row quadrants, 2 = also 16-row
+// blocks of a ragged quadrant (the MoE decode spill tile; gemm_skip_dead op for A/B)
+static int g_skip_dead = 2;
+int gemm_skip_dead(int set) {
+  if (set >= 0) g_skip_dead = set;
+  return g_skip_dead;
+}
 
 int gemm_sk_mode(int set) {
   if (set >= 0) g_sk_mode = set;

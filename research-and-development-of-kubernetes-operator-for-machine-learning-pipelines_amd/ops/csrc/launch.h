@@ -74,6 +74,7 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 int gemm_big_variant(int set);
 int gemm_half_tile(int set);
 int gemm_grouped_narrow(int set);
+int gemm_skip_dead(int set);
 void gemm_grouped_plan(int bm, int bn, int stages, int splits);
 void gemm_dense_plan(int variant, int bm, int bn, int splits, int stages = 0);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip), variant 6 its 128x256
@@ -118,6 +119,13 @@ struct NormPro {
 // decode norm chain (gemv.hip PRO_RS / EPI_RES, M <= 4): C = epi(rowscale(A) . B^T) with
 // rowscale = rsqrt(mean(A_row^2) + eps) (norm weights folded into B); residual += A . B^T
 bool gemv_chain_takes(int M, int N, int K, int epi);
+// weight-streaming MFMA GEMM (gemm_ws.hip) at gemv_chain_max_m() < M <= gemm_ws_max_m() (64):
+// epi 0 plain, 1 SiLU-mul, 3 RoPE + paged K/V (re), 5 residual += (C in place); rs: A is the raw
+// residual, rows scaled by rsqrt(mean(a^2) + eps) (norm weights folded into B)
+bool ws_takes(int M, int N, int K, int epi);
+int gemm_ws_max_m(int set);
+void launch_ws(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int epi,
+               bool rs, const RopeEpi& re, float eps, hipStream_t st);
 int gemv_chain_max_m();
 void launch_gemv_rs(const void* A, int lda, const void* B, void* C, int ldc, int M, int N, int K, int epi,
                     const RopeEpi& re, float eps, hipStream_t st);

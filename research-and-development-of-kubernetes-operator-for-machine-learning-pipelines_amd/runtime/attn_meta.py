@@ -9,8 +9,8 @@ Sequence-indexed arrays (q_start, q_len, ctx_len, block_tables) are indexed by
 a stable *row* (the sequence's slot in [0, max_seqs)), so the host only
 touches the rows that changed; tiles (16 MFMA q-rows = 16/G query tokens)
 point at rows.  Rows with a prompt chunk of at least ``flash_min_q`` tokens
-get flash-prefill tiles instead (128 q-rows = 128/G tokens each, emitted
-latest-first so the longest causal ranges start first).
+get flash-prefill tiles instead (128 q-rows = 128/G tokens each, ordered
+longest-first over the whole step so the longest causal ranges start first).
 """
 from __future__ import annotations
 
@@ -55,6 +55,29 @@ MIN_PART = 128
 TARGET_WGS = 1024
 
 
+# flash-prefill tiles dispatched longest-first over the WHOLE step (LPT list scheduling), not
+# sequence by sequence: a causal tile reads kv_end = ctx - q_len + q0 + 128/G keys, so with
+# several prompts the per-sequence order put the last prompt's heaviest tiles behind most of
+# the light ones and the launch ended on them (the tail of 4 x 2048 / 16 x 512,
+# profiles/r06_flash_lpt.md).  The kv-head-fastest workgroup order inside a tile is unchanged.
+# Only for steps with a prompt chunk of >= FLASH_LPT_MIN_Q tokens: measured on one box
+# (scripts/bench_flash.py, ORDER=seq / lpt, interleaved) 4 x 2048 175 -> 166 us, 8 x 1024
+# 110 -> 96 us, 1 x 8192 / 2 x 4096 unchanged, but 16 x 512 70 -> 74 us: short prompts lose more
+# from the sequences' K / V pages interleaving in L2 than they gain in the tail.
+# MLOP_FLASH_LPT=0: the per-sequence order (A/B switch).
+FLASH_LPT = os.environ.get("MLOP_FLASH_LPT", "1") not in ("0", "false", "")
+FLASH_LPT_MIN_Q = 1024
+
+
+def order_flash_tiles(seq: np.ndarray, q0: np.ndarray, work: np.ndarray) -> None:
+    """In place: (seq, q0) tile pairs sorted by descending ``work`` (keys read), ties in their
+    given order (stable)."""
+    o = np.argsort(-work, kind="stable")
+    seq[:] = seq[o]
+    q0[:] = q0[o]
+    work[:] = work[o]
+
+
 def plan_partitions(num_tiles: int, n_kv: int, max_ctx: int, min_part: int | None = None,
                     target_wgs: int | None = None) -> tuple[int, int]:
     """Split the KV range so a launch has >= ~target_wgs workgroups (256 CUs),
@@ -87,6 +110,7 @@ class MetaBuffers:
         self.flash_min_q = flash_min_q if self.pqt else 1 << 30
         self.max_tiles = max_tokens  # worst case: one tile per token
         self.npt = 0                 # flash tiles of the last fill
+        self._pwork = np.zeros(self.max_tiles, dtype=np.int32)  # per flash tile: keys it reads
         sizes = [("positions", max_tokens), ("slots", max_tokens), ("tile_seq", self.max_tiles),
                  ("tile_q0", self.max_tiles), ("ptile_seq", self.max_tiles), ("ptile_q0", self.max_tiles),
                  ("q_start", max_seqs), ("q_len", max_seqs), ("ctx_len", max_seqs)]
@@ -199,6 +223,7 @@ class MetaBuffers:
         ts_h, tq_h = self.view_h("tile_seq"), self.view_h("tile_q0")
         pts_h, ptq_h = self.view_h("ptile_seq"), self.view_h("ptile_q0")
         npt, pqt = 0, self.pqt
+        max_flash_q = 0
         qs_h, ql_h, cl_h = self.view_h("q_start"), self.view_h("q_len"), self.view_h("ctx_len")
         qt = self.qt
         for i, row in enumerate(rows):
@@ -212,6 +237,8 @@ class MetaBuffers:
                 n = (ql + pqt - 1) // pqt
                 pts_h[npt:npt + n] = row
                 ptq_h[npt:npt + n] = np.arange(n - 1, -1, -1, dtype=np.int32) * pqt  # latest first
+                self._pwork[npt:npt + n] = (cl - ql + pqt) + ptq_h[npt:npt + n]  # keys each tile reads
+                max_flash_q = max(max_flash_q, ql)
                 npt += n
             else:
                 ntile = (ql + qt - 1) // qt
@@ -222,6 +249,8 @@ class MetaBuffers:
             if want_logits is None or want_logits[i]:
                 self.lidx_hn[nl] = t - 1
                 nl += 1
+        if npt > 1 and FLASH_LPT and max_flash_q >= FLASH_LPT_MIN_Q:
+            order_flash_tiles(pts_h[:npt], ptq_h[:npt], self._pwork[:npt])
         self.npt = npt
         return t, nt, nl
 

@@ -93,7 +93,7 @@ class LLMBackend:
         return self._thread.is_alive()
 
     def start(self):
-        self.ktime.warm()  # the tracer's one-time start-up before serving (gpu_metrics.py)
+        self.ktime.warm(background=True)  # the tracer's one-time start-up, off the engine thread
         self._thread.start()
         return self
 

@@ -164,44 +164,84 @@ class KernelTimeSampler:
     after its launch; the window closes at the first later step boundary where that event has
     completed (``Event.query()``, non-blocking).  Under one-step-ahead scheduling that is the
     next step (the engine has read its tokens), so the window covers the profiled step plus at
-    most the step queued behind it -- shares, not absolute times, are published."""
+    most the step queued behind it -- shares, not absolute times, are published.
 
-    def __init__(self, period_s: float | None = None, on_shares=None):
+    The engine thread only opens and stops the window; the event reduction (``key_averages``,
+    the bulk of a window's host cost) runs on a helper thread (``MLOP_KERNEL_SAMPLE_ASYNC``,
+    default on), and the first window opens one period after serving starts, never on the
+    first step.  The tracer's one-time start-up (~2 s measured) is paid by ``warm``, on a
+    background thread at predictor start-up (``warm(background=True)``) so neither readiness
+    nor the first window waits for it (profiles/r06_sampler.md)."""
+
+    def __init__(self, period_s: float | None = None, on_shares=None, async_reduce: bool | None = None):
         self.period_s = float(os.environ.get("MLOP_KERNEL_SAMPLE_S", 30.0) if period_s is None else period_s)
         self.on_shares = on_shares
+        self.async_reduce = (os.environ.get("MLOP_KERNEL_SAMPLE_ASYNC", "1") not in ("0", "false", "")
+                             if async_reduce is None else bool(async_reduce))
         self.last: dict = {}
-        self._next = 0.0
+        self._next = None  # first window: one period after the first step
         self._prof = None
         self._done_ev = None
         self.windows = 0
-        # the sampler's own cost ON THE ENGINE THREAD (opening + closing + reducing a window),
+        # the sampler's own cost ON THE ENGINE THREAD (opening + closing [+ reducing] a window),
         # per window, and the one-time tracer start-up paid in ``warm``
         self.host_ms: list = []
+        self.reduce_ms: list = []
         self._open_ms = 0.0
         self.warm_ms = None
+        self._warm_thread = None
+        self._reducer = None
 
-    def warm(self) -> None:
-        """Pay the tracer's one-time start-up (profiler library + HIP activity callbacks) now, at
-        predictor start-up before it reports ready, with a throwaway window around one tiny
-        kernel -- not inside the first served window, where it stalled the step loop."""
+    def warm(self, background: bool = False) -> None:
+        """Pay the tracer's one-time start-up (profiler library + HIP activity callbacks) with a
+        throwaway window around one tiny kernel, instead of inside the first served window,
+        where it stalled the step loop.  ``background``: on a daemon thread (the predictor's
+        readiness does not wait for it; a window opens only after it finished)."""
         import time
 
-        if self.period_s <= 0 or self.warm_ms is not None:
+        if self.period_s <= 0 or self.warm_ms is not None or self._warm_thread is not None:
             return
         import torch
 
         if not torch.cuda.is_available():
             return
-        t0 = time.perf_counter()
-        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as p:
-            torch.ones(1, device="cuda").add_(1)
-            torch.cuda.synchronize()
-        p.key_averages()
-        self.warm_ms = round(1e3 * (time.perf_counter() - t0), 3)
+
+        def run():
+            t0 = time.perf_counter()
+            dev = torch.cuda.current_device()
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as p:
+                with torch.cuda.device(dev):
+                    torch.ones(1, device="cuda").add_(1)
+                    torch.cuda.synchronize()
+            p.key_averages()
+            self.warm_ms = round(1e3 * (time.perf_counter() - t0), 3)
+
+        if background:
+            import threading
+
+            dev = torch.cuda.current_device()
+
+            def bg():
+                torch.cuda.set_device(dev)
+                run()
+
+            self._warm_thread = threading.Thread(target=bg, name="ktime-warm", daemon=True)
+            self._warm_thread.start()
+        else:
+            run()
 
     def before_step(self, now: float) -> None:
-        if self.period_s <= 0 or now < self._next or self._prof is not None:
+        if self.period_s <= 0 or self._prof is not None:
             return
+        if self._next is None:
+            self._next = now + self.period_s
+            return
+        if now < self._next:
+            return
+        if self._warm_thread is not None and self._warm_thread.is_alive():
+            return  # the tracer is still starting on its own thread
+        if self._reducer is not None and self._reducer.is_alive():
+            return  # the previous window is still being reduced
         import time
 
         import torch
@@ -227,17 +267,41 @@ class KernelTimeSampler:
         if not self._done_ev.query():  # still running: look again after the next step
             return None
         t0 = time.perf_counter()
-        self._prof.__exit__(None, None, None)
-        ev = [(e.key, float(getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)))
-              for e in self._prof.key_averages()]
+        prof = self._prof
+        prof.__exit__(None, None, None)
         self._prof, self._done_ev = None, None
         self._next = now + self.period_s
         self.windows += 1
-        shares = shares_from_events(ev)
+        if self.async_reduce:
+            import threading
+
+            self.host_ms.append(round(self._open_ms + 1e3 * (time.perf_counter() - t0), 3))
+            del self.host_ms[:-64]
+            self._reducer = threading.Thread(target=self._reduce, args=(prof,), name="ktime-reduce", daemon=True)
+            self._reducer.start()
+            return None
+        shares = self._reduce(prof)
         self.host_ms.append(round(self._open_ms + 1e3 * (time.perf_counter() - t0), 3))
         del self.host_ms[:-64]
+        return shares
+
+    def _reduce(self, prof) -> dict:
+        import time
+
+        t0 = time.perf_counter()
+        ev = [(e.key, float(getattr(e, "device_time_total", 0.0) or getattr(e, "cuda_time_total", 0.0)))
+              for e in prof.key_averages()]
+        shares = shares_from_events(ev)
+        self.reduce_ms.append(round(1e3 * (time.perf_counter() - t0), 3))
+        del self.reduce_ms[:-64]
         if shares:
             self.last = shares
             if self.on_shares is not None:
                 self.on_shares(shares)
         return shares
+
+    def join(self, timeout: float = 30.0) -> None:
+        """Wait for a pending background warm-up / reduction (tests, benches)."""
+        for t in (self._warm_thread, self._reducer):
+            if t is not None:
+                t.join(timeout)

@@ -31,6 +31,11 @@ for s in range(S):  # latest tiles first (the longest causal ranges dispatch fir
     n = (L + pqt - 1) // pqt
     pts += [s] * n
     ptq += list(range((n - 1) * pqt, -1, -pqt))
+if os.environ.get("ORDER", "lpt") == "lpt":  # attn_meta.order_flash_tiles (the engine: prompts >= 1024)
+    from mlopamd.runtime.attn_meta import order_flash_tiles
+
+    pts, ptq = np.asarray(pts, dtype=np.int32), np.asarray(ptq, dtype=np.int32)
+    order_flash_tiles(pts, ptq, (ptq + pqt).astype(np.int32))
 
 
 class Meta:
@@ -62,7 +67,7 @@ for _ in range(3):
     ev[1].record()
     ev[1].synchronize()
     best = min(best, ev[0].elapsed_time(ev[1]) / ITERS * 1e3)
-line = dict(S=S, L=L, tiles=len(pts), us=round(best, 1), tflops=round(flops / best / 1e6, 1))
+line = dict(S=S, L=L, order=os.environ.get("ORDER", "lpt"), tiles=len(pts), us=round(best, 1), tflops=round(flops / best / 1e6, 1))
 if os.environ.get("CHECK"):
     from mlopamd.ops import reference as ref
 

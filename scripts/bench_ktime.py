@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--period", type=float, default=5.0)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--no-warm", action="store_true")
+    ap.add_argument("--sync-reduce", action="store_true", help="reduce the window on the engine thread")
     a = ap.parse_args()
 
     from mlopamd.runtime.deploy import build_engine
@@ -68,17 +69,30 @@ def main():
 
     serve(10.0, None)  # ramp: every first-cohort prompt admitted, steady mix
     res = {"config": vars(a), "off": [], "on": []}
-    sampler = KernelTimeSampler(period_s=a.period)
-    if not a.no_warm:
-        sampler.warm()
+    sampler = KernelTimeSampler(period_s=a.period, async_reduce=not a.sync_reduce)
+    warm_steps = []
+    if not a.no_warm:  # as the predictor does: in the background, while serving
+        sampler.warm(background=True)
+        t_w = time.perf_counter()
+        while sampler._warm_thread.is_alive():
+            warm_steps += serve(0.05, None)
+        res["warm_wall_ms"] = round(1e3 * (time.perf_counter() - t_w), 1)
     res["warm_ms"] = sampler.warm_ms
     for r in range(a.rounds):
         res["off"] += serve(a.seconds, None)
         sampler._next = time.perf_counter() + 0.5  # first window half a second into the run
+        sampler.join()
         res["on"] += serve(a.seconds, sampler)
         print(f"round {r + 1}: off {len(res['off'])} steps, on {len(res['on'])} steps, "
               f"windows {sampler.windows}", file=sys.stderr, flush=True)
-    out = {"warm_ms": res["warm_ms"], "windows": sampler.windows, "window_host_ms": sampler.host_ms,
+    sampler.join()
+    if warm_steps:
+        w = np.asarray(warm_steps)
+        res["during_warm"] = {"steps": int(w.size), "p50_ms": round(float(np.percentile(w, 50)), 3),
+                              "max_ms": round(float(w.max()), 3)}
+    out = {"warm_ms": res["warm_ms"], "warm_wall_ms": res.get("warm_wall_ms"), "during_warm": res.get("during_warm"),
+           "async_reduce": sampler.async_reduce, "reduce_ms": sampler.reduce_ms,
+           "windows": sampler.windows, "window_host_ms": sampler.host_ms,
            "last_shares": {k: round(v, 4) for k, v in sorted(sampler.last.items(), key=lambda kv: -kv[1])[:8]}}
     for mode in ("off", "on"):
         t = np.asarray(res[mode])

@@ -110,11 +110,12 @@ def test_mixtral_decode_fused_moe_glue(gpu):
     _check_greedy(model, prompts, outs)
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_kernel_time_sampler_on_engine_steps(gpu, graphs):
+@pytest.mark.parametrize("graphs,async_reduce", [(False, False), (True, False), (True, True)])
+def test_kernel_time_sampler_on_engine_steps(gpu, graphs, async_reduce):
     """G3: the in-process sampler (runtime/gpu_metrics.KernelTimeSampler, what the predictor
     exports as mlop_kernel_time_fraction) sees this engine's HIP kernels -- eager launches and
-    decode-graph replays -- and splits them into the classes the canary gate guards."""
+    decode-graph replays -- and splits them into the classes the canary gate guards.
+    ``async_reduce``: the event reduction runs on a helper thread (the predictor's default)."""
     from mlopamd.runtime.gpu_metrics import KernelTimeSampler
 
     model = build_model(TINY_LLAMA, device=gpu, seed=3)
@@ -125,17 +126,24 @@ def test_kernel_time_sampler_on_engine_steps(gpu, graphs):
     for _ in range(3):  # past the prefill: the sampled step is a decode step
         eng.step()
     got = []
-    s = KernelTimeSampler(period_s=1e-6, on_shares=got.append)
-    s.before_step(0.0)
+    s = KernelTimeSampler(period_s=1e-6, on_shares=got.append, async_reduce=async_reduce)
+    s.warm()
+    s.before_step(0.0)  # the first call only arms the first window, one period later
+    assert s._prof is None
+    s.before_step(1.0)
     eng.step()
     assert s.after_step(1.0) is None  # never waits for the device: the window stays open
     sh = None
     for k in range(50):  # closes at the first step boundary after the profiled step completed
-        s.before_step(2.0 + k)
         eng.step()
         sh = s.after_step(2.0 + k)
-        if sh is not None:
+        if s.windows:
             break
+    if async_reduce:  # reduced on the helper thread: published once it finished
+        assert sh is None
+        s.join()
+        sh = s.last
     assert got and sh == got[0] and s.windows == 1, sh
+    assert s.host_ms and s.warm_ms is not None
     assert abs(sum(sh.values()) - 1.0) < 1e-6
     assert sh.get("gemm", 0) > 0 and sh.get("attention", 0) > 0, sh
