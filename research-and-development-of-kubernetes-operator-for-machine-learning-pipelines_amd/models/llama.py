@@ -161,9 +161,10 @@ class LlamaModel:
         residual = h
         M = ids.shape[0]
         # TP > 1: the decode (GEMV) form only, its residual adds riding in the all-reduces
-        chain = (tp.size == 1 or M <= ops.GEMV_CHAIN_MAX_M) and self._chain_ok(M)
+        dmax = ops.decode_chain_max_m()  # the GEMV (<= 4 rows) / weight-streaming MFMA (<= 64) forms
+        chain = (tp.size == 1 or M <= dmax) and self._chain_ok(M)
         ss = None  # norm chain: x is None and ss holds the residual's row partials
-        if chain and M <= ops.GEMV_CHAIN_MAX_M:
+        if chain and M <= dmax:
             # decode form: the QKV GEMV takes the embedding rows' factors itself (ss unused)
             x, ss = None, ops.ss_init(h, ops.ss_buffer(M, cfg.hidden_size, h.device))
         else:
@@ -225,7 +226,7 @@ class LlamaModel:
         return None, ss
 
     def _chain_layer_tp(self, i, a, residual, last, eps, ss):
-        """Tensor-parallel decode chain (M <= 4): the row-parallel O / down partial sums are
+        """Tensor-parallel decode chain (M <= decode_chain_max_m()): the row-parallel O / down partial sums are
         all-reduced AND added into the replicated residual in one launch (Group.all_reduce_add,
         K15), gate_up and the next QKV take their rows' RMSNorm factors from the residual chunks
         they stream (gemv.hip PRO_RS).  Two add + RMSNorm launches per layer fewer than

@@ -478,7 +478,16 @@ NORM_CHAIN = "1"
 # chunks they stream, so a layer has no add + RMSNorm launch.  False keeps the decode norms (the
 # GPU tests' A/B).
 GEMV_CHAIN = True
-GEMV_CHAIN_MAX_M = 4  # = gemv.hip gemv_chain_max_m
+GEMV_CHAIN_MAX_M = 4  # = gemv.hip gemv_chain_max_m (the GEMV form; the torch reference's decode form)
+
+
+def decode_chain_max_m() -> int:
+    """Rows the decode form of the norm chain takes: the GEMV up to 4 rows, then the
+    weight-streaming MFMA kernel (gemm_ws.hip) up to ``gemm_ws_max_m`` (64; the
+    ``gemm_ws_max_m`` op is its A/B switch).  Without the extension (CPU): the GEMV bound."""
+    if _loaded:
+        return int(torch.ops.mlop.decode_chain_max_m())
+    return GEMV_CHAIN_MAX_M
 
 
 def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
@@ -495,7 +504,7 @@ def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
     if device is not None and torch.device(device).type != "cuda":
         return False  # the torch reference path (CPU) has no chain kernels
     _need_gpu()
-    if M <= GEMV_CHAIN_MAX_M:
+    if M <= decode_chain_max_m():
         epis = epis or [EPI_NONE] * len(shapes)
         return GEMV_CHAIN and all(bool(torch.ops.mlop.gemv_chain_supported(M, N, K, e))
                                   for (N, K), e in zip(shapes, epis))

@@ -243,7 +243,6 @@ int64_t gemm_slab_nt(int64_t set) { return mlop::gemm_slab_nt((int)set); }
 int64_t gemm_rope_split(int64_t set) { return mlop::gemm_rope_split((int)set); }
 int64_t gemm_split_target(int64_t set) { return mlop::gemm_split_target((int)set); }
 int64_t gemm_grouped_narrow(int64_t set) { return mlop::gemm_grouped_narrow((int)set); }
-int64_t gemm_skip_dead(int64_t set) { return mlop::gemm_skip_dead((int)set); }
 int64_t moe_mid_max_tokens(int64_t set) { return mlop::moe_mid_max_tokens((int)set); }
 void gemm_dense_plan(int64_t variant, int64_t bm, int64_t bn, int64_t splits, int64_t stages) {
   mlop::gemm_dense_plan((int)variant, (int)bm, (int)bn, (int)splits, (int)stages);
@@ -342,12 +341,16 @@ bool gemm_res_ss(Tensor residual, Tensor a, Tensor w, Tensor ss_out) {
                   residual.stride(0) % 8 == 0, "residual [M, N]");
   TORCH_CHECK(N % 128 == 0, "N % 128");
   check_ss(ss_out, M, N, "ss");
-  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: the GEMV chain (gemv.hip EPI_RES); its consumers take their row
-                 // factors from the residual itself, so ss_out is not written
-    if (residual.stride(0) != N || !mlop::gemv_chain_takes((int)M, (int)N, (int)K, 0)) return false;
+  if (M <= mlop::decode_chain_max_m()) {  // decode sizes: the GEMV (M <= 4) / weight-streaming MFMA chain
+                 // (EPI_RES); its consumers take their row factors from the residual itself, so ss_out is not written
+    if (residual.stride(0) != N || !mlop::decode_chain_takes((int)M, (int)N, (int)K, 0)) return false;
     c10::DeviceGuard g(a.device());
-    mlop::launch_gemv_res(a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(), (int)M, (int)N,
-                          (int)K, cur_stream());
+    if (M <= mlop::gemv_chain_max_m())
+      mlop::launch_gemv_res(a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(), (int)M, (int)N,
+                            (int)K, cur_stream());
+    else
+      mlop::launch_ws(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, residual.data_ptr(), (int)N, (int)M,
+                      (int)N, (int)K, 5, false, mlop::RopeEpi{}, 0.f, cur_stream());
     return true;
   }
   mlop::RopeEpi re{};
@@ -371,11 +374,15 @@ bool gemm_rs(Tensor out, Tensor a, Tensor w, Tensor ss_in, double eps, int64_t e
                   out.stride(0) % 8 == 0, "out [M, N or N/2]");
   TORCH_CHECK(K % 128 == 0, "K % 128");
   check_ss(ss_in, M, K, "ss");
-  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: gemv.hip PRO_RS, row factors from the streamed chunks (ss_in unused)
-    if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi)) return false;
+  if (M <= mlop::decode_chain_max_m()) {  // decode sizes: PRO_RS, row factors from the streamed chunks (ss_in unused)
+    if (!mlop::decode_chain_takes((int)M, (int)N, (int)K, (int)epi)) return false;
     c10::DeviceGuard g(a.device());
-    mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
-                         (int)N, (int)K, (int)epi, mlop::RopeEpi{}, (float)eps, cur_stream());
+    if (M <= mlop::gemv_chain_max_m())
+      mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
+                           (int)N, (int)K, (int)epi, mlop::RopeEpi{}, (float)eps, cur_stream());
+    else
+      mlop::launch_ws(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, out.data_ptr(), (int)out.stride(0),
+                      (int)M, (int)N, (int)K, (int)epi, true, mlop::RopeEpi{}, (float)eps, cur_stream());
     return true;
   }
   mlop::RopeEpi re{};
@@ -409,11 +416,15 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
   mlop::RopeEpi re{(uint16_t*)q_out.data_ptr(), (uint16_t*)k_cache.data_ptr(),
                    (uint16_t*)v_cache.data_ptr(), pos.data_ptr<int>(), cos_sin.data_ptr<float>(),
                    slots.data_ptr<int>(), (int)Hq, (int)Hkv, (int)BS};
-  if (M <= mlop::gemv_chain_max_m()) {  // decode sizes: gemv.hip PRO_RS + the RoPE / paged K/V epilogue (ss_in unused)
-    if (!mlop::gemv_chain_takes((int)M, (int)N, (int)K, 3)) return false;
+  if (M <= mlop::decode_chain_max_m()) {  // decode sizes: PRO_RS + the RoPE / paged K/V epilogue (ss_in unused)
+    if (!mlop::decode_chain_takes((int)M, (int)N, (int)K, 3)) return false;
     c10::DeviceGuard g(a.device());
-    mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re,
-                         (float)eps, cur_stream());
+    if (M <= mlop::gemv_chain_max_m())
+      mlop::launch_gemv_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N, (int)K, 3, re,
+                           (float)eps, cur_stream());
+    else
+      mlop::launch_ws(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, nullptr, 0, (int)M, (int)N, (int)K, 3,
+                      true, re, (float)eps, cur_stream());
     return true;
   }
   if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
@@ -465,10 +476,14 @@ bool gemm_ws(Tensor out, Tensor a, Tensor w, int64_t epi, bool rs, double eps) {
 }
 
 int64_t gemm_ws_max_m(int64_t set) { return mlop::gemm_ws_max_m((int)set); }
+void gemm_ws_plan(int64_t rb, int64_t u, int64_t nt) { mlop::gemm_ws_plan((int)rb, (int)u, (int)nt); }
+int64_t gemm_ws_small_m(int64_t set) { return mlop::gemm_ws_small_m((int)set); }
 
 bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
-  return mlop::gemv_chain_takes((int)M, (int)N, (int)K, (int)epi);
+  return mlop::decode_chain_takes((int)M, (int)N, (int)K, (int)epi);
 }
+
+int64_t decode_chain_max_m() { return mlop::decode_chain_max_m(); }
 
 // grouped (MoE): rows of a sorted by group, offsets [G+1]; w [G, N, K]
 void grouped_gemm(Tensor out, Tensor a, Tensor w, Tensor offsets, int64_t max_rows, int64_t epi,
@@ -845,8 +860,10 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_rope_split(int set=-1) -> int", &gemm_rope_split);
   m.def("gemm_split_target(int set=-1) -> int", &gemm_split_target);
   m.def("gemm_grouped_narrow(int set=-1) -> int", &gemm_grouped_narrow);
-  m.def("gemm_skip_dead(int set=-1) -> int", &gemm_skip_dead);
   m.def("gemm_ws_max_m(int set=-1) -> int", &gemm_ws_max_m);
+  m.def("decode_chain_max_m() -> int", &decode_chain_max_m);
+  m.def("gemm_ws_plan(int rb, int u, int nt) -> ()", &gemm_ws_plan);
+  m.def("gemm_ws_small_m(int set=-1) -> int", &gemm_ws_small_m);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
   m.def("gemm_dense_plan(int variant, int bm, int bn, int splits, int stages=0) -> ()", &gemm_dense_plan);

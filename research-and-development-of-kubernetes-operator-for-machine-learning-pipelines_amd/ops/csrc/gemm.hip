@@ -531,7 +531,7 @@ struct SkArgs {
   int n_base;   // first stream-K block (grouped: the worst-case tile count of the grid)
   int cus;      // CUs the split was planned for
   int min_half; // shortest K-range (K-tiles) the planner may cut
-  int skip_dead;  // 1: quadrants past the last row issue no MFMAs; 2: also 16-row blocks (gemm_skip_dead)
+  int skip_dead;  // 1: quadrants past the last row issue no MFMAs (MLOP_GEMM_SKIP_DEAD=0: A/B)
 };
 
 // d for the r = T % cus tail tiles of a T-tile launch: each is cut into d equal K-ranges
@@ -709,14 +709,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
           __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? rsA : rsB, (lds_void_t*)dst, 16, voff[h][i], soff, 0, 0);
       }
     };
-    // 16-row blocks of this wave's quadrant holding rows (skip_dead == 2 only; 4 otherwise): a
-    // ragged quadrant (the 1-64 row spill m-tile of an MoE expert with 256 + a few rows)
-    // multiplies only those blocks
-    const int rows_tile = __builtin_amdgcn_readfirstlane(sk.skip_dead ? m_end - m0 : BM);
-    auto live_blocks = [&](int mi) {
-      const int r = rows_tile - (grp * 128 + mi * 64);
-      return sk.skip_dead == 2 ? (r <= 0 ? 0 : r >= 64 ? 4 : (r + 15) >> 4) : 4;
-    };
     auto read_a = [&](int buf, int mi, bf16x8 (&fa)[4][2]) {
       const uint16_t* sA = smem + buf * BUF;
 #pragma unroll
@@ -749,7 +741,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
     // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform): the
     // partner group's MFMAs then run alone on the SIMD.  Ragged M, and above all the last
     // m-tile of every expert in the grouped (MoE) GEMM, half empty on average.
-    const int rows_here = rows_tile;
+    const int rows_here = sk.skip_dead ? m_end - m0 : BM;
     // K-loop: two phases per K-tile, 32 MFMAs each.
     //   X(t): read A(mi 0) + B(nj 0, 1) of t | DMA A(mi 1) of t+1 -> buffer (t+1)&1
     //   Y(t): read A(mi 1) of t             | DMA A(mi 0) + B of t+2 -> buffer t&1
@@ -769,14 +761,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       __builtin_amdgcn_sched_barrier(0);
       // a 64-row quadrant wholly past the tile's last row issues no MFMAs (wave-uniform)
       if (grp * 128 + mi * 64 < rows_here) {
-        const int nb = live_blocks(mi);
         __builtin_amdgcn_s_setprio(1);
-        // a ragged quadrant multiplies only its live 16-row blocks (wave-uniform branches; one
-        // code path with every index static: a second, ragged copy of this block pushed the
-        // kernel past 256 VGPRs into scratch)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (i >= nb) continue;
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -784,7 +771,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
               acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
               acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
             }
-        }
         __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -955,13 +941,7 @@ struct SkBuf {
 static SkBuf g_sk[16];
 static int g_sk_mode = 1;
 static const int g_sk_min_iters = 16;
-// dead-row skipping of the ping-pong kernel: 1 = whole 64-row quadrants, 2 = also 16-row
-// blocks of a ragged quadrant (the MoE decode spill tile; gemm_skip_dead op for A/B)
-static int g_skip_dead = 2;
-int gemm_skip_dead(int set) {
-  if (set >= 0) g_skip_dead = set;
-  return g_skip_dead;
-}
+static const int g_skip_dead = 1;
 
 int gemm_sk_mode(int set) {
   if (set >= 0) g_sk_mode = set;
@@ -1397,6 +1377,10 @@ bool launch_gemm_rope(const void* A, int lda, const void* B, int M, int N, int K
     launch_gemv_rope(A, lda, B, M, N, K, re, st);
     return true;
   }
+  if (ws_prefer(M, N, K, EPI_ROPE) && lda % 8 == 0) {  // 5-16 rows: the weight-streaming MFMA kernel
+    launch_ws(A, lda, B, K, nullptr, 0, M, N, K, EPI_ROPE, false, re, 0.f, st);
+    return true;
+  }
   Plan p = rope_plan(M, N, K);
   if (!((p.BM == 256 || p.variant == 6) && p.BN >= 128)) {  // small M: split-K slabs + fused reduce / RoPE / cache
     float* ws = sk_buf()->ws;
@@ -1477,6 +1461,13 @@ bool launch_gemm_add_rmsnorm(const void* A, int lda, const void* B, void* out, v
                              int K, hipStream_t st) {
   if (M == 0) return true;
   if (gemv_takes(M, N, K, EPI_NONE)) return false;  // decode sizes: GEMV + add_rmsnorm (or the norm chain)
+  if (ws_prefer(M, N, K, EPI_NONE) && lda % 8 == 0) {
+    // 5-16 rows of an O-size projection: the weight-streaming MFMA kernel adds into the residual
+    // in place (bf16(res + bf16(y)), norm.hip's rounding), then one RMSNorm pass
+    launch_ws(A, lda, B, K, residual, N, M, N, K, 5, false, RopeEpi{}, 0.f, st);
+    launch_rmsnorm(out, residual, w, eps, M, N, st);
+    return true;
+  }
   int splits;
   const Plan p = plan(M, N, K, false, 0, 0);
   if (p.splits <= 1 || p.splits > kMaxSplits || (long)p.splits * M * N > ws_floats || N % 8) return false;

@@ -49,12 +49,12 @@ __device__ __forceinline__ float ws_sq8(const bf16x8& v, float c) {
   return ws_dot2(w.w, w.w, c);
 }
 
-template <int MT, int RB, int U, int EPI, bool RS>
+template <int MT, int RB, int U, int EPI, bool RS, bool NT = true>
 __global__ void __launch_bounds__(256) gemm_ws_kernel(const uint16_t* __restrict__ A, int lda,
                                                       const uint16_t* __restrict__ B, int ldb,
                                                       uint16_t* __restrict__ C, int ldc, int M, int K,
                                                       RopeEpi re, float eps) {
-  static_assert(EPI != WS_SILU_MUL || RB == 2, "gate / up row blocks");
+  static_assert(EPI != WS_SILU_MUL || RB % 2 == 0, "gate / up row block pairs");
   static_assert(EPI != WS_ROPE || RB == 2, "rotate-half row blocks");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int blk = blockIdx.x;
@@ -62,9 +62,12 @@ __global__ void __launch_bounds__(256) gemm_ws_kernel(const uint16_t* __restrict
   // first weight row of each of this workgroup's RB 16-row blocks
   int rbase[RB];
   bool rope_blk = false;
-  if constexpr (EPI == WS_SILU_MUL) {
-    rbase[0] = 32 * blk;
-    rbase[1] = 32 * blk + 16;
+  if constexpr (EPI == WS_SILU_MUL) {  // RB / 2 (gate, up) 16-row group pairs
+#pragma unroll
+    for (int g = 0; g < RB / 2; ++g) {
+      rbase[2 * g] = 32 * (blk * (RB / 2) + g);
+      rbase[2 * g + 1] = rbase[2 * g] + 16;
+    }
   } else if constexpr (EPI == WS_ROPE) {
     const int rope_blocks = (re.Hq + re.Hkv) * 4;  // 4 blocks of 16 dim pairs per q / k head
     rope_blk = blk < rope_blocks;
@@ -104,7 +107,10 @@ __global__ void __launch_bounds__(256) gemm_ws_kernel(const uint16_t* __restrict
   bf16x8 bq[U][RB], aq[U][MT];
   auto load = [&](int u, int s) {
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) bq[u][rb] = __builtin_nontemporal_load(bp[rb] + 4 * s);
+    for (int rb = 0; rb < RB; ++rb) {
+      if constexpr (NT) bq[u][rb] = __builtin_nontemporal_load(bp[rb] + 4 * s);
+      else bq[u][rb] = bp[rb][4 * s];
+    }
 #pragma unroll
     for (int t = 0; t < MT; ++t) aq[u][t] = ap[t][4 * s];
   };
@@ -173,7 +179,9 @@ __global__ void __launch_bounds__(256) gemm_ws_kernel(const uint16_t* __restrict
       for (int rb = 0; rb < RB; ++rb) y[rb] *= inv;
     }
     if constexpr (EPI == WS_SILU_MUL) {
-      C[(size_t)m * ldc + blk * 16 + col] = f2bf(silu_bf(y[0]) * bf2f(f2bf(y[1])));
+#pragma unroll
+      for (int g = 0; g < RB / 2; ++g)
+        C[(size_t)m * ldc + (blk * (RB / 2) + g) * 16 + col] = f2bf(silu_bf(y[2 * g]) * bf2f(f2bf(y[2 * g + 1])));
     } else if constexpr (EPI == WS_ROPE) {
       const int slot = re.slots[m];
       const int pblk = slot >= 0 ? slot / re.BS : 0, poff = slot >= 0 ? slot % re.BS : 0;
@@ -212,16 +220,37 @@ __global__ void __launch_bounds__(256) gemm_ws_kernel(const uint16_t* __restrict
   }
 }
 
-int g_ws_max_m = 64;  // rows the weight-streaming kernel takes from (gemv_max_m, ws_max_m]; 0 = off
+// rows the weight-streaming kernel takes, (gemv_chain_max_m, g_ws_max_m]: 0 = off (default, the
+// decode chain stays at the GEMV's 4 rows).  Measured slower than the planner's LDS-ring small
+// tiles on gate_up / down at every M and on all shapes at M >= 32 (profiles/r06_small_m_ws.md);
+// the gemm_ws_max_m op turns it on for A/B runs
+int g_ws_max_m = 0;
+
+// A/B plan of the sweep (gemm_ws_plan op, scripts/bench_ws.py): row blocks per workgroup (plain: 1 / 2 /
+// 4, SiLU-mul: 2 / 4; 0 = default 1 / 2), K-steps in flight (4 / 8; 0 = 8 where K allows) and
+// non-temporal (1) or cached (0, default: 64 B per row per load, the two halves of a line on
+// consecutive loads, which the cached path merges in L2 -- 1.3-1.9x faster than nt at o / qkv)
+// weight loads.  The RoPE / residual / row-scale forms keep the defaults.
+int g_ws_rb = 0, g_ws_u = 0, g_ws_nt = 0;
+
+template <int MT, int RB, int EPI, bool RS, int U, bool NT>
+void launch_ws_k(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N, int K,
+                 const RopeEpi& re, float eps, hipStream_t st) {
+  gemm_ws_kernel<MT, RB, U, EPI, RS, NT><<<N / (16 * RB), 256, 0, st>>>(A, lda, B, ldb, C, ldc, M, K, re, eps);
+}
 
 template <int MT, int RB, int EPI, bool RS>
 void run_ws_mt(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint16_t* C, int ldc, int M, int N, int K,
                const RopeEpi& re, float eps, hipStream_t st) {
-  const int blocks = N / (16 * RB);
-  if ((K >> 2) % (32 * 8) == 0)
-    gemm_ws_kernel<MT, RB, 8, EPI, RS><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, M, K, re, eps);
-  else
-    gemm_ws_kernel<MT, RB, 4, EPI, RS><<<blocks, 256, 0, st>>>(A, lda, B, ldb, C, ldc, M, K, re, eps);
+  const bool u8 = (K >> 2) % (32 * 8) == 0 && g_ws_u != 4;
+  constexpr bool SWEEP = !RS && (EPI == WS_NONE || EPI == WS_SILU_MUL);
+  if (SWEEP && g_ws_nt) {
+    if (u8) launch_ws_k<MT, RB, EPI, RS, 8, true>(A, lda, B, ldb, C, ldc, M, N, K, re, eps, st);
+    else launch_ws_k<MT, RB, EPI, RS, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, re, eps, st);
+    return;
+  }
+  if (u8) launch_ws_k<MT, RB, EPI, RS, 8, false>(A, lda, B, ldb, C, ldc, M, N, K, re, eps, st);
+  else launch_ws_k<MT, RB, EPI, RS, 4, false>(A, lda, B, ldb, C, ldc, M, N, K, re, eps, st);
 }
 
 template <int RB, int EPI, bool RS>
@@ -242,6 +271,32 @@ int gemm_ws_max_m(int set) {
   return g_ws_max_m;
 }
 
+// Outside the chain, the plain decode projections take this kernel where it measured faster
+// than the planner's small tiles (profiles/r06_small_m_ws.md): the O-size (33 MB) and QKV-size
+// (50 MB) matrices at 5-8 rows.  Cold-weight microbench: o 8.4 vs 15.9 us, qkv 12.4 vs 17.8 (the
+// QKV form also does RoPE + the paged K/V stores, so the rope_cache slab reduce launch goes);
+// in the model the planner's O runs nearer 9 us, so end to end batch 8 gains 1.7 % and batch
+// 16 is within noise (-1 %): 8 rows.  gate_up / down and 32+ rows stay on the planner.  The
+// gemm_ws_small_m op (0 = off) is the A/B switch.
+int g_ws_small_m = 8;
+
+int gemm_ws_small_m(int set) {
+  if (set >= 0) g_ws_small_m = set > 64 ? 64 : set;
+  return g_ws_small_m;
+}
+
+bool ws_prefer(int M, int N, int K, int epi) {
+  if (M <= gemv_chain_max_m() || M > g_ws_small_m || (long)N * K > 32L * 1024 * 1024 || K % 512) return false;
+  if (epi == WS_ROPE) return N % 128 == 0;
+  return (epi == WS_NONE || epi == WS_RES) && N % 16 == 0;
+}
+
+void gemm_ws_plan(int rb, int u, int nt) {
+  g_ws_rb = rb == 1 || rb == 2 || rb == 4 ? rb : 0;
+  g_ws_u = u == 4 || u == 8 ? u : 0;
+  g_ws_nt = nt != 0;
+}
+
 // Shapes this path takes: gemv_max_m() < M <= ws max (default 64), K a multiple of 512 (four K
 // quarters of whole 4-step rings), 16-B aligned rows, whole 16-row blocks (plain / residual),
 // whole 32-row gate / up groups (SiLU-mul), a QKV projection of 128-wide heads (RoPE).
@@ -252,6 +307,12 @@ bool ws_takes(int M, int N, int K, int epi) {
   return (epi == WS_NONE || epi == WS_RES) && N % 16 == 0;
 }
 
+int decode_chain_max_m() { return g_ws_max_m > gemv_chain_max_m() ? g_ws_max_m : gemv_chain_max_m(); }
+
+bool decode_chain_takes(int M, int N, int K, int epi) {
+  return M <= gemv_chain_max_m() ? gemv_chain_takes(M, N, K, epi) : ws_takes(M, N, K, epi);
+}
+
 void launch_ws(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int epi,
                bool rs, const RopeEpi& re, float eps, hipStream_t st) {
   auto* a = (const uint16_t*)A;
@@ -259,6 +320,7 @@ void launch_ws(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
   auto* c = (uint16_t*)C;
   if (epi == WS_SILU_MUL) {
     if (rs) run_ws<2, WS_SILU_MUL, true>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
+    else if (g_ws_rb == 4 && N % 64 == 0) run_ws<4, WS_SILU_MUL, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
     else run_ws<2, WS_SILU_MUL, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
   } else if (epi == WS_ROPE) {
     if (rs) run_ws<2, WS_ROPE, true>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
@@ -267,6 +329,8 @@ void launch_ws(const void* A, int lda, const void* B, int ldb, void* C, int ldc,
     run_ws<1, WS_RES, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
   } else {
     if (rs) run_ws<1, WS_NONE, true>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
+    else if (g_ws_rb == 4 && N % 64 == 0) run_ws<4, WS_NONE, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
+    else if (g_ws_rb == 2 && N % 32 == 0) run_ws<2, WS_NONE, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
     else run_ws<1, WS_NONE, false>(a, lda, b, ldb, c, ldc, M, N, K, re, eps, st);
   }
 }

@@ -74,7 +74,6 @@ long gemm_workspace_floats(int M, int N, int K, int epi);
 int gemm_big_variant(int set);
 int gemm_half_tile(int set);
 int gemm_grouped_narrow(int set);
-int gemm_skip_dead(int set);
 void gemm_grouped_plan(int bm, int bn, int stages, int splits);
 void gemm_dense_plan(int variant, int bm, int bn, int splits, int stages = 0);
 // variant 5: the four-wave hand-scheduled 256x256 kernel (gemm_w4.hip), variant 6 its 128x256
@@ -124,6 +123,14 @@ bool gemv_chain_takes(int M, int N, int K, int epi);
 // residual, rows scaled by rsqrt(mean(a^2) + eps) (norm weights folded into B)
 bool ws_takes(int M, int N, int K, int epi);
 int gemm_ws_max_m(int set);
+void gemm_ws_plan(int rb, int u, int nt);
+int gemm_ws_small_m(int set);
+// the plain (non-chain) decode projections this kernel takes instead of the planner
+bool ws_prefer(int M, int N, int K, int epi);
+// the decode norm chain's forms: the GEMV up to gemv_chain_max_m() rows, then the weight-
+// streaming MFMA kernel up to gemm_ws_max_m()
+int decode_chain_max_m();
+bool decode_chain_takes(int M, int N, int K, int epi);
 void launch_ws(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int epi,
                bool rs, const RopeEpi& re, float eps, hipStream_t st);
 int gemv_chain_max_m();

@@ -169,9 +169,14 @@ def make_parallel_state(tp_size: int = 1, ep_size: int = 1, custom_ar: bool = Tr
         # rank before it carries a single real message; otherwise the whole group stays on the
         # process-group collectives (custom_ar.py self_check / agree)
         inj = os.environ.get("MLOP_INJECT_CAR_CORRUPT", "")
-        verdict = car.self_check(inject_rank=int(inj) if inj.strip() else None)
+        # every rank mapped every peer (else nobody launches a kernel a peer cannot answer)
+        if car.agree({"ok": car.init_error is None}):
+            verdict = car.self_check(inject_rank=int(inj) if inj.strip() else None)
+        else:
+            verdict = {"ok": False, "checks": {}, "error_word": -1,
+                       "exception": car.init_error or "a peer could not map the IPC buffers"}
         tp.car_check = verdict
-        if car.agree(verdict):
+        if car.agree(verdict):  # collective: every rank calls it exactly once
             tp.car, tp.car_status = car, "ok"
         else:
             import sys

@@ -45,15 +45,30 @@ class CustomAllReduce:
         self.device = torch.device(device)
         self.max_bytes = int(max_bytes)
         self.split_data = SPLIT_DATA if split_data is None else bool(split_data)
-        self.h = torch.ops.mlop.car_create(rank, world, self.max_bytes, self.device.index or 0, self.split_data)
-        mine = torch.ops.mlop.car_ipc_handle(self.h)
+        # First contact never raises half-way: a rank whose buffer or peer mapping fails records
+        # it (init_error) and still takes part in every collective below, so the group reaches
+        # the self-check agreement together (a raise here would leave the peers blocked in the
+        # handle exchange or the barrier)
+        self.h, self.init_error = 0, None
+        mine = None
+        try:
+            self.h = torch.ops.mlop.car_create(rank, world, self.max_bytes, self.device.index or 0, self.split_data)
+            mine = bytes(torch.ops.mlop.car_ipc_handle(self.h).numpy().tobytes())
+        except Exception as e:  # noqa: BLE001 - agreed on in make_parallel_state
+            self.init_error = f"create: {type(e).__name__}: {e}"
         if world > 1:
             allh = [None] * world
-            dist.all_gather_object(allh, bytes(mine.numpy().tobytes()), group=group)
+            dist.all_gather_object(allh, mine, group=group)
         else:
-            allh = [bytes(mine.numpy().tobytes())]
-        table = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(world, 128).clone()
-        torch.ops.mlop.car_open(self.h, table)
+            allh = [mine]
+        if self.init_error is None and any(h is None for h in allh):
+            self.init_error = "a peer could not create its buffer"
+        if self.init_error is None:
+            try:
+                table = torch.frombuffer(bytearray(b"".join(allh)), dtype=torch.uint8).view(world, 128).clone()
+                torch.ops.mlop.car_open(self.h, table)
+            except Exception as e:  # noqa: BLE001
+                self.init_error = f"open: {type(e).__name__}: {e}"
         if world > 1:
             dist.barrier(group=group)
 
@@ -122,8 +137,10 @@ class CustomAllReduce:
 
     def close(self):
         if self.h:
-            torch.ops.mlop.car_destroy(self.h)
-            self.h = 0
+            try:
+                torch.ops.mlop.car_destroy(self.h)
+            finally:
+                self.h = 0
 
     # ------------------------------------------------------------ first contact --
     def self_check(self, hidden: int = 4096, inject_rank: int | None = None) -> dict:
@@ -158,6 +175,8 @@ class CustomAllReduce:
             return acc
 
         res = {"ok": True, "checks": {}}
+        if self.init_error is not None:  # nothing to test: this rank never mapped its peers
+            return {"ok": False, "checks": {}, "exception": self.init_error, "error_word": -1}
         try:
             for salt, (name, n) in enumerate(rows.items()):
                 xs = inputs(n, salt)

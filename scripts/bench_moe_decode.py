@@ -61,13 +61,8 @@ def main():
     ap.add_argument("--counts", default="",
                     help="explicit per-expert row counts instead of --rows, ';'-separated sets of 8 "
                          "comma-separated counts (e.g. '256,256,256,256,256,256,256,256;257,...')")
-    ap.add_argument("--skip-dead", default="",
-                    help="comma list of ping-pong dead-row modes to interleave (gemm_skip_dead: 1 = 64-row "
-                         "quadrants, 2 = also 16-row blocks); empty = the default only")
     a = ap.parse_args()
     ops.load()
-    sds = [int(v) for v in a.skip_dead.split(",") if v] or [None]
-    sd0 = torch.ops.mlop.gemm_skip_dead(-1)
     dev = torch.device("cuda")
     bf = torch.bfloat16
     ops._sk_reserve(dev)
@@ -86,9 +81,7 @@ def main():
             ref = None
             best = {}
             for _ in range(2):  # interleaved rounds
-                for (label0, bm, bn, st, sp), sd in [(c, sd) for c in CANDIDATES[group] for sd in sds]:
-                    label = label0 if sd is None else f"{label0}/sd{sd}"
-                    torch.ops.mlop.gemm_skip_dead(sd0 if sd is None else sd)
+                for label, bm, bn, st, sp in CANDIDATES[group]:
                     torch.ops.mlop.gemm_grouped_plan(bm, bn, st, sp)
                     try:
                         y = ops.grouped_gemm(x, w, off, epi=epi, avg_rows=rows // E)
@@ -102,7 +95,6 @@ def main():
                     if label not in best or (best[label][0] is not None and t < best[label][0]):
                         best[label] = (t, err)
             torch.ops.mlop.gemm_grouped_plan(-1, -1, -1, -1)
-            torch.ops.mlop.gemm_skip_dead(sd0)
             wbytes = int((counts > 0).sum()) * N * K * 2
             for label, (t, err) in best.items():
                 if t is None:

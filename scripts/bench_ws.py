@@ -53,6 +53,7 @@ def main():
     ops.load()
     dev = torch.device("cuda")
     ops._sk_reserve(dev)
+    torch.ops.mlop.gemm_ws_max_m(64)  # off by default in serving
     bf = torch.bfloat16
     for M in [int(m) for m in a.ms.split(",")]:
         for name in a.shapes.split(","):
@@ -77,15 +78,25 @@ def main():
                 if silu:
                     exp = ref_silu_mul(exp)
                 err = float((out.float() - exp).abs().max() / exp.abs().max())
-            runs = {"planner": lambda: ops.gemm(x, nxt(), epi=epi)}
+            runs = {"planner": (None, lambda: ops.gemm(x, nxt(), epi=epi))}
             if ok:
-                runs["ws"] = lambda: torch.ops.mlop.gemm_ws(out, x, nxt(), epi, False, 0.0)
+                for rb in ((2, 4) if silu else (1, 2, 4)):
+                    for u in (4, 8):
+                        for nt in (0, 1):
+                            runs[f"ws_rb{rb}_u{u}_nt{nt}"] = (
+                                (rb, u, nt), lambda: torch.ops.mlop.gemm_ws(out, x, nxt(), epi, False, 0.0))
             res = {}
             for _ in range(a.rounds):
-                for k, fn in runs.items():
+                for k, (plan, fn) in runs.items():
+                    if plan is not None:
+                        torch.ops.mlop.gemm_ws_plan(*plan)
                     res[k] = min(res.get(k, 1e9), timeit(fn, a.iters))
+            torch.ops.mlop.gemm_ws_plan(0, 0, 1)
+            best = min((k for k in res if k != "planner"), key=res.get, default=None)
+            if best:
+                res = {"planner": res["planner"], "ws_best": res[best], **res}
             wbytes = N * K * 2
-            print(json.dumps(dict(shape=name, M=M, ws_taken=ok, rel_err=err,
+            print(json.dumps(dict(shape=name, M=M, ws_taken=ok, rel_err=err, ws_best_plan=best if ok else None,
                                   **{f"{k}_us": round(v, 2) for k, v in res.items()},
                                   **{f"{k}_tbs": round(wbytes / v / 1e6, 2) for k, v in res.items()})), flush=True)
             del x, ws

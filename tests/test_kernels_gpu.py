@@ -992,3 +992,38 @@ def test_attention_kv_policy_bit_identical(gpu, case):
     assert torch.equal(a, b)
     close(b, ref.paged_attention(q, kc, vc, m))
 
+
+
+@pytest.fixture
+def ws_on():
+    """The weight-streaming MFMA kernel is off in serving (gemm_ws_max_m = 0): on for the test."""
+    prev = torch.ops.mlop.gemm_ws_max_m(-1)
+    torch.ops.mlop.gemm_ws_max_m(64)
+    yield
+    torch.ops.mlop.gemm_ws_max_m(prev)
+    torch.ops.mlop.gemm_ws_plan(0, 0, 1)
+
+
+@pytest.mark.parametrize("plan", [(0, 0, 1), (4, 4, 0), (2, 8, 1)], ids=["default", "rb4u4c", "rb2u8nt"])
+@pytest.mark.parametrize("M", [5, 16, 17, 33, 64])
+@pytest.mark.parametrize("N,K,epi", [(1024, 4096, 0), (2048, 4096, 1), (512, 14336, 0), (4096, 1024, 0)])
+def test_gemm_ws_vs_fp32(gpu, ws_on, plan, M, N, K, epi):
+    """K2 at 5-64 rows, the weight-streaming MFMA kernel (gemm_ws.hip): plain and SiLU-mul
+    (16-interleaved gate / up rows) against the fp32 product; rows past M are never written."""
+    from mlopamd import ops
+
+    torch.manual_seed(M * 7 + N)
+    torch.ops.mlop.gemm_ws_plan(*plan)
+    a = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    w = (0.02 * torch.randn(N, K, device=gpu)).to(torch.bfloat16)
+    out = torch.full((M + 3, N // 2 if epi else N), 7.0, device=gpu, dtype=torch.bfloat16)
+    assert torch.ops.mlop.gemm_ws(out[:M], a, w, epi, False, 0.0)
+    exp = a.float() @ w.float().t()
+    if epi:
+        exp = ops.reference.silu_mul(ops.deinterleave_cols(exp.to(torch.bfloat16))).float()
+    torch.testing.assert_close(out[:M].float(), exp, atol=2e-2 * exp.abs().max().item() / 4 + 1e-2, rtol=2e-2)
+    assert bool((out[M:] == 7.0).all())
+    # deterministic relaunch
+    out2 = torch.empty_like(out[:M])
+    torch.ops.mlop.gemm_ws(out2, a, w, epi, False, 0.0)
+    assert torch.equal(out2, out[:M])

@@ -15,6 +15,16 @@ bf = torch.bfloat16
 H, I, EPS = 4096, 14336, 1e-5
 
 
+@pytest.fixture
+def ws_on():
+    """The decode chain's weight-streaming MFMA form (5-64 rows) is off in serving
+    (gemm_ws_max_m = 0): on for these tests."""
+    prev = torch.ops.mlop.gemm_ws_max_m(-1)
+    torch.ops.mlop.gemm_ws_max_m(64)
+    yield
+    torch.ops.mlop.gemm_ws_max_m(prev)
+
+
 def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
@@ -136,12 +146,13 @@ def test_llama_forward_chain_on_off(gpu, w4, monkeypatch):
                 toks.append(t)
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4])
-def test_gemv_chain_res_rs(gpu, w4, M):
-    """Decode form of the chain (gemv.hip EPI_RES / PRO_RS, M <= 4): O / down add into the
-    residual in place with norm.hip's rounding, gate_up / plain / QKV + RoPE scale each row by
-    rsqrt(mean(a^2) + eps) of the residual chunks they stream.  The ss buffers are NaN: the
-    GEMV form must neither read nor need them (the four-wave form would turn them into NaNs)."""
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8, 16, 17, 33, 48, 64])
+def test_gemv_chain_res_rs(gpu, w4, ws_on, M):
+    """Decode form of the chain (M <= 4: gemv.hip EPI_RES / PRO_RS; 5-64 rows: the
+    weight-streaming MFMA kernel, gemm_ws.hip WS_RES / RS): O / down add into the residual in
+    place with norm.hip's rounding, gate_up / plain / QKV + RoPE scale each row by
+    rsqrt(mean(a^2) + eps) of the residual they stream.  The ss buffers are NaN: the decode
+    form must neither read nor need them (the four-wave form would turn them into NaNs)."""
     from mlopamd.models.layers import rope_table
 
     torch.manual_seed(M)
@@ -185,11 +196,12 @@ def test_gemv_chain_res_rs(gpu, w4, M):
     close(vc, vr)
 
 
-@pytest.mark.parametrize("batch", [1, 3, 4])
-def test_llama_decode_gemv_chain_on_off(gpu, w4, monkeypatch, batch):
+@pytest.mark.parametrize("batch", [1, 3, 4, 8, 24])
+def test_llama_decode_gemv_chain_on_off(gpu, w4, ws_on, monkeypatch, batch):
     """2-layer Llama-3-8B-wide engine, graphs on: decode steps of 1 / 3 / 4 sequences with the
-    GEMV chain (five launches per layer, no add + RMSNorm; batch 3 replays the 4-row graph with
-    a padding row) and without it both follow the fp32 dense oracle."""
+    GEMV chain, of 8 / 24 with the weight-streaming MFMA chain (five launches per layer, no add
+    + RMSNorm; batch 3 / 24 replay the 4- / 32-row graphs with padding rows) and without the
+    chain all follow the fp32 dense oracle."""
     from mlopamd.models import build_model
     from mlopamd.models.config import get_config
     from mlopamd.models.reference import dense_logits
@@ -207,7 +219,7 @@ def test_llama_decode_gemv_chain_on_off(gpu, w4, monkeypatch, batch):
         eng = Engine(model, EngineConfig(max_num_seqs=batch, max_num_batched_tokens=512, max_model_len=128,
                                          num_kv_blocks=batch * 8 + 1, use_graphs=True))
         outs[on] = eng.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
-        small = set(k[3] for k in ops._GEMM_USED if k[0] <= 4)
+        small = set(k[3] for k in ops._GEMM_USED if k[0] <= 64)
         assert (ops.EPI_ADD_SS in small) == on, small
     for on in (False, True):
         for p, o in zip(prompts, outs[on]):
