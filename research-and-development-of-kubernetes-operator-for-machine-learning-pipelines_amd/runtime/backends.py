@@ -93,7 +93,6 @@ class LLMBackend:
         return self._thread.is_alive()
 
     def start(self):
-        self.ktime.warm(background=True)  # the tracer's one-time start-up, off the engine thread
         self._thread.start()
         return self
 

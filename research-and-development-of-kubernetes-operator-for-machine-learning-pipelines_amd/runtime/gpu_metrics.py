@@ -169,9 +169,10 @@ class KernelTimeSampler:
     The engine thread only opens and stops the window; the event reduction (``key_averages``,
     the bulk of a window's host cost) runs on a helper thread (``MLOP_KERNEL_SAMPLE_ASYNC``,
     default on), and the first window opens one period after serving starts, never on the
-    first step.  The tracer's one-time start-up (~2 s measured) is paid by ``warm``, on a
-    background thread at predictor start-up (``warm(background=True)``) so neither readiness
-    nor the first window waits for it (profiles/r06_sampler.md)."""
+    first step.  The tracer's one-time start-up (~2 s measured) is paid by ``warm`` on a
+    background thread when the first window falls due; the window opens once it finished, so
+    neither readiness, the first served requests nor a window's step waits for it
+    (profiles/r06_sampler.md)."""
 
     def __init__(self, period_s: float | None = None, on_shares=None, async_reduce: bool | None = None):
         self.period_s = float(os.environ.get("MLOP_KERNEL_SAMPLE_S", 30.0) if period_s is None else period_s)
@@ -238,6 +239,14 @@ class KernelTimeSampler:
             return
         if now < self._next:
             return
+        if self.warm_ms is None:
+            # first due window: start the tracer's one-time start-up on its own thread now (not at
+            # predictor start, where its ~2 s of GIL-holding work slowed the first served requests
+            # -- a fresh canary's -- ~10x: profiles/r06_sampler.md), open the window once it is done
+            if self._warm_thread is None:
+                self.warm(background=True)
+            if self._warm_thread is not None and self._warm_thread.is_alive():
+                return
         if self._warm_thread is not None and self._warm_thread.is_alive():
             return  # the tracer is still starting on its own thread
         if self._reducer is not None and self._reducer.is_alive():

@@ -1,4 +1,4 @@
-"""Norm-chain kernels in isolation (M = 4088, Llama-3-8B gate_up / QKV / O shapes): plain
+"""Norm-chain kernels in isolation (M = 4088, Llama-3-8B gate_up / O / down shapes): plain
 four-wave SiLU-mul on a normalised x vs the row-scaled (W4_RS) variant on the raw residual,
 and each kernel on both inputs (is a slowdown the variant's code or the operand data?)."""
 import os
@@ -39,6 +39,8 @@ def t(fn, n=20):
 
 
 r2 = res.clone()
+wd = (0.02 * torch.randn(H, I, device=dev)).to(torch.bfloat16)
+act = torch.randn(M, I, device=dev).to(torch.bfloat16)
 cases = {
     "gate_up silu   (x)": lambda: ops.gemm(x, wgu, epi=ops.EPI_SILU_MUL),
     "gate_up silu   (res)": lambda: ops.gemm(res, wgu, epi=ops.EPI_SILU_MUL),
@@ -47,6 +49,12 @@ cases = {
     "o plain        (a)": lambda: ops.gemm(a, wo),
     "o add_ss       (a)": lambda: ops.gemm_res_ss(a, wo, r2, ss_out),
     "o + add_rmsnorm(a)": lambda: ops.add_rmsnorm(ops.gemm(a, wo), r2, torch.ones(H, device=dev, dtype=torch.bfloat16), 1e-5),
+    "down plain     (act)": lambda: ops.gemm(act, wd),
+    "down add_ss    (act)": lambda: ops.gemm_res_ss(act, wd, r2, ss_out),
 }
 for rnd in range(3):
     print("round", rnd, "  ".join(f"{k}: {t(f):7.1f}" for k, f in cases.items()), flush=True)
+flops = {"gate_up": 2 * M * 2 * I * H, "o": 2 * M * H * H, "down": 2 * M * H * I}
+for k, f in cases.items():
+    us = min(t(f) for _ in range(2))
+    print(f"{k:22s} {us:8.1f} us  {flops[k.split()[0]] / us / 1e9:7.1f} TF/s", flush=True)
