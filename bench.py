@@ -110,8 +110,9 @@ def parse(argv=None):
     ap.add_argument("--tp-steps", type=int, default=10, help="timed engine steps of the TP phase")
     ap.add_argument("--tp-warmup", type=int, default=3)
     ap.add_argument("--tp-timeout", type=float, default=240.0,
-                    help="watchdog of the TP phase (seconds): past it rank 0 prints the line with "
-                         "tp.error and every rank exits, so a first-contact hang cannot eat the DP result")
+                    help="time limit of the TP phase (seconds): its child processes are stopped past it and the "
+                         "line carries tp.error, so a first-contact hang cannot eat the DP result")
+    ap.add_argument("--tp-phase-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cr-ready-samples", type=int, default=3,
                     help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
                          "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
@@ -236,6 +237,8 @@ def main(argv=None):
     a = parse(argv)
     if a.http:
         return http_main(a)
+    if a.tp_phase_child:
+        return _tp_child_main(a)
     from mlopamd.parallel.comm import env_rank_info, init_distributed
     import torch.distributed as dist
 
@@ -324,16 +327,110 @@ def main(argv=None):
     if a.tp == 1:
         engine.shutdown()
     if _tp_phase_on(a, world):
-        # the driver's N-GPU command is DP replicas; on the same ranks, a short TP = N phase then
+        # the driver's N-GPU command is DP replicas; on the same GPUs, a short TP = N phase then
         # carries Llama-3 over RCCL + the K15 IPC all-reduce across the N devices (xGMI), with
-        # its own first-contact checks (runtime/bench_tp.py), reported as the line's "tp" block
+        # its own first-contact checks (runtime/bench_tp.py), reported as the line's "tp" block.
+        # It runs in CHILD processes (one per rank, their own process group): a first-contact
+        # failure there -- a hang, an abort, a GPU fault -- ends the child, never this process,
+        # which holds the DP result and prints the line either way
         del engine
-        from mlopamd.runtime.bench_tp import tp_phase
-
-        tp = tp_phase(a, rank, world, dev, serve_closed_loop, res, _emit)
+        tp = _tp_phase_children(a, argv, rank, world, dev)
         if res is not None:
             res["tp"] = tp
     _emit(res)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _tp_phase_children(a, argv, rank: int, world: int, dev) -> dict | None:
+    """Run ``runtime/bench_tp.tp_phase`` in one child process per rank (``--tp-phase-child``),
+    on a fresh rendezvous port, and collect rank 0's ``tp`` block from the file its child
+    writes.  Every parent waits at most ``--tp-timeout`` + 60 s for its child (killed past it),
+    then the parents meet at a barrier; a child that died leaves ``tp.error``."""
+    import gc
+    import socket
+    import subprocess
+    import tempfile
+
+    import torch.distributed as dist
+
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+    box = [None, None]
+    if rank == 0:
+        with socket.socket() as s_:
+            s_.bind(("127.0.0.1", 0))
+            box[0] = s_.getsockname()[1]
+        fd, box[1] = tempfile.mkstemp(prefix="mlop-tp-phase-", suffix=".json")
+        os.close(fd)
+    if world > 1:
+        dist.broadcast_object_list(box, src=0)
+    port, out_path = box
+    # the child is its own job: its own rendezvous (no torchrun agent store), same rank layout
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+               LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)), MLOP_TP_PHASE_OUT=out_path,
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--tp-phase-child"]
+    t0 = time.perf_counter()
+    _progress(rank, f"TP = {world} phase in a child process (port {port})")
+    p = subprocess.Popen(cmd, env=env)
+    try:
+        rc = p.wait(timeout=a.tp_timeout + 60)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        rc = p.wait()
+        _progress(rank, "TP phase child killed at its time limit")
+    if world > 1:
+        dist.barrier()  # every child is gone before the parents go on
+    if rank != 0:
+        return None
+    tp = None
+    try:
+        with open(out_path) as f:
+            txt = f.read().strip()
+        tp = json.loads(txt) if txt else None
+    except (OSError, ValueError):
+        tp = None
+    finally:
+        try:
+            os.unlink(out_path)
+        except OSError:
+            pass
+    if tp is None:
+        tp = {"tp": world, "error": f"TP phase child exited with {rc} and no result"}
+    tp["child_rc"] = rc
+    tp["child_wall_s"] = round(time.perf_counter() - t0, 2)
+    return tp
+
+
+def _tp_child_main(a) -> None:
+    """``--tp-phase-child``: one rank of the TP phase (spawned by ``_tp_phase_children``); rank
+    0 writes the ``tp`` block, or the error that ended the phase, to $MLOP_TP_PHASE_OUT."""
+    from mlopamd.parallel.comm import env_rank_info, init_distributed
+    from mlopamd.runtime.bench_tp import tp_phase
+    import torch.distributed as dist
+
+    rank, local_rank, world = env_rank_info()
+    out_path = os.environ.get("MLOP_TP_PHASE_OUT", "")
+
+    def write(block):
+        if rank == 0 and out_path:
+            with open(out_path, "w") as f:
+                f.write(json.dumps(block))
+
+    if a.share_gpu:
+        os.environ.setdefault("MLOP_CUSTOM_AR", "force")  # K15 over the gloo group (same-GPU IPC)
+    if world > 1:
+        init_distributed(backend="gloo" if a.share_gpu else None)
+    dev = torch.device("cuda", 0 if a.share_gpu else local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    tp = tp_phase(a, rank, world, dev, serve_closed_loop, lambda msg: write({"tp": world, "error": msg}))
+    write(tp)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -22,9 +22,10 @@ TP = N phase of the same model, reported as the JSON line's ``tp`` block:
   4. a closed-loop serve of ``--tp-batch`` requests, ``--tp-warmup`` + ``--tp-steps`` engine
      steps timed between device syncs + world barriers -> ``tokens_per_sec``.
 
-A watchdog bounds the phase (``--tp-timeout``): a first-contact hang on real peers must not
-cost the DP result, so past the deadline rank 0 prints the line with ``tp.error`` and every
-rank exits.
+bench.py runs the phase in child processes (``--tp-phase-child``), one per rank with its own
+process group, so a first-contact failure on real peers -- a hang, an abort, a GPU fault --
+ends the children, never the DP ranks that hold the line's value.  A watchdog bounds the
+phase inside the children (``--tp-timeout``) and the parents kill a child past it + 60 s.
 """
 from __future__ import annotations
 
@@ -93,9 +94,11 @@ def _clamp_prompts(prompts, vocab):
     return [[t % vocab for t in p] for p in prompts]
 
 
-def tp_phase(a, rank: int, world: int, dev, serve, res_dp: dict | None, emit) -> dict | None:
+def tp_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
     """Run the TP = world phase on every rank; rank 0 returns the ``tp`` block (others None).
-    ``serve``: bench.serve_closed_loop; ``emit``: bench._emit (the watchdog's printer)."""
+    ``serve``: bench.serve_closed_loop; ``on_fail(msg)``: called by the watchdog or on an
+    exception, right before this process exits (bench.py runs the phase in child processes
+    whose rank 0 writes the block, or that message, to a file its parent reads)."""
     import torch.distributed as dist
 
     from ..models import build_model
@@ -113,12 +116,12 @@ def tp_phase(a, rank: int, world: int, dev, serve, res_dp: dict | None, emit) ->
             return
         msg = f"TP phase exceeded --tp-timeout {a.tp_timeout:.0f} s (first-contact hang?)"
         print(f"[bench rank {rank}] {msg}: exiting", file=sys.stderr, flush=True)
-        if res_dp is not None:
-            res_dp["tp"] = {"tp": world, "error": msg}
-            emit(res_dp)
-        os._exit(0)
+        on_fail(msg)
+        os._exit(3)
 
     threading.Thread(target=watchdog, daemon=True, name="tp-phase-watchdog").start()
+    if os.environ.get("MLOP_INJECT_TP_PHASE_ABORT") == str(rank):  # fault injection: this rank dies
+        os.abort()
     out: dict = {"tp": world, "world": world}
     try:
         gc.collect()
@@ -189,12 +192,10 @@ def tp_phase(a, rank: int, world: int, dev, serve, res_dp: dict | None, emit) ->
 
         traceback.print_exc()
         msg = f"{type(e).__name__}: {e}"
-        if res_dp is not None:
-            res_dp["tp"] = {"tp": world, "error": msg[:500]}
-            emit(res_dp)
+        on_fail(msg[:500])
         # peers may be blocked in a collective with us: leave now, their watchdogs end them
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)  # the line (rank 0) carries the error; a non-zero rank exit would drop it
+        os._exit(4)
     finally:
         done.set()

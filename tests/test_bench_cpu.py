@@ -74,6 +74,7 @@ def test_bench_two_ranks_gloo():
     assert tp["tp"] == 2 and tp["world"] == 2 and tp["backend"] == "gloo" and tp["k15"] == "off"
     assert tp["tokens_per_sec"] > 0 and tp["steps"] == 3 and tp["batch"] == 16
     assert tp["first_token_match"] and tp["tokens_match"] and tp["tokens_checked"] == 32
+    assert tp["child_rc"] == 0  # the phase ran in child processes (bench.py --tp-phase-child)
 
 
 def test_bench_tp_phase_watchdog_keeps_the_dp_result():
@@ -82,7 +83,21 @@ def test_bench_tp_phase_watchdog_keeps_the_dp_result():
     d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
               *ARGS, "--tp-batch", "64", "--tp-steps", "200", "--tp-timeout", "3"])
     assert d["value"] > 0 and d["n_gpus"] == 2
-    assert "tp-timeout" in d["tp"]["error"]
+    assert "tp-timeout" in d["tp"]["error"] and d["tp"]["child_rc"] == 3
+
+
+def test_bench_tp_phase_child_crash_keeps_the_dp_result():
+    """A rank of the TP phase that dies outright (abort: what a GPU fault does to a process) ends
+    only its child process: the DP ranks still print THE line, with tp.error, and exit 0."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", MLOP_INJECT_TP_PHASE_ABORT="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
+                        *ARGS, *TP_ARGS, "--tp-timeout", "20"], cwd="/tmp", capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and "no result" in d["tp"]["error"] and d["tp"]["child_rc"] != 0
 
 
 def test_bench_self_launches_n_ranks():
