@@ -112,7 +112,14 @@ def parse(argv=None):
     ap.add_argument("--tp-timeout", type=float, default=240.0,
                     help="time limit of the TP phase (seconds): its child processes are stopped past it and the "
                          "line carries tp.error, so a first-contact hang cannot eat the DP result")
-    ap.add_argument("--tp-phase-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--ep-phase", choices=("auto", "on", "off"), default="auto",
+                    help="after the TP phase, a short EP = world phase of --ep-model (config 5: DP attention, every "
+                         "MoE layer an expert exchange over IPC peer memory across the devices), with a greedy-token "
+                         "check against the dense fp32 EP = 1 model, reported as the 'ep' block.  auto: on when "
+                         "world > 1")
+    ap.add_argument("--ep-model", default="mixtral-8x7b")
+    ap.add_argument("--ep-batch", type=int, default=256, help="concurrent requests PER RANK in the EP phase")
+    ap.add_argument("--phase-child", choices=("tp", "ep"), default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cr-ready-samples", type=int, default=3,
                     help="CR -> ready measurements with the predictor as a FRESH OS process (operator -> "
                          "ProcessLauncher -> /v2/health/ready), taken before the serving run on rank 0's GPU; "
@@ -237,8 +244,8 @@ def main(argv=None):
     a = parse(argv)
     if a.http:
         return http_main(a)
-    if a.tp_phase_child:
-        return _tp_child_main(a)
+    if a.phase_child:
+        return _phase_child_main(a)
     from mlopamd.parallel.comm import env_rank_info, init_distributed
     import torch.distributed as dist
 
@@ -334,20 +341,24 @@ def main(argv=None):
         # failure there -- a hang, an abort, a GPU fault -- ends the child, never this process,
         # which holds the DP result and prints the line either way
         del engine
-        tp = _tp_phase_children(a, argv, rank, world, dev)
+        tp = _phase_children("tp", a, argv, rank, world, dev)
         if res is not None:
             res["tp"] = tp
+    if _ep_phase_on(a, world):
+        ep = _phase_children("ep", a, argv, rank, world, dev)
+        if res is not None:
+            res["ep"] = ep
     _emit(res)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _tp_phase_children(a, argv, rank: int, world: int, dev) -> dict | None:
-    """Run ``runtime/bench_tp.tp_phase`` in one child process per rank (``--tp-phase-child``),
-    on a fresh rendezvous port, and collect rank 0's ``tp`` block from the file its child
-    writes.  Every parent waits at most ``--tp-timeout`` + 60 s for its child (killed past it),
-    then the parents meet at a barrier; a child that died leaves ``tp.error``."""
+def _phase_children(phase: str, a, argv, rank: int, world: int, dev) -> dict | None:
+    """Run ``runtime/bench_tp.tp_phase`` / ``runtime/bench_ep.ep_phase`` in one child process per
+    rank (``--phase-child``), on a fresh rendezvous port, and collect rank 0's block from the
+    file its child writes.  Every parent waits at most ``--tp-timeout`` + 60 s for its child
+    (killed past it), then the parents meet at a barrier; a child that died leaves ``error``."""
     import gc
     import socket
     import subprocess
@@ -364,7 +375,7 @@ def _tp_phase_children(a, argv, rank: int, world: int, dev) -> dict | None:
         with socket.socket() as s_:
             s_.bind(("127.0.0.1", 0))
             box[0] = s_.getsockname()[1]
-        fd, box[1] = tempfile.mkstemp(prefix="mlop-tp-phase-", suffix=".json")
+        fd, box[1] = tempfile.mkstemp(prefix=f"mlop-{phase}-phase-", suffix=".json")
         os.close(fd)
     if world > 1:
         dist.broadcast_object_list(box, src=0)
@@ -374,16 +385,16 @@ def _tp_phase_children(a, argv, rank: int, world: int, dev) -> dict | None:
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)), MLOP_TP_PHASE_OUT=out_path,
                HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--tp-phase-child"]
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase-child", phase]
     t0 = time.perf_counter()
-    _progress(rank, f"TP = {world} phase in a child process (port {port})")
+    _progress(rank, f"{phase.upper()} = {world} phase in a child process (port {port})")
     p = subprocess.Popen(cmd, env=env)
     try:
         rc = p.wait(timeout=a.tp_timeout + 60)
     except subprocess.TimeoutExpired:
         p.kill()
         rc = p.wait()
-        _progress(rank, "TP phase child killed at its time limit")
+        _progress(rank, f"{phase.upper()} phase child killed at its time limit")
     if world > 1:
         dist.barrier()  # every child is gone before the parents go on
     if rank != 0:
@@ -401,21 +412,21 @@ def _tp_phase_children(a, argv, rank: int, world: int, dev) -> dict | None:
         except OSError:
             pass
     if tp is None:
-        tp = {"tp": world, "error": f"TP phase child exited with {rc} and no result"}
+        tp = {phase: world, "error": f"{phase.upper()} phase child exited with {rc} and no result"}
     tp["child_rc"] = rc
     tp["child_wall_s"] = round(time.perf_counter() - t0, 2)
     return tp
 
 
-def _tp_child_main(a) -> None:
-    """``--tp-phase-child``: one rank of the TP phase (spawned by ``_tp_phase_children``); rank
-    0 writes the ``tp`` block, or the error that ended the phase, to $MLOP_TP_PHASE_OUT."""
+def _phase_child_main(a) -> None:
+    """``--phase-child tp|ep``: one rank of a parallel phase (spawned by ``_phase_children``);
+    rank 0 writes the block, or the error that ended the phase, to $MLOP_TP_PHASE_OUT."""
     from mlopamd.parallel.comm import env_rank_info, init_distributed
-    from mlopamd.runtime.bench_tp import tp_phase
     import torch.distributed as dist
 
     rank, local_rank, world = env_rank_info()
     out_path = os.environ.get("MLOP_TP_PHASE_OUT", "")
+    phase = a.phase_child
 
     def write(block):
         if rank == 0 and out_path:
@@ -429,11 +440,21 @@ def _tp_child_main(a) -> None:
     dev = torch.device("cuda", 0 if a.share_gpu else local_rank) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    tp = tp_phase(a, rank, world, dev, serve_closed_loop, lambda msg: write({"tp": world, "error": msg}))
-    write(tp)
+    if phase == "tp":
+        from mlopamd.runtime.bench_tp import tp_phase as run_phase
+    else:
+        from mlopamd.runtime.bench_ep import ep_phase as run_phase
+    block = run_phase(a, rank, world, dev, serve_closed_loop, lambda msg: write({phase: world, "error": msg}))
+    write(block)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _ep_phase_on(a, world: int) -> bool:
+    if a.ep_phase == "off" or a.tp > 1 or a.ep > 1:
+        return False
+    return world > 1 or a.ep_phase == "on"
 
 
 def _tp_phase_on(a, world: int) -> bool:

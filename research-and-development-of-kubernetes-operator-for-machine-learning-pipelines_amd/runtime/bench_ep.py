@@ -1,0 +1,159 @@
+"""The benchmark's expert-parallel phase: Mixtral-8x7B EP = world over the same GPUs (config 5).
+
+After the Llama-3 DP replicas and the TP = N phase (runtime/bench_tp.py), ``bench.py --gpus N``
+serves a short EP = N phase of Mixtral-8x7B in child processes, reported as the JSON line's
+``ep`` block, so the one run on an N-GPU node also carries the expert exchange across devices
+(CL4 over IPC peer memory, ops/csrc/ep_exchange.hip; RCCL all-to-all without it):
+
+  1. every rank builds its EP shard: the dense weights (embedding, attention, router, norms)
+     are drawn from the same seeded stream on every rank, and each expert's weights from a
+     generator seeded by its GLOBAL expert id (``_init_experts``), so the N shards are exactly
+     one model whose experts are all different (a dispatch to the wrong rank changes tokens);
+  2. rank 0 also holds that full model (EP = 1: its dense weights copied from its shard, every
+     expert initialised the same way) for the dense fp32 oracle (models/reference.py);
+  3. greedy check: 8 fixed prompts x ``CHECK_TOKENS`` tokens through the EP group's engines
+     (rank 0 serves them, the others join with padding-only forwards: DP attention, every MoE
+     layer an exchange over the whole group); rank 0 teacher-forces the oracle over the same
+     tokens (top-5 and within 0.25 logit std, bench_tp._dense_agreement);
+  4. a closed-loop serve, ``--ep-batch`` requests PER RANK, ``--tp-warmup`` + ``--tp-steps``
+     steps timed between syncs and world barriers -> ``tokens_per_sec`` (all ranks).
+"""
+from __future__ import annotations
+
+import gc
+import os
+import sys
+import threading
+import time
+
+import torch
+
+from .bench_tp import PROMPTS, _clamp_prompts, _dense_agreement
+
+CHECK_TOKENS = 2
+
+
+@torch.no_grad()
+def _init_experts(model, seed: int) -> None:
+    """Expert e of layer l <- N(0, 0.02) from a generator seeded by (seed, l, e): the same values
+    whichever rank (or the full model) holds expert e."""
+    for li, L in enumerate(model.layers):
+        for j in range(model.n_local_experts):
+            e = model.expert_start + j
+            g = torch.Generator(device=model.device).manual_seed(seed * 7919 + li * 1024 + e)
+            for name in ("w13", "w2"):
+                t = L[name][j]
+                t.copy_(torch.empty(t.shape, device=model.device, dtype=torch.float32).normal_(0.0, 0.02, generator=g)
+                        .to(t.dtype))
+
+
+@torch.no_grad()
+def _copy_dense(dst, src) -> None:
+    """dst (EP = 1) <- src's dense weights (EP shard of the same config): everything but experts."""
+    dst.embed.copy_(src.embed)
+    for Ld, Ls in zip(dst.layers, src.layers):
+        for k in Ld:
+            if k not in ("w13", "w2"):
+                Ld[k].copy_(Ls[k])
+    dst.final_norm.copy_(src.final_norm)
+    if dst.lm_head is not dst.embed:
+        dst.lm_head.copy_(src.lm_head)
+
+
+def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
+    """Run the EP = world phase on every rank; rank 0 returns the ``ep`` block (others None)."""
+    import torch.distributed as dist
+
+    from ..models import build_model
+    from ..models.config import get_config
+    from ..parallel.comm import make_parallel_state
+    from .engine import Engine, EngineConfig
+    from .kv_cache import blocks_needed
+    from .sampler import SamplingParams
+
+    t_phase = time.perf_counter()
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(a.tp_timeout):
+            return
+        msg = f"EP phase exceeded --tp-timeout {a.tp_timeout:.0f} s"
+        print(f"[bench rank {rank}] {msg}: exiting", file=sys.stderr, flush=True)
+        on_fail(msg)
+        os._exit(3)
+
+    threading.Thread(target=watchdog, daemon=True, name="ep-phase-watchdog").start()
+    out: dict = {"ep": world, "world": world, "model": a.ep_model}
+    try:
+        gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+        dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+        cfg = get_config(a.ep_model)
+        seed = a.seed + 91
+        t0 = time.perf_counter()
+        ps = make_parallel_state(tp_size=1, ep_size=world)
+        out["backend"] = dist.get_backend() if dist.is_initialized() else None
+        shard = build_model(cfg, device=dev, dtype=dtype, pstate=ps, seed=seed)
+        _init_experts(shard, seed)
+        full = None
+        if rank == 0:  # the dense oracle's model: one model with the group's weights
+            full = build_model(cfg, device=dev, dtype=dtype, seed=seed)
+            _copy_dense(full, shard)
+            _init_experts(full, seed)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        out["build_s"] = round(time.perf_counter() - t0, 2)
+        out["weight_gb_per_gpu"] = round(shard.weight_bytes() / 1e9, 3)
+        B = max(len(PROMPTS), a.ep_batch)
+        nb = B * blocks_needed(min(a.max_model_len, a.prompt_len + a.output_len + 16)) + 64
+        ec = EngineConfig(max_num_seqs=B, max_num_batched_tokens=a.max_batched_tokens,
+                          max_model_len=a.max_model_len, num_kv_blocks=nb, use_graphs=not a.no_graphs,
+                          prefill_min_batch=a.prefill_min_batch, max_decode_gap=a.max_decode_gap,
+                          mixed_prefill=not a.no_mixed, mixed_min_chunk=a.mixed_min_chunk,
+                          enable_prefix_caching=not a.no_prefix_cache)
+        t0 = time.perf_counter()
+        eng = Engine(shard, ec)
+        out["engine_s"] = round(time.perf_counter() - t0, 2)
+        out["exchange"] = "ipc" if getattr(ps.ep, "ex", None) is not None else "all_to_all"
+        # greedy check: rank 0's requests, every rank stepping together (generate on EVERY rank)
+        prompts = _clamp_prompts(PROMPTS, cfg.vocab_size)
+        mine = prompts if rank == 0 else []
+        toks = eng.generate(mine, SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
+        gen, elapsed, stats, ramp = serve(eng, a, a.ep_batch, a.tp_steps, a.tp_warmup, rank, ep_group=ps.ep_cpu)
+        t_all = torch.tensor([float(gen), elapsed], dtype=torch.float64)
+        if dist.is_initialized():
+            parts = [torch.zeros_like(t_all) for _ in range(world)]
+            dist.all_gather(parts, t_all, group=ps.ep_cpu)
+        else:
+            parts = [t_all]
+        if rank != 0:
+            out = None
+        else:
+            tot = sum(float(p[0]) for p in parts)
+            t_max = max(float(p[1]) for p in parts)
+            out.update({"batch_per_rank": a.ep_batch, "steps": a.tp_steps, "warmup": a.tp_warmup, "ramp_steps": ramp,
+                        "tokens_per_sec": round(tot / max(t_max, 1e-9), 2),
+                        "ms_per_step": round(1e3 * t_max / max(1, a.tp_steps), 3),
+                        "graph_steps": int(stats.get("graph_steps", 0))})
+            t0 = time.perf_counter()
+            out.update(_dense_agreement(full, prompts, toks))
+            out["check_s"] = round(time.perf_counter() - t0, 2)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier()
+        if out is not None:
+            out["wall_s"] = round(time.perf_counter() - t_phase, 2)
+        return out
+    except Exception as e:  # noqa: BLE001 - reported in the line; the DP value stands
+        import traceback
+
+        traceback.print_exc()
+        on_fail(f"{type(e).__name__}: {e}"[:500])
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(4)
+    finally:
+        done.set()

@@ -22,7 +22,7 @@ TP = N phase of the same model, reported as the JSON line's ``tp`` block:
   4. a closed-loop serve of ``--tp-batch`` requests, ``--tp-warmup`` + ``--tp-steps`` engine
      steps timed between device syncs + world barriers -> ``tokens_per_sec``.
 
-bench.py runs the phase in child processes (``--tp-phase-child``), one per rank with its own
+bench.py runs the phase in child processes (``--phase-child tp``), one per rank with its own
 process group, so a first-contact failure on real peers -- a hang, an abort, a GPU fault --
 ends the children, never the DP ranks that hold the line's value.  A watchdog bounds the
 phase inside the children (``--tp-timeout``) and the parents kill a child past it + 60 s.

@@ -28,7 +28,7 @@ def _run(cmd):
 
 
 ARGS = ["--model", "tiny-llama", "--steps", "4", "--warmup", "2", "--batch", "8"]
-TP_ARGS = ["--tp-batch", "16", "--tp-steps", "3", "--tp-warmup", "1"]
+TP_ARGS = ["--tp-batch", "16", "--tp-steps", "3", "--tp-warmup", "1", "--ep-model", "tiny-mixtral", "--ep-batch", "8"]
 
 
 def test_bench_single_process_json():
@@ -74,14 +74,20 @@ def test_bench_two_ranks_gloo():
     assert tp["tp"] == 2 and tp["world"] == 2 and tp["backend"] == "gloo" and tp["k15"] == "off"
     assert tp["tokens_per_sec"] > 0 and tp["steps"] == 3 and tp["batch"] == 16
     assert tp["first_token_match"] and tp["tokens_match"] and tp["tokens_checked"] == 32
-    assert tp["child_rc"] == 0  # the phase ran in child processes (bench.py --tp-phase-child)
+    assert tp["child_rc"] == 0  # the phase ran in child processes (bench.py --phase-child tp)
+    # and an EP = world phase of a MoE model: DP attention + the expert exchange, greedy tokens
+    # against the dense fp32 EP = 1 model whose experts are the group's
+    ep = d["ep"]
+    assert ep["ep"] == 2 and ep["model"] == "tiny-mixtral" and ep["exchange"] == "all_to_all"
+    assert ep["tokens_per_sec"] > 0 and ep["child_rc"] == 0
+    assert ep["first_token_match"] and ep["tokens_match"] and ep["tokens_checked"] == 16
 
 
 def test_bench_tp_phase_watchdog_keeps_the_dp_result():
     """A TP phase that overruns --tp-timeout (a first-contact hang on real peers) must not cost
     the DP value: rank 0 prints THE line with tp.error and every rank exits 0."""
     d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
-              *ARGS, "--tp-batch", "64", "--tp-steps", "200", "--tp-timeout", "3"])
+              *ARGS, "--tp-batch", "64", "--tp-steps", "200", "--tp-timeout", "3", "--ep-phase", "off"])
     assert d["value"] > 0 and d["n_gpus"] == 2
     assert "tp-timeout" in d["tp"]["error"] and d["tp"]["child_rc"] == 3
 
@@ -91,7 +97,8 @@ def test_bench_tp_phase_child_crash_keeps_the_dp_result():
     only its child process: the DP ranks still print THE line, with tp.error, and exit 0."""
     env = dict(os.environ, OMP_NUM_THREADS="2", MLOP_INJECT_TP_PHASE_ABORT="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
-                        *ARGS, *TP_ARGS, "--tp-timeout", "20"], cwd="/tmp", capture_output=True, text=True,
+                        *ARGS, *TP_ARGS, "--tp-timeout", "20", "--ep-phase", "off"], cwd="/tmp",
+                       capture_output=True, text=True,
                        timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
