@@ -139,6 +139,16 @@ def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
                         "graph_steps": int(stats.get("graph_steps", 0))})
             t0 = time.perf_counter()
             out.update(_dense_agreement(full, prompts, toks))
+            # the same prompts through an EP = 1 engine on the full model (same HIP kernels, the
+            # single-rank MoE path): the bf16 noise floor, and whether a mismatch is the exchange
+            e1 = Engine(full, EngineConfig(max_num_seqs=len(prompts), max_num_batched_tokens=a.max_batched_tokens,
+                                           max_model_len=a.max_model_len, num_kv_blocks=len(prompts) * 8 + 16,
+                                           use_graphs=not a.no_graphs, graph_buckets=(len(prompts),),
+                                           async_scheduling=False))
+            ref = e1.generate(prompts, SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
+            e1.shutdown()
+            out["ep1_engine_vs_dense"] = _dense_agreement(full, prompts, ref)
+            out["tokens_equal_ep1_engine"] = sum(int(x == y) for p_, q_ in zip(toks, ref) for x, y in zip(p_, q_))
             out["check_s"] = round(time.perf_counter() - t0, 2)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
