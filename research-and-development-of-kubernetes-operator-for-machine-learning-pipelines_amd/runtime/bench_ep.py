@@ -9,14 +9,15 @@ serves a short EP = N phase of Mixtral-8x7B in child processes, reported as the 
      are drawn from the same seeded stream on every rank, and each expert's weights from a
      generator seeded by its GLOBAL expert id (``_init_experts``), so the N shards are exactly
      one model whose experts are all different (a dispatch to the wrong rank changes tokens);
-  2. rank 0 also holds that full model (EP = 1: its dense weights copied from its shard, every
-     expert initialised the same way) for the dense fp32 oracle (models/reference.py);
-  3. greedy check: 8 fixed prompts x ``CHECK_TOKENS`` tokens through the EP group's engines
-     (rank 0 serves them, the others join with padding-only forwards: DP attention, every MoE
-     layer an exchange over the whole group); rank 0 teacher-forces the oracle over the same
-     tokens (top-5 and within 0.25 logit std, bench_tp._dense_agreement);
-  4. a closed-loop serve, ``--ep-batch`` requests PER RANK, ``--tp-warmup`` + ``--tp-steps``
-     steps timed between syncs and world barriers -> ``tokens_per_sec`` (all ranks).
+  2. greedy check (``_check``) at the model's full width and CHECK_LAYERS depth: 8 fixed prompts
+     x ``CHECK_TOKENS`` tokens through the EP group's engines (rank 0 serves them, the others
+     join with padding-only forwards: DP attention, every MoE layer an exchange over the whole
+     group); rank 0 then holds the same model whole (EP = 1) and checks the tokens against the
+     dense fp32 oracle (models/reference.py; top-5 and within 0.25 logit std,
+     bench_tp._dense_agreement) and against an EP = 1 engine;
+  3. a closed-loop serve of the FULL-depth shard, ``--ep-batch`` requests PER RANK,
+     ``--tp-warmup`` + ``--tp-steps`` steps timed between syncs and world barriers ->
+     ``tokens_per_sec`` (all ranks).
 """
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ import torch
 from .bench_tp import PROMPTS, _clamp_prompts, _dense_agreement
 
 CHECK_TOKENS = 2
+CHECK_LAYERS = 2
 
 
 @torch.no_grad()
@@ -60,6 +62,50 @@ def _copy_dense(dst, src) -> None:
         dst.lm_head.copy_(src.lm_head)
 
 
+def _check(a, rank: int, dev, dtype, cfg, ps, seed: int) -> dict:
+    """Greedy check of the EP group on ``cfg`` (the bench model's width at CHECK_LAYERS depth).
+
+    Every rank builds its shard and an engine and steps ``generate`` together (rank 0 with the
+    prompts, the others padding-only forwards that still join every exchange). Rank 0 then holds
+    the same model whole (EP = 1) and returns (others: {}):
+      * the dense fp32 oracle's verdict on the EP tokens (bench_tp._dense_agreement);
+      * ``tokens_equal_ep1_engine``: EP tokens equal to an EP = 1 engine's on the whole model
+        (the same kernels without the exchange).
+
+    Why not full depth: a random-init Mixtral's greedy tokens are chaotic in depth. Rounding only
+    the MoE input to bf16 in the fp32 oracle flips 10 of 8,320 router top-2 selections over 32
+    layers and moves the oracle's own argmax to rank 133-210 (profiles/r06_ep_phase.md,
+    scripts/ep_chaos_probe.py); any bf16 engine, EP or not, then lands at rank ~2,000. At 2
+    layers no selection flips, the engine agrees 15/16 exactly, and a wrong dispatch or
+    combine gives a token at a random rank of 32k."""
+    from ..models import build_model
+    from .engine import Engine, EngineConfig
+    from .sampler import SamplingParams
+
+    shard = build_model(cfg, device=dev, dtype=dtype, pstate=ps, seed=seed)
+    _init_experts(shard, seed)
+    prompts = _clamp_prompts(PROMPTS, cfg.vocab_size)
+    ec = dict(max_num_seqs=len(prompts), max_num_batched_tokens=a.max_batched_tokens, max_model_len=a.max_model_len,
+              num_kv_blocks=len(prompts) * 8 + 16, use_graphs=not a.no_graphs, graph_buckets=(len(prompts),),
+              async_scheduling=False)
+    eng = Engine(shard, EngineConfig(**ec))
+    toks = eng.generate(prompts if rank == 0 else [], SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
+    eng.shutdown()
+    del eng
+    if rank != 0:
+        return {}
+    full = build_model(cfg, device=dev, dtype=dtype, seed=seed)
+    _copy_dense(full, shard)
+    _init_experts(full, seed)
+    out = {"check_layers": cfg.num_layers}
+    out.update(_dense_agreement(full, prompts, toks))
+    e1 = Engine(full, EngineConfig(**ec))
+    ref = e1.generate(prompts, SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
+    e1.shutdown()
+    out["tokens_equal_ep1_engine"] = sum(int(x == y) for p_, q_ in zip(toks, ref) for x, y in zip(p_, q_))
+    return out
+
+
 def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
     """Run the EP = world phase on every rank; rank 0 returns the ``ep`` block (others None)."""
     import torch.distributed as dist
@@ -69,7 +115,6 @@ def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
     from ..parallel.comm import make_parallel_state
     from .engine import Engine, EngineConfig
     from .kv_cache import blocks_needed
-    from .sampler import SamplingParams
 
     t_phase = time.perf_counter()
     done = threading.Event()
@@ -92,21 +137,27 @@ def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
         dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
         cfg = get_config(a.ep_model)
         seed = a.seed + 91
-        t0 = time.perf_counter()
         ps = make_parallel_state(tp_size=1, ep_size=world)
         out["backend"] = dist.get_backend() if dist.is_initialized() else None
+        out["exchange"] = "ipc" if getattr(ps.ep, "ex", None) is not None else "all_to_all"
+        # 1. greedy check at CHECK_LAYERS depth (full width, every MoE layer an exchange)
+        t0 = time.perf_counter()
+        out.update(_check(a, rank, dev, dtype, get_config(a.ep_model, num_layers=min(cfg.num_layers, CHECK_LAYERS)),
+                          ps, seed))
+        out["check_s"] = round(time.perf_counter() - t0, 2)
+        gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+        # 2. the timed serve on the full-depth shard
+        t0 = time.perf_counter()
         shard = build_model(cfg, device=dev, dtype=dtype, pstate=ps, seed=seed)
         _init_experts(shard, seed)
-        full = None
-        if rank == 0:  # the dense oracle's model: one model with the group's weights
-            full = build_model(cfg, device=dev, dtype=dtype, seed=seed)
-            _copy_dense(full, shard)
-            _init_experts(full, seed)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         out["build_s"] = round(time.perf_counter() - t0, 2)
         out["weight_gb_per_gpu"] = round(shard.weight_bytes() / 1e9, 3)
-        B = max(len(PROMPTS), a.ep_batch)
+        B = a.ep_batch
         nb = B * blocks_needed(min(a.max_model_len, a.prompt_len + a.output_len + 16)) + 64
         ec = EngineConfig(max_num_seqs=B, max_num_batched_tokens=a.max_batched_tokens,
                           max_model_len=a.max_model_len, num_kv_blocks=nb, use_graphs=not a.no_graphs,
@@ -116,11 +167,6 @@ def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
         t0 = time.perf_counter()
         eng = Engine(shard, ec)
         out["engine_s"] = round(time.perf_counter() - t0, 2)
-        out["exchange"] = "ipc" if getattr(ps.ep, "ex", None) is not None else "all_to_all"
-        # greedy check: rank 0's requests, every rank stepping together (generate on EVERY rank)
-        prompts = _clamp_prompts(PROMPTS, cfg.vocab_size)
-        mine = prompts if rank == 0 else []
-        toks = eng.generate(mine, SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
         gen, elapsed, stats, ramp = serve(eng, a, a.ep_batch, a.tp_steps, a.tp_warmup, rank, ep_group=ps.ep_cpu)
         t_all = torch.tensor([float(gen), elapsed], dtype=torch.float64)
         if dist.is_initialized():
@@ -137,19 +183,6 @@ def ep_phase(a, rank: int, world: int, dev, serve, on_fail) -> dict | None:
                         "tokens_per_sec": round(tot / max(t_max, 1e-9), 2),
                         "ms_per_step": round(1e3 * t_max / max(1, a.tp_steps), 3),
                         "graph_steps": int(stats.get("graph_steps", 0))})
-            t0 = time.perf_counter()
-            out.update(_dense_agreement(full, prompts, toks))
-            # the same prompts through an EP = 1 engine on the full model (same HIP kernels, the
-            # single-rank MoE path): the bf16 noise floor, and whether a mismatch is the exchange
-            e1 = Engine(full, EngineConfig(max_num_seqs=len(prompts), max_num_batched_tokens=a.max_batched_tokens,
-                                           max_model_len=a.max_model_len, num_kv_blocks=len(prompts) * 8 + 16,
-                                           use_graphs=not a.no_graphs, graph_buckets=(len(prompts),),
-                                           async_scheduling=False))
-            ref = e1.generate(prompts, SamplingParams(max_tokens=CHECK_TOKENS, ignore_eos=True))
-            e1.shutdown()
-            out["ep1_engine_vs_dense"] = _dense_agreement(full, prompts, ref)
-            out["tokens_equal_ep1_engine"] = sum(int(x == y) for p_, q_ in zip(toks, ref) for x, y in zip(p_, q_))
-            out["check_s"] = round(time.perf_counter() - t0, 2)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         if dist.is_initialized():

@@ -81,6 +81,7 @@ def test_bench_two_ranks_gloo():
     assert ep["ep"] == 2 and ep["model"] == "tiny-mixtral" and ep["exchange"] == "all_to_all"
     assert ep["tokens_per_sec"] > 0 and ep["child_rc"] == 0
     assert ep["first_token_match"] and ep["tokens_match"] and ep["tokens_checked"] == 16
+    assert ep["tokens_equal_ep1_engine"] == 16 and ep["check_layers"] == 2
 
 
 def test_bench_tp_phase_watchdog_keeps_the_dp_result():
