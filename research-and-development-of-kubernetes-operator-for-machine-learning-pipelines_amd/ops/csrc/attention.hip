@@ -32,6 +32,7 @@
 // REQUIREMENT: the cache is zero-initialised at allocation (masked lanes multiply
 // p = 0 with whatever the unused slots hold; NaN garbage would poison O).
 #include <type_traits>
+#include <algorithm>
 
 #include "common.h"
 #include "launch.h"
@@ -496,20 +497,18 @@ __device__ __forceinline__ uint32_t vt32_base(int lane) {
   return 256u * t + 16u * (c ^ vswz(t)) + 8u * (p & 1);
 }
 
-template <int G, int WPC>
-__global__ void __launch_bounds__(256, WPC) flash32_prefill_kernel(
-    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
-    const int* __restrict__ q_start, const int* __restrict__ q_len,
-    const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int num_blocks) {
+// one flash tile (128 q-rows of ONE kv head against its whole causal key range)
+template <int G>
+__device__ __forceinline__ void flash32_item(
+    uint16_t* smem, int tile, int kvh, uint16_t* __restrict__ out, const uint16_t* __restrict__ q,
+    const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc, const int* __restrict__ block_tables,
+    int bt_stride, const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
+    const int* __restrict__ q_start, const int* __restrict__ q_len, const int* __restrict__ ctx_len, int Hq,
+    int Hkv, float scale_log2, int num_blocks) {
   constexpr int QB = 128 / G;            // query tokens per workgroup
   constexpr int STAGES = 3;
   constexpr int STAGE = 4 * kBS * kD;    // bf16 per stage: K page A | K page B | V page A | V page B
   constexpr int PAGE = kBS * kD;
-  __shared__ __attribute__((aligned(256))) uint16_t smem[STAGES * STAGE];
-
-  const int tile = blockIdx.x / Hkv, kvh = blockIdx.x % Hkv;  // kv head fastest: one XCD per head
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int s = ptile_seq[tile], q0 = ptile_q0[tile];
   const int ql = q_len[s], ctx = ctx_len[s], qs = q_start[s];
@@ -729,17 +728,76 @@ __global__ void __launch_bounds__(256, WPC) flash32_prefill_kernel(
     }
 }
 
+// PERSIST: a persistent grid of S x Hkv workgroups (S slots per kv head; blockIdx % Hkv = kv
+// head, so each head stays on one XCD as in the one-item grid) walks the tile list in rounds of
+// S tiles, boustrophedon: slot j takes tile r S + j in even rounds and r S + S - 1 - j in odd
+// ones.  The host's per-sequence latest-first tile order then pairs a heavy tile with its light
+// mirror on every slot (16 x 512: positions p, 15 - p, p, 15 - p), and the launch holds whole
+// rounds instead of ~2 k one-item workgroups.
+template <int G, int WPC, bool PERSIST>
+__global__ void __launch_bounds__(256, WPC) flash32_prefill_kernel(
+    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
+    const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int num_blocks, int num_ptiles) {
+  constexpr int STAGES = 3;
+  constexpr int STAGE = 4 * kBS * kD;    // bf16 per stage: K page A | K page B | V page A | V page B
+  __shared__ __attribute__((aligned(256))) uint16_t smem[STAGES * STAGE];
+  if constexpr (!PERSIST) {
+    flash32_item<G>(smem, blockIdx.x / Hkv, blockIdx.x % Hkv, out, q, kc, vc, block_tables, bt_stride, ptile_seq,
+                    ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks);
+  } else {
+    const int kvh = blockIdx.x % Hkv, j = blockIdx.x / Hkv, S = gridDim.x / Hkv;
+    for (int r = 0; r * S < num_ptiles; ++r) {
+      const int t = r * S + ((r & 1) ? S - 1 - j : j);
+      if (t >= num_ptiles) continue;  // a partial last round: every slot still leaves the loop
+      if (r > 0) __syncthreads();      // the previous tile's last ring reads before this tile's DMAs
+      flash32_item<G>(smem, t, kvh, out, q, kc, vc, block_tables, bt_stride, ptile_seq, ptile_q0, q_start, q_len,
+                      ctx_len, Hq, Hkv, scale_log2, num_blocks);
+    }
+  }
+}
+
+// flash_persist op: 0 = one workgroup per (tile, kv head) item; n = the persistent grid of n
+// workgroups per CU (flash32_prefill_kernel PERSIST); n >= 64: exactly n / 64 slots per kv head
+// (tests: several rounds on a few tiles).  Off by default: +3-5 % at 16 x 512 in the host's
+// per-sequence order, nothing or -1-2 % at 1024+ tokens in the LPT order the engine uses there
+// (profiles/r06_flash_persist.md).
+static int g_flash_persist = 0;
+int flash_persist(int set) {
+  if (set >= 0) g_flash_persist = set;
+  return g_flash_persist;
+}
+
+static int device_cus() {
+  static int cus[16] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) return 256;
+  if (cus[dev] == 0) (void)hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev);
+  return cus[dev] > 0 ? cus[dev] : 256;
+}
+
 void launch_flash_prefill(void* out, const void* q, const void* kc, const void* vc, const int* bt,
                           int bt_stride, const int* ptile_seq, const int* ptile_q0,
                           const int* q_start, const int* q_len, const int* ctx_len, int num_ptiles,
                           int Hq, int Hkv, float scale_log2, int num_blocks, hipStream_t st) {
   if (num_ptiles == 0) return;
-  dim3 grid(num_ptiles * Hkv);
-#define MLOP_FLASH_CASE(GG)                                                                       \
-  case GG:                                                                                        \
-    flash32_prefill_kernel<GG, 2><<<grid, 256, 0, st>>>(                                          \
-        (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt,        \
-        bt_stride, ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks); \
+  const int slots = g_flash_persist >= 64 ? g_flash_persist / 64
+                    : g_flash_persist > 0 ? std::max(1, g_flash_persist * device_cus() / Hkv) : 0;
+  const bool persist = slots > 0 && num_ptiles > slots;
+  dim3 grid((persist ? slots : num_ptiles) * Hkv);
+#define MLOP_FLASH_CASE(GG)                                                                              \
+  case GG:                                                                                               \
+    if (persist)                                                                                         \
+      flash32_prefill_kernel<GG, 2, true><<<grid, 256, 0, st>>>(                                         \
+          (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt, bt_stride,   \
+          ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks, num_ptiles);    \
+    else                                                                                                 \
+      flash32_prefill_kernel<GG, 2, false><<<grid, 256, 0, st>>>(                                        \
+          (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt, bt_stride,   \
+          ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks, num_ptiles);    \
     break;
   switch (Hq / Hkv) {
     MLOP_FLASH_CASE(1)

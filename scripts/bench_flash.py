@@ -55,22 +55,29 @@ vc = torch.randn(NB, Hkv, BS, D, device=dev, dtype=bf)
 q = torch.randn(S * L, Hq, D, device=dev, dtype=bf)
 out = torch.empty_like(q)
 flops = 4 * S * (L * (L + 1) // 2) * D * Hq
-for _ in range(3):
-    ops.paged_attention(q, kc, vc, m, out=out)
-torch.cuda.synchronize()
-ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-best = float("inf")
-for _ in range(3):
-    ev[0].record()
-    for _ in range(ITERS):
+# PERSIST: flash_persist values to interleave (0 = one workgroup per item; n = the persistent
+# grid with n workgroups per CU), e.g. "0,2,3"
+for pv in [int(v) for v in os.environ.get("PERSIST", str(torch.ops.mlop.flash_persist(-1))).split(",")]:
+    torch.ops.mlop.flash_persist(pv)
+    for _ in range(3):
         ops.paged_attention(q, kc, vc, m, out=out)
-    ev[1].record()
-    ev[1].synchronize()
-    best = min(best, ev[0].elapsed_time(ev[1]) / ITERS * 1e3)
-line = dict(S=S, L=L, order=os.environ.get("ORDER", "lpt"), tiles=len(pts), us=round(best, 1), tflops=round(flops / best / 1e6, 1))
-if os.environ.get("CHECK"):
-    from mlopamd.ops import reference as ref
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    best = float("inf")
+    for _ in range(3):
+        ev[0].record()
+        for _ in range(ITERS):
+            ops.paged_attention(q, kc, vc, m, out=out)
+        ev[1].record()
+        ev[1].synchronize()
+        best = min(best, ev[0].elapsed_time(ev[1]) / ITERS * 1e3)
+    line = dict(S=S, L=L, order=os.environ.get("ORDER", "lpt"), persist=pv, tiles=len(pts), us=round(best, 1),
+                tflops=round(flops / best / 1e6, 1))
+    if os.environ.get("CHECK"):
+        from mlopamd.ops import reference as ref
 
-    exp = ref.paged_attention(q, kc, vc, m)
-    line["max_abs_err"] = (out.float() - exp.float()).abs().max().item()
-print(json.dumps(line), flush=True)
+        out.zero_()
+        ops.paged_attention(q, kc, vc, m, out=out)
+        exp = ref.paged_attention(q, kc, vc, m)
+        line["max_abs_err"] = (out.float() - exp.float()).abs().max().item()
+    print(json.dumps(line), flush=True)

@@ -32,7 +32,11 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3
 
 
-for M in [int(m) for m in os.environ.get("BENCH_MS", "512,1024,2048,3072,4096").split(",")]:
+# SLAB_NT: gemm_slab_nt values to interleave (e.g. "15,31": bit 4 = the RoPE epilogue's one-block
+# cos / sin lookahead of round 5)
+NTS = [int(v) for v in os.environ.get("SLAB_NT", str(torch.ops.mlop.gemm_slab_nt(-1))).split(",")]
+for M, nt in [(int(m), nt) for m in os.environ.get("BENCH_MS", "512,1024,2048,3072,4096").split(",") for nt in NTS]:
+    torch.ops.mlop.gemm_slab_nt(nt)
     NB = M // BS + 8
     x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
@@ -54,7 +58,7 @@ for M in [int(m) for m in os.environ.get("BENCH_MS", "512,1024,2048,3072,4096").
         tr.append(timeit(rope))
         tn.append(timeit(fused_ns))
         tp.append(timeit(plain))
-    print(json.dumps(dict(M=M, fused_us=round(min(tf), 1), hipblaslt_plus_rope_us=round(min(tu), 1),
+    print(json.dumps(dict(M=M, slab_nt=nt, fused_us=round(min(tf), 1), hipblaslt_plus_rope_us=round(min(tu), 1),
                           rope_cache_us=round(min(tr), 1), fused_noslots_us=round(min(tn), 1),
                           mlop_plain_us=round(min(tp), 1), speedup=round(min(tu) / min(tf), 2),
                           fused_tflops=round(2 * M * N * K / min(tf) / 1e6, 1))), flush=True)

@@ -164,13 +164,23 @@ def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shu
     return m, t
 
 
+@pytest.fixture(params=[0, 3 * 64], ids=["grid", "persist3"])
+def flash_persist(request):
+    """One workgroup per flash item, or the persistent grid forced to 3 slots per kv head (every
+    slot walks several boustrophedon rounds, a partial last one included)."""
+    prev = torch.ops.mlop.flash_persist(-1)
+    torch.ops.mlop.flash_persist(request.param)
+    yield request.param
+    torch.ops.mlop.flash_persist(prev)
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16), (32, 16), (16, 8)])
 @pytest.mark.parametrize("q_lens,ctx_lens", [
     ([1, 40, 200, 17], [1, 40, 200, 17]),            # fresh prompts, partial last tiles
     ([300, 1, 130], [1500, 700, 130]),               # chunked prefill continuing a context + a decode row
     ([1024], [1024]),                                # one long prompt (many causal tiles)
 ])
-def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens):
+def test_flash_prefill(gpu, Hq, Hkv, q_lens, ctx_lens, flash_persist):
     """K7 flash-prefill tiles (with the decode kernel on the short rows of the
     same launch) against the fp32 reference attention."""
     torch.manual_seed(0)
