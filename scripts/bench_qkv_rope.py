@@ -32,8 +32,8 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3
 
 
-# SLAB_NT: gemm_slab_nt values to interleave (e.g. "15,31": bit 4 = the RoPE epilogue's one-block
-# cos / sin lookahead of round 5)
+# SLAB_NT: gemm_slab_nt values to interleave (e.g. "15,7": bit 3 = the RoPE epilogue's q / K / V
+# stores non-temporal)
 NTS = [int(v) for v in os.environ.get("SLAB_NT", str(torch.ops.mlop.gemm_slab_nt(-1))).split(",")]
 for M, nt in [(int(m), nt) for m in os.environ.get("BENCH_MS", "512,1024,2048,3072,4096").split(",") for nt in NTS]:
     torch.ops.mlop.gemm_slab_nt(nt)
