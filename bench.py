@@ -110,8 +110,12 @@ def parse(argv=None):
     ap.add_argument("--tp-steps", type=int, default=10, help="timed engine steps of the TP phase")
     ap.add_argument("--tp-warmup", type=int, default=3)
     ap.add_argument("--tp-timeout", type=float, default=240.0,
-                    help="time limit of the TP phase (seconds): its child processes are stopped past it and the "
-                         "line carries tp.error, so a first-contact hang cannot eat the DP result")
+                    help="time limit of ONE phase (TP or EP; seconds): its child processes stop past it and the "
+                         "line carries tp.error / ep.error, so a first-contact hang cannot eat the DP result")
+    ap.add_argument("--phase-budget", type=float, default=240.0,
+                    help="wall-time budget of the TP and EP phases together (seconds): a phase gets at most "
+                         "what is left of it (a phase with < 30 s left is skipped and says so), so a hang in "
+                         "the first phase cannot push the whole command past the driver's time limit")
     ap.add_argument("--ep-phase", choices=("auto", "on", "off"), default="auto",
                     help="after the TP phase, a short EP = world phase of --ep-model (config 5: DP attention, every "
                          "MoE layer an expert exchange over IPC peer memory across the devices), with a greedy-token "
@@ -333,44 +337,49 @@ def main(argv=None):
     res = _report(a, rank, world, dev, float(gen), elapsed, ready_s, stats, deploy_info, engine, proc_ready)
     if a.tp == 1:
         engine.shutdown()
-    if _tp_phase_on(a, world):
-        # the driver's N-GPU command is DP replicas; on the same GPUs, a short TP = N phase then
-        # carries Llama-3 over RCCL + the K15 IPC all-reduce across the N devices (xGMI), with
-        # its own first-contact checks (runtime/bench_tp.py), reported as the line's "tp" block.
-        # It runs in CHILD processes (one per rank, their own process group): a first-contact
-        # failure there -- a hang, an abort, a GPU fault -- ends the child, never this process,
-        # which holds the DP result and prints the line either way
+    # the driver's N-GPU command is DP replicas; on the same GPUs, a short TP = N phase of Llama-3
+    # (RCCL + the K15 IPC all-reduce across the N devices, with its own first-contact checks,
+    # runtime/bench_tp.py) and an EP = N phase of Mixtral (the IPC expert exchange,
+    # runtime/bench_ep.py) follow, reported as the line's "tp" / "ep" blocks.  They run in CHILD
+    # processes (one per rank, their own process group): a first-contact failure there -- a hang,
+    # an abort, a GPU fault -- ends the child, never this process, which holds the DP result and
+    # prints the line either way
+    phases = [ph for ph, on in (("tp", _tp_phase_on(a, world)), ("ep", _ep_phase_on(a, world))) if on]
+    if phases:
+        import gc
+
         del engine
-        tp = _phase_children("tp", a, argv, rank, world, dev)
-        if res is not None:
-            res["tp"] = tp
-    if _ep_phase_on(a, world):
-        ep = _phase_children("ep", a, argv, rank, world, dev)
-        if res is not None:
-            res["ep"] = ep
+        gc.collect()
+        if dev.type == "cuda":  # the DP engines' memory back to the device for the children
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+        # the parents coordinate the phases over gloo (host only): a child that wedged the device
+        # must not be able to hang the parent that holds the DP result
+        coord = dist.new_group(backend="gloo") if world > 1 else None
+        deadline = time.perf_counter() + a.phase_budget
+        for ph in phases:
+            blk = _phase_children(ph, a, argv, rank, world, coord, deadline)
+            if res is not None:
+                res[ph] = blk
     _emit(res)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def _phase_children(phase: str, a, argv, rank: int, world: int, dev) -> dict | None:
+def _phase_children(phase: str, a, argv, rank: int, world: int, coord, deadline: float) -> dict | None:
     """Run ``runtime/bench_tp.tp_phase`` / ``runtime/bench_ep.ep_phase`` in one child process per
     rank (``--phase-child``), on a fresh rendezvous port, and collect rank 0's block from the
-    file its child writes.  Every parent waits at most ``--tp-timeout`` + 60 s for its child
-    (killed past it), then the parents meet at a barrier; a child that died leaves ``error``."""
-    import gc
+    file its child writes.  The phase gets min(``--tp-timeout``, what is left of
+    ``--phase-budget``): the children's watchdog fires 15 s before the parents kill them.  The
+    parents then meet at a barrier of ``coord`` (gloo); a child that died leaves ``error``."""
     import socket
     import subprocess
     import tempfile
 
     import torch.distributed as dist
 
-    gc.collect()
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-        torch.cuda.empty_cache()
-    box = [None, None]
+    box = [None, None, deadline]
     if rank == 0:
         with socket.socket() as s_:
             s_.bind(("127.0.0.1", 0))
@@ -378,25 +387,45 @@ def _phase_children(phase: str, a, argv, rank: int, world: int, dev) -> dict | N
         fd, box[1] = tempfile.mkstemp(prefix=f"mlop-{phase}-phase-", suffix=".json")
         os.close(fd)
     if world > 1:
-        dist.broadcast_object_list(box, src=0)
-    port, out_path = box
+        dist.broadcast_object_list(box, src=0, group=coord)
+    port, out_path, _ = box
+    left = deadline - time.perf_counter()
+    if world > 1:  # one verdict for the group (the clocks of the ranks differ slightly)
+        t = torch.tensor([left], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=coord)
+        left = float(t.item())
+    child_limit = min(a.tp_timeout, left - 15.0)  # the child's own watchdog (it writes its error)
+    limit = child_limit + 15.0                     # the parents kill it past this
+    if left < 30:
+        if rank == 0:
+            try:
+                os.unlink(out_path)
+            except OSError:
+                pass
+            return {phase: world, "error": f"skipped: {max(left, 0):.0f} s left of --phase-budget {a.phase_budget:.0f}"}
+        return None
     # the child is its own job: its own rendezvous (no torchrun agent store), same rank layout
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                LOCAL_RANK=os.environ.get("LOCAL_RANK", str(rank)), MLOP_TP_PHASE_OUT=out_path,
                HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase-child", phase]
+    # the child's own watchdog (--tp-timeout, the last occurrence wins) fires before the kill below
+    cmd = [sys.executable, os.path.abspath(__file__), *argv, "--phase-child", phase,
+           "--tp-timeout", f"{child_limit:.1f}"]
     t0 = time.perf_counter()
-    _progress(rank, f"{phase.upper()} = {world} phase in a child process (port {port})")
+    _progress(rank, f"{phase.upper()} = {world} phase in a child process (port {port}, limit {limit:.0f} s)")
     p = subprocess.Popen(cmd, env=env)
     try:
-        rc = p.wait(timeout=a.tp_timeout + 60)
+        rc = p.wait(timeout=limit)
     except subprocess.TimeoutExpired:
         p.kill()
-        rc = p.wait()
+        try:
+            rc = p.wait(timeout=20)
+        except subprocess.TimeoutExpired:  # unkillable (stuck in the driver): leave it, report it
+            rc = "unreaped"
         _progress(rank, f"{phase.upper()} phase child killed at its time limit")
     if world > 1:
-        dist.barrier()  # every child is gone before the parents go on
+        dist.barrier(group=coord)  # every child is gone (or given up on) before the parents go on
     if rank != 0:
         return None
     tp = None
@@ -415,6 +444,7 @@ def _phase_children(phase: str, a, argv, rank: int, world: int, dev) -> dict | N
         tp = {phase: world, "error": f"{phase.upper()} phase child exited with {rc} and no result"}
     tp["child_rc"] = rc
     tp["child_wall_s"] = round(time.perf_counter() - t0, 2)
+    tp["limit_s"] = round(limit, 1)
     return tp
 
 

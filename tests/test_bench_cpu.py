@@ -93,6 +93,15 @@ def test_bench_tp_phase_watchdog_keeps_the_dp_result():
     assert "tp-timeout" in d["tp"]["error"] and d["tp"]["child_rc"] == 3
 
 
+def test_bench_phase_budget_skips_what_does_not_fit():
+    """The TP and EP phases share ``--phase-budget``: a hang in the first cannot push the command
+    past the driver's limit.  With less than 30 s of budget, both say so and do not start."""
+    d = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cr-ready-samples", "0",
+              *ARGS, *TP_ARGS, "--phase-budget", "25"])
+    assert d["value"] > 0 and d["n_gpus"] == 2
+    assert d["tp"]["error"].startswith("skipped") and d["ep"]["error"].startswith("skipped")
+
+
 def test_bench_tp_phase_child_crash_keeps_the_dp_result():
     """A rank of the TP phase that dies outright (abort: what a GPU fault does to a process) ends
     only its child process: the DP ranks still print THE line, with tp.error, and exit 0."""
