@@ -151,11 +151,11 @@ class CustomAllReduce:
 
         Every rank generates every rank's input from a seed (rank r: seed 0x5EED + r), so the
         exact expected result is known locally without trusting any collective: the fp32 sum
-        in rank order rounded to bf16 -- what the kernels compute, bit for bit.  Checked:
-        one-shot (16 rows), two-shot (256 rows, above TWO_SHOT_MIN_BYTES), the one-shot
-        all-reduce + residual add, the broadcast and the all-gather; plus the process-group
-        all-reduce of the same inputs (fp32, within its own rounding) as a cross-check of the
-        fallback path itself.  ``inject_rank``: that rank perturbs its one-shot output (the
+        in rank order rounded to bf16 -- what the kernels compute, bit for bit.  Checked: the
+        process-group all-reduce of the one-shot inputs (fp32, within its own rounding; a
+        cross-check of the fallback path itself, run first), then one-shot (16 rows), two-shot
+        (256 rows, above TWO_SHOT_MIN_BYTES), the one-shot all-reduce + residual add, the
+        broadcast and the all-gather.  ``inject_rank``: that rank perturbs its one-shot output (the
         forced-corruption test, env ``MLOP_INJECT_CAR_CORRUPT``).  Returns this rank's
         verdict; ``agree`` makes it the group's."""
         dev, W = self.device, self.world
@@ -178,6 +178,19 @@ class CustomAllReduce:
         if self.init_error is not None:  # nothing to test: this rank never mapped its peers
             return {"ok": False, "checks": {}, "exception": self.init_error, "error_word": -1}
         try:
+            # the process-group path the fallback would use, FIRST: it is the only blocking
+            # collective here, so every rank reaches it even if a K15 call below raises on one
+            # rank (the K15 kernels' spins are bounded: the peers then see the error word and
+            # everyone meets again in ``agree``)
+            xs = inputs(rows["one_shot"], 0)
+            exp = oracle(xs)
+            pg = xs[self.rank].float()
+            if dist.is_initialized() and W > 1:
+                on_cpu = dist.get_backend(self.group) == "gloo"
+                t = pg.cpu() if on_cpu else pg
+                dist.all_reduce(t, group=self.group)
+                pg = t.to(dev)
+            res["checks"]["process_group"] = bool(torch.allclose(pg, exp, rtol=1e-5, atol=1e-5 * W))
             for salt, (name, n) in enumerate(rows.items()):
                 xs = inputs(n, salt)
                 out = torch.empty_like(xs[self.rank])
@@ -196,15 +209,6 @@ class CustomAllReduce:
                     res["checks"]["broadcast"] = bool(torch.equal(b, xs[0]))
                     ga = self.all_gather(xs[self.rank])
                     res["checks"]["all_gather"] = bool(torch.equal(ga, torch.stack(xs)))
-                    # the process-group path the fallback would use, on the same inputs
-                    pg = xs[self.rank].float()
-                    if dist.is_initialized() and W > 1:
-                        on_cpu = dist.get_backend(self.group) == "gloo"
-                        t = pg.cpu() if on_cpu else pg
-                        dist.all_reduce(t, group=self.group)
-                        pg = t.to(dev)
-                    res["checks"]["process_group"] = bool(
-                        torch.allclose(pg, exp, rtol=1e-5, atol=1e-5 * W))
             torch.cuda.synchronize(dev)
             res["error_word"] = self.error()
         except Exception as e:  # noqa: BLE001 - reported, the group falls back together
