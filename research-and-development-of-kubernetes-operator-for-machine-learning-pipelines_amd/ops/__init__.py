@@ -510,6 +510,10 @@ def norm_chain_ok(M: int, H: int, shapes, device=None, epis=None) -> bool:
                                   for (N, K), e in zip(shapes, epis))
     if device is not None and torch.device(device).type == "cuda":
         _sk_reserve(torch.device(device))
+    if M <= 64 and epis is not None:
+        # 5-64 rows: the planner's small tiles (O / down finish their split-K and leave the row
+        # sums of squares, gate_up / QKV scale their rows: gemm.hip mid_chain_ok)
+        return all(bool(torch.ops.mlop.mid_chain_ok(M, N, K, e)) for (N, K), e in zip(shapes, epis))
     return all(bool(torch.ops.mlop.w4_chain_ok(M, N, K)) for N, K in shapes)
 
 

@@ -357,6 +357,9 @@ bool gemm_res_ss(Tensor residual, Tensor a, Tensor w, Tensor ss_out) {
   re.ss_out = ss_out.data_ptr<float>();
   re.ss_tot = re.ss_out + M * (N / 128);
   c10::DeviceGuard g(a.device());
+  if (mlop::mid_chain_ok((int)M, (int)N, (int)K, 0))  // 5-64 rows: the planner's split-K tiles finish themselves
+    return mlop::launch_mid_res_ss(a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(),
+                                   (int)residual.stride(0), (int)M, (int)N, (int)K, re.ss_tot, cur_stream());
   return mlop::launch_w4_chain(4, a.data_ptr(), (int)a.stride(0), w.data_ptr(), residual.data_ptr(),
                                (int)residual.stride(0), (int)M, (int)N, (int)K, re, cur_stream());
 }
@@ -390,6 +393,9 @@ bool gemm_rs(Tensor out, Tensor a, Tensor w, Tensor ss_in, double eps, int64_t e
   re.ss_inv_k = 1.f / (float)K;
   re.ss_eps = (float)eps;
   c10::DeviceGuard g(a.device());
+  if (mlop::mid_chain_ok((int)M, (int)N, (int)K, (int)epi))  // 5-64 rows: the planner's SiLU tile, row-scaled
+    return mlop::launch_mid_rs(a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0),
+                               (int)M, (int)N, (int)K, re.ss_in, (float)eps, cur_stream());
   return mlop::launch_w4_chain((int)epi | 8, a.data_ptr(), (int)a.stride(0), w.data_ptr(), out.data_ptr(),
                                (int)out.stride(0), (int)M, (int)N, (int)K, re, cur_stream());
 }
@@ -427,10 +433,20 @@ bool gemm_rs_rope(Tensor q_out, Tensor k_cache, Tensor v_cache, Tensor a, Tensor
                       true, re, (float)eps, cur_stream());
     return true;
   }
-  if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
   re.ss_in = ss_in.data_ptr<float>() + M * (K / 128);
   re.ss_inv_k = 1.f / (float)K;
   re.ss_eps = (float)eps;
+  if (mlop::mid_chain_ok((int)M, (int)N, (int)K, 3)) {  // 5-64 rows
+    c10::DeviceGuard g(a.device());
+    if (mlop::ws_prefer((int)M, (int)N, (int)K, 3)) {  // row scale computed from the streamed rows
+      mlop::launch_ws(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)K, nullptr, 0, (int)M, (int)N, (int)K, 3,
+                      true, re, (float)eps, cur_stream());
+      return true;
+    }
+    return mlop::launch_gemm_rope(a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)M, (int)N, (int)K, re,
+                                  cur_stream());  // the slab path: row scale in the RoPE + cache reduce
+  }
+  if (!mlop::w4_chain_ok((int)M, (int)N, (int)K)) return false;
   c10::DeviceGuard g(a.device());
   return mlop::launch_w4_chain(3 | 8, a.data_ptr(), (int)a.stride(0), w.data_ptr(), nullptr, 0, (int)M, (int)N,
                                (int)K, re, cur_stream());
@@ -479,6 +495,10 @@ int64_t gemm_ws_max_m(int64_t set) { return mlop::gemm_ws_max_m((int)set); }
 void gemm_ws_plan(int64_t rb, int64_t u, int64_t nt) { mlop::gemm_ws_plan((int)rb, (int)u, (int)nt); }
 int64_t gemm_ws_small_m(int64_t set) { return mlop::gemm_ws_small_m((int)set); }
 int64_t flash_persist(int64_t set) { return mlop::flash_persist((int)set); }
+int64_t gemm_mid_chain(int64_t set) { return mlop::gemm_mid_chain((int)set); }
+bool mid_chain_ok(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return mlop::mid_chain_ok((int)M, (int)N, (int)K, (int)epi);
+}
 
 bool gemv_chain_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::decode_chain_takes((int)M, (int)N, (int)K, (int)epi);
@@ -866,6 +886,8 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_ws_plan(int rb, int u, int nt) -> ()", &gemm_ws_plan);
   m.def("gemm_ws_small_m(int set=-1) -> int", &gemm_ws_small_m);
   m.def("flash_persist(int set=-1) -> int", &flash_persist);
+  m.def("gemm_mid_chain(int set=-1) -> int", &gemm_mid_chain);
+  m.def("mid_chain_ok(int M, int N, int K, int epi) -> bool", &mid_chain_ok);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);
   m.def("gemm_grouped_plan(int bm, int bn, int stages, int splits) -> ()", &gemm_grouped_plan);
   m.def("gemm_dense_plan(int variant, int bm, int bn, int splits, int stages=0) -> ()", &gemm_dense_plan);

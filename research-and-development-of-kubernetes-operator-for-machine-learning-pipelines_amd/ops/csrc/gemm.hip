@@ -42,6 +42,7 @@ namespace mlop {
 enum { EPI_NONE = 0, EPI_SILU_MUL = 1, EPI_ROPE = 3 };
 constexpr int kBK = 64;
 constexpr int kStages = 3;
+constexpr int kMaxSplits = 8;  // plan(): split-K factors are at most 8
 
 // 16-B slot of chunk c in image row r is c ^ swz(r).  Two 128-B rows share one
 // 256-B bank row, so (r>>1)&7 (not r&7) makes the 16 rows of a ds_read_b128 lane
@@ -49,6 +50,141 @@ constexpr int kStages = 3;
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 
+
+// Mid-M norm chain (5-64 rows, launch_mid_res_ss): the O / down projection's split-K GEMM
+// finishes itself.  Every split stored its fp32 partial write-through (sc1), waited for it,
+// met its workgroup at a barrier, and one lane draws a relaxed agent-scope ticket on the
+// tile's counter; the split that draws the last ticket reads the partials with sc1 loads only
+// (re.mid_acq 0: MI355X_MICROARCH.md "Valid forms", sc1 stores, every storing wave's vmcnt(0)
+// and the workgroup barrier before the ONE lane's ticket, sc1 loads of every handed-off byte),
+// or with plain loads behind one agent acquire (re.mid_acq 1: attention.hip's split-KV combine
+// protocol, for kernels with several workgroups per CU), and
+//   * sums the tile's slabs in split order (splitk_add_rmsnorm's order and rounding: the
+//     residual comes out bit-identical to the unfused path), residual = bf16(res + bf16(y));
+//   * stores each row's sum of squares over the tile's BN columns (sc1) to the partials
+//     [M][gx] past the slabs, then draws the row band's ticket;
+// the band's last tile sums every row's partials in tile order into ss_tot[M], which the
+// consumers (gate_up / QKV) turn into their rows' RMSNorm factors.  Counters: [gx * gy) tiles,
+// then gy bands, re-armed by their last arriver.
+// buffer loads with a fixed cache policy (AUX 16: sc1)
+template <int AUX>
+__device__ __forceinline__ u32x4 ld_b128(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX));
+}
+template <int AUX>
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, AUX));
+}
+
+template <int BM, int BN, int T>
+__device__ __forceinline__ void mid_chain_finish(uint16_t* __restrict__ C, int ldc, float* __restrict__ ws, int M,
+                                                 int N, int m0, int n0, int rows_here, int bx, int by, int gx, int gy,
+                                                 int n_splits, const RopeEpi& re, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's partial stored (and its LDS ring reads retired: flag reuses it)
+  const int tid = threadIdx.x;
+  int* tcnt = re.ss_cnt + by * gx + bx;
+  if (tid == 0) flag[0] = __hip_atomic_fetch_add(tcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_splits - 1;
+  __syncthreads();
+  if (!flag[0]) return;
+  const bool acq = re.mid_acq != 0;
+  if (tid == 0) {
+    if (acq) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_store(tcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (acq) __syncthreads();
+  constexpr int VPR = BN / 8;  // 8-column vectors per tile row
+  constexpr int RPP = T / VPR;  // rows per pass
+  static_assert(T % VPR == 0 && VPR <= 64 && (VPR & (VPR - 1)) == 0, "row lanes");
+  float* ssp = ws + (size_t)n_splits * M * N;  // [M][gx] row partials
+  const auto rsS = __builtin_amdgcn_make_buffer_rsrc(ssp, 0, 0x7fffffff, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+  for (int r0 = 0; r0 < BM; r0 += RPP) {
+    const int r = r0 + tid / VPR, c = (tid % VPR) * 8;
+    const int m = m0 + r, n = n0 + c;
+    const bool ok = r < rows_here && n < N;
+    float ssq = 0.f;
+    if (ok) {
+      // every slab's two loads in flight together (a runtime-bound loop waits out one memory
+      // round trip per split), then summed in split order
+      u32x4 x[kMaxSplits], y[kMaxSplits];
+#pragma unroll
+      for (int sp = 0; sp < kMaxSplits; ++sp)
+        if (sp < n_splits) {
+          const uint32_t off = (uint32_t)((((size_t)sp * M + m) * N + n) * 4);
+          x[sp] = acq ? ld_b128<0>(rsW, off) : ld_b128<16>(rsW, off);
+          y[sp] = acq ? ld_b128<0>(rsW, off + 16u) : ld_b128<16>(rsW, off + 16u);
+        }
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sp = 0; sp < kMaxSplits; ++sp)
+        if (sp < n_splits) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] += __uint_as_float(x[sp][e]);
+            a[4 + e] += __uint_as_float(y[sp][e]);
+          }
+        }
+      uint16_t* rp = C + (size_t)m * ldc + n;
+      const u32x4 res = *reinterpret_cast<const u32x4*>(rp);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = pack2(bf2f(f2bf(a[2 * j])) + lo_bf(res[j]), bf2f(f2bf(a[2 * j + 1])) + hi_bf(res[j]));
+        const float h0 = lo_bf(o[j]), h1 = hi_bf(o[j]);
+        ssq += h0 * h0 + h1 * h1;
+      }
+      *reinterpret_cast<u32x4*>(rp) = o;
+    }
+#pragma unroll
+    for (int o2 = VPR / 2; o2 > 0; o2 >>= 1) ssq += __shfl_xor(ssq, o2);
+    if (ok && (tid % VPR) == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ssq), rsS, (uint32_t)(((size_t)m * gx + bx) * 4), 0,
+                                            16 /* sc1 */);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* bcnt = re.ss_cnt + gx * gy + by;
+  if (tid == 0) flag[1] = __hip_atomic_fetch_add(bcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gx - 1;
+  __syncthreads();
+  if (!flag[1]) return;
+  if (tid == 0) {
+    if (acq) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_store(bcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (acq) __syncthreads();
+  // row totals: L = T / BM lanes per row, each summing the partials b = l, l + L, ... (loads
+  // batched 8 at a time), then a fixed shuffle tree over the L lanes: deterministic, and no
+  // chain of gx dependent memory round trips
+  constexpr int L = T / BM >= 64 ? 64 : T / BM;
+  static_assert(L >= 1 && (L & (L - 1)) == 0, "lanes per row");
+  for (int r0 = 0; r0 < BM; r0 += T / L) {
+    const int r = r0 + tid / L, l = tid % L;
+    float sum = 0.f;
+    if (r < rows_here) {
+      const uint32_t row_off = (uint32_t)((size_t)(m0 + r) * gx * 4);
+      for (int b0 = l; b0 < gx; b0 += 8 * L) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int b = b0 + k * L;
+          v[k] = b >= gx ? 0.f : acq ? ld_f32<0>(rsS, row_off + (uint32_t)b * 4u) : ld_f32<16>(rsS, row_off + (uint32_t)b * 4u);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+      }
+    }
+#pragma unroll
+    for (int o2 = L / 2; o2 > 0; o2 >>= 1) sum += __shfl_xor(sum, o2);
+    if (r < rows_here && l == 0) re.ss_tot[m0 + r] = sum;
+  }
+}
 
 template <int BM, int BN, int WM, int WN, int EPI, bool GROUPED, int STAGES = 3, bool SETPRIO = false>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
@@ -179,8 +315,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
 
   const int rows_here = min(BM, m_end - m0);
   if (split) {
-    // split-K: fp32 partial slab [kz][M][N] (plain stores; reduce kernel in the next launch)
+    // split-K: fp32 partial slab [kz][M][N] (plain stores; reduce kernel in the next launch).
+    // Mid norm chain (re.ss_cnt set, launch_mid_res_ss): write-through (sc1) stores, then the
+    // last split of the tile finishes it in this launch (mid_chain_finish).
     float* P = ws + (size_t)bz * M * N;
+    const bool fix = !GROUPED && re.ss_cnt != nullptr;
+    const auto rsP = __builtin_amdgcn_make_buffer_rsrc(P, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -190,11 +330,18 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
         for (int r = 0; r < 4; ++r) {
           const int ml = wm * WTM + i * 16 + 4 * (lane >> 4) + r;
           if (ml < rows_here && n < N) {
-            if (re.ws_nt & 1) __builtin_nontemporal_store(acc[i][j][r], P + (size_t)(m0 + ml) * N + n);
+            if (fix)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rsP,
+                                                    (uint32_t)(((size_t)(m0 + ml) * N + n) * 4), 0, 16 /* sc1 */);
+            else if (re.ws_nt & 1) __builtin_nontemporal_store(acc[i][j][r], P + (size_t)(m0 + ml) * N + n);
             else P[(size_t)(m0 + ml) * N + n] = acc[i][j][r];
           }
         }
       }
+    if constexpr (!GROUPED) {
+      if (fix) mid_chain_finish<BM, BN, T>(C, ldc, ws, M, N, m0, n0, rows_here, bx, by, gx, m_tiles_y, n_splits, re,
+                                           reinterpret_cast<int*>(smem));
+    }
     return;
   }
   raw_barrier();  // every wave is done reading the ring before it becomes the C tile
@@ -239,11 +386,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(
         if (r >= rows_here || n0 + c0 + gcol >= N) continue;
         const float* g = sC + r * LDC + gcol;
         const float* u = g + 16;
+        // mid norm chain (re.ss_in: the producer's row totals): the row's RMSNorm factor scales
+        // the accumulators first (W4_RS's order)
+        const float f = re.ss_in != nullptr ? rsqrtf(re.ss_in[m0 + r] * re.ss_inv_k + re.ss_eps) : 1.f;
         u32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          o[j] = pack2(silu_bf(g[2 * j]) * bf2f(f2bf(u[2 * j])),
-                       silu_bf(g[2 * j + 1]) * bf2f(f2bf(u[2 * j + 1])));
+          o[j] = pack2(silu_bf(g[2 * j] * f) * bf2f(f2bf(u[2 * j] * f)),
+                       silu_bf(g[2 * j + 1] * f) * bf2f(f2bf(u[2 * j + 1] * f)));
         *reinterpret_cast<u32x4*>(C + (size_t)(m0 + r) * ldc + (n0 + c0) / 2 + j0) = o;
       }
     }
@@ -289,7 +439,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(uint16_t* __restrict
   }
 }
 
-constexpr int kMaxSplits = 8;  // plan(): split-K factors are at most 8
 // split-K reduce fused with the decoder's residual add + RMSNorm (one row per block):
 //   y = bf16(sum_s slab[s][r]);  residual[r] = bf16(residual[r] + y);  out[r] = rmsnorm(residual[r]) * w
 template <int VPT>
@@ -1418,6 +1567,77 @@ bool launch_w4_chain(int epi, const void* A, int lda, const void* B, void* C, in
   if (!w4_chain_ok(M, N, K) || !gemm_w4_ok(M, N, K, lda, K, ldc)) return false;
   const Plan p = plan(M, N, K, false, 0, 0);
   if (!run_w4(epi, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)C, ldc, M, N, K, st, re, p.BM)) return false;
+  return true;
+}
+
+// Mid-M norm chain (rows in (decode_chain_max_m, 64], TP = 1): the decoder layer's two add +
+// RMSNorm launches (splitk_add_rmsnorm) fold into the planner's small-tile GEMMs.  O / down
+// (epi 0) split K and the tile's last split adds into the residual and leaves the row sums of
+// squares (mid_chain_finish); gate_up (epi 1, one K range) scales its accumulator rows by the
+// RMSNorm factor in its SiLU epilogue; QKV + RoPE (epi 3) takes the factor in the split-K slab
+// reduce of the RoPE + cache kernel, or in the weight-streaming kernel's row-scale prologue at
+// 5-8 rows (which computes it from the rows it streams).
+// gemm_mid_chain op: 0 off (default), 1 on (sc1 hand-off), 2 on (acquire hand-off).  Off by
+// default: the in-kernel finish adds ~3.5 us to each O / down call (two ticket round trips,
+// write-through partials, the band's row totals) against the ~5 us splitk_add_rmsnorm launch it
+// replaces, and the row scale costs gate_up ~0.8 us; interleaved on one box, batch 16 -1 % /
+// -3 % and batch 64 -2.6 % / -3.7 % (sc1 / acquire); without the band step (a timing probe,
+// numerics off) batch 16 +2-3 % and batch 64 -0.6 % (profiles/r06_mid_chain.md).
+static int g_mid_chain = 0;
+int gemm_mid_chain(int set) {
+  if (set >= 0) g_mid_chain = set;
+  return g_mid_chain;
+}
+
+bool mid_chain_ok(int M, int N, int K, int epi) {
+  if (!g_mid_chain || M <= decode_chain_max_m() || M > 64 || K % kBK || N % 128) return false;
+  int cus = 0;
+  if (!gemm_sk_available(&cus)) return false;
+  if (epi == EPI_ROPE) {
+    if (ws_prefer(M, N, K, EPI_ROPE)) return K % 512 == 0;
+    const Plan p = rope_plan(M, N, K);
+    return !((p.BM == 256 || p.variant == 6) && p.BN >= 128) && rope_slabs_ok(p, M, N);
+  }
+  const Plan p = plan(M, N, K, false, 0, 0);
+  if (p.variant != 0 || p.BM > 64 || N % p.BN) return false;
+  if (epi == EPI_SILU_MUL) return p.splits == 1;
+  if (epi != EPI_NONE || p.splits < 2) return false;
+  const long gx = N / p.BN, gy = (M + p.BM - 1) / p.BM;
+  return gx * gy + gy <= kSkMaxWg &&
+         (size_t)p.splits * M * N + (size_t)M * gx <= (size_t)2 * kSkMaxWg * 256 * 256;
+}
+
+// residual [M, N] += A . B^T in place and ss_tot [M] <- the new rows' sums of squares (epi 0)
+bool launch_mid_res_ss(const void* A, int lda, const void* B, void* residual, int ldr, int M, int N, int K,
+                       float* ss_tot, hipStream_t st) {
+  if (M == 0) return true;
+  if (!mid_chain_ok(M, N, K, EPI_NONE)) return false;
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  int cus = 0;
+  if (!gemm_sk_scratch(&ws, &cnt, &cus)) return false;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  RopeEpi re{};
+  re.ss_cnt = cnt;
+  re.ss_tot = ss_tot;
+  re.mid_acq = g_mid_chain == 2;
+  launch_plan<EPI_NONE, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)residual, ldr, ws, M,
+                               N, K, nullptr, 0, st, re);
+  return true;
+}
+
+// out = SiLU-mul(diag(rsqrt(ss_tot / K + eps)) . A . B^T) (epi 1, gate_up)
+bool launch_mid_rs(const void* A, int lda, const void* B, void* out, int ldo, int M, int N, int K,
+                   const float* ss_tot, float eps, hipStream_t st) {
+  if (M == 0) return true;
+  if (!mid_chain_ok(M, N, K, EPI_SILU_MUL)) return false;
+  const Plan p = plan(M, N, K, false, 0, 0);
+  RopeEpi re{};
+  re.ss_in = ss_tot;
+  re.ss_inv_k = 1.f / (float)K;
+  re.ss_eps = eps;
+  launch_plan<EPI_SILU_MUL, false>(p, (const uint16_t*)A, lda, (const uint16_t*)B, K, (uint16_t*)out, ldo, nullptr,
+                                   M, N, K, nullptr, 0, st, re);
   return true;
 }
 

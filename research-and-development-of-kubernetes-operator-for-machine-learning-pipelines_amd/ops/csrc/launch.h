@@ -65,6 +65,9 @@ struct RopeEpi {
   // gemm_kernel: split-K slabs stored non-temporal (not left dirty in L2 for the kernel boundary's
   // write-back; MI355X_MICROARCH.md "boundary"); set by run_cfg (gemm_slab_nt)
   int ws_nt = 0;
+  // mid norm chain (gemm.hip mid_chain_finish): 1 = the finishing split reads the partials with
+  // plain loads behind one agent acquire, 0 = with sc1 loads only (gemm_mid_chain op 2 / 1)
+  int mid_acq = 0;
 };
 // RoPE + paged-cache stores from the QKV projection's fp32 split-K slabs ws[splits][T][N] (the
 // split-K reduce fused in: small-M launch_gemm_rope)
@@ -128,6 +131,15 @@ void gemm_ws_plan(int rb, int u, int nt);
 int gemm_ws_small_m(int set);
 // the plain (non-chain) decode projections this kernel takes instead of the planner
 bool ws_prefer(int M, int N, int K, int epi);
+// mid-M norm chain on the planner's small tiles (gemm.hip): epi 0 = O / down (split-K, the
+// last split adds into the residual and leaves the row sums of squares), 1 = gate_up (SiLU-mul,
+// row-scaled), 3 = QKV + RoPE (row-scaled slab reduce, or the ws kernel at 5-8 rows)
+int gemm_mid_chain(int set);
+bool mid_chain_ok(int M, int N, int K, int epi);
+bool launch_mid_res_ss(const void* A, int lda, const void* B, void* residual, int ldr, int M, int N, int K,
+                       float* ss_tot, hipStream_t st);
+bool launch_mid_rs(const void* A, int lda, const void* B, void* out, int ldo, int M, int N, int K,
+                   const float* ss_tot, float eps, hipStream_t st);
 // the decode norm chain's forms: the GEMV up to gemv_chain_max_m() rows, then the weight-
 // streaming MFMA kernel up to gemm_ws_max_m()
 int decode_chain_max_m();

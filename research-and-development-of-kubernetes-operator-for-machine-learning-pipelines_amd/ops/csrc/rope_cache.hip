@@ -17,9 +17,11 @@ namespace mlop {
 // SLABS: the input is the QKV projection's split-K partials instead of its bf16 output,
 // ws[s][T][qkv_stride] fp32: the 8 values of a vector are summed over the splits and rounded
 // to bf16 (splitk_reduce_kernel's order and rounding), so one launch replaces reduce + RoPE.
+// f: the row's RMSNorm factor of the mid norm chain (1 otherwise), applied to the summed
+// accumulators before the bf16 rounding (W4_RS's order)
 template <bool SLABS>
 __device__ __forceinline__ u32x4 load8(const uint16_t* row, const float* ws, int t, int T, int stride,
-                                       int splits, int col) {
+                                       int splits, int col, float f = 1.f) {
   if constexpr (!SLABS) {
     return *reinterpret_cast<const u32x4*>(row + col);
   } else {
@@ -32,7 +34,7 @@ __device__ __forceinline__ u32x4 load8(const uint16_t* row, const float* ws, int
     }
     u32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = pack2(a[2 * j], a[2 * j + 1]);
+    for (int j = 0; j < 4; ++j) o[j] = pack2(a[2 * j] * f, a[2 * j + 1] * f);
     return o;
   }
 }
@@ -42,8 +44,10 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const uint16_t* __restrict__ qkv, const int* __restrict__ pos, const float* __restrict__ cos_sin,
     const int* __restrict__ slots, int Hq, int Hkv, int D, int qkv_stride, int BS,
-    const float* __restrict__ ws = nullptr, int splits = 0) {
+    const float* __restrict__ ws = nullptr, int splits = 0, const float* __restrict__ ss_in = nullptr,
+    float ss_inv_k = 0.f, float ss_eps = 0.f) {
   const int t = blockIdx.x, T = gridDim.x;
+  const float f = SLABS && ss_in != nullptr ? rsqrtf(ss_in[t] * ss_inv_k + ss_eps) : 1.f;
   const int half = D >> 1;
   const int vph = half >> 3;  // 8-element vectors per half-head
   const int p = pos[t];
@@ -60,8 +64,8 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     if (it < n_rope) {
       const int h = it / vph, c = (it % vph) * 8;
       // q heads then k heads are contiguous
-      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + c);
-      u32x4 b = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + half + c);
+      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + c, f);
+      u32x4 b = load8<SLABS>(row, ws, t, T, qkv_stride, splits, h * D + half + c, f);
       const float4* cp = reinterpret_cast<const float4*>(cs + c);
       const float4* sp = reinterpret_cast<const float4*>(cs + half + c);
       float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
@@ -88,7 +92,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     } else if (slot >= 0) {
       const int iv = it - n_rope;
       const int kh = iv / (D >> 3), c = (iv % (D >> 3)) * 8;
-      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, (Hq + Hkv + kh) * D + c);
+      u32x4 a = load8<SLABS>(row, ws, t, T, qkv_stride, splits, (Hq + Hkv + kh) * D + c, f);
       *reinterpret_cast<u32x4*>(v_cache + (((size_t)blk * Hkv + kh) * BS + off) * D + c) = a;
     }
   }
@@ -112,7 +116,8 @@ void launch_rope_cache_slabs(const RopeEpi& re, const float* ws, int splits, int
   // scripts/r5_ropesplit.sh)
   const int by = std::min(2, (items + 255) / 256);
   rope_cache_kernel<true><<<dim3(T, by), 256, 0, st>>>(re.q_out, re.k_cache, re.v_cache, nullptr, re.pos, re.cos_sin,
-                                             re.slots, re.Hq, re.Hkv, 128, N, re.BS, ws, splits);
+                                             re.slots, re.Hq, re.Hkv, 128, N, re.BS, ws, splits, re.ss_in,
+                                             re.ss_inv_k, re.ss_eps);
 }
 
 }  // namespace mlop
