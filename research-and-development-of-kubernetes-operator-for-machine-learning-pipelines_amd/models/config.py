@@ -107,8 +107,13 @@ TINY_MIXTRAL = ModelConfig(
     name="tiny-mixtral", vocab_size=512, hidden_size=256, intermediate_size=256, num_layers=2,
     num_heads=4, num_kv_heads=1, max_position=2048, num_experts=4, top_k=2, eos_token_id=1)
 
+# CPU rehearsals of the 8-rank bench (bench.py --gpus 8 over gloo): 8 q heads so TP = 8 shards them
+# (the one kv head is replicated), 8 experts so EP = 8 gives every rank one
+TINY_LLAMA_8H = replace(TINY_LLAMA, name="tiny-llama-8h", num_heads=8)
+TINY_MIXTRAL_8E = replace(TINY_MIXTRAL, name="tiny-mixtral-8e", num_experts=8)
+
 PRESETS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, LLAMA31_8B, LLAMA31_70B, MIXTRAL_8X7B, TINY_LLAMA,
-                                TINY_MIXTRAL)}
+                                TINY_MIXTRAL, TINY_LLAMA_8H, TINY_MIXTRAL_8E)}
 # accepted aliases (MLflow tags / CR annotations use HF-ish names)
 ALIASES = {
     "meta-llama/Meta-Llama-3-8B": "llama3-8b", "llama-3-8b": "llama3-8b", "Llama-3-8B": "llama3-8b",
