@@ -494,6 +494,7 @@ bool gemm_ws(Tensor out, Tensor a, Tensor w, int64_t epi, bool rs, double eps) {
 int64_t gemm_ws_max_m(int64_t set) { return mlop::gemm_ws_max_m((int)set); }
 void gemm_ws_plan(int64_t rb, int64_t u, int64_t nt) { mlop::gemm_ws_plan((int)rb, (int)u, (int)nt); }
 int64_t gemm_ws_small_m(int64_t set) { return mlop::gemm_ws_small_m((int)set); }
+int64_t gemm_ws_rope_m(int64_t set) { return mlop::gemm_ws_rope_m((int)set); }
 int64_t flash_persist(int64_t set) { return mlop::flash_persist((int)set); }
 int64_t gemm_mid_chain(int64_t set) { return mlop::gemm_mid_chain((int)set); }
 bool mid_chain_ok(int64_t M, int64_t N, int64_t K, int64_t epi) {
@@ -885,6 +886,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("decode_chain_max_m() -> int", &decode_chain_max_m);
   m.def("gemm_ws_plan(int rb, int u, int nt) -> ()", &gemm_ws_plan);
   m.def("gemm_ws_small_m(int set=-1) -> int", &gemm_ws_small_m);
+  m.def("gemm_ws_rope_m(int set=-1) -> int", &gemm_ws_rope_m);
   m.def("flash_persist(int set=-1) -> int", &flash_persist);
   m.def("gemm_mid_chain(int set=-1) -> int", &gemm_mid_chain);
   m.def("mid_chain_ok(int M, int N, int K, int epi) -> bool", &mid_chain_ok);

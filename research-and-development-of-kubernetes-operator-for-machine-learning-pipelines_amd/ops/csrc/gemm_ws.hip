@@ -285,10 +285,18 @@ int gemm_ws_small_m(int set) {
   return g_ws_small_m;
 }
 
+// QKV + RoPE takes the weight-streaming kernel up to g_ws_rope_m rows (gemm_ws_rope_m op): it
+// replaces the planner's split-K tile AND the rope_cache slab-reduce launch after it
+int g_ws_rope_m = 8;
+int gemm_ws_rope_m(int set) {
+  if (set >= 0) g_ws_rope_m = set > 64 ? 64 : set;
+  return g_ws_rope_m;
+}
+
 bool ws_prefer(int M, int N, int K, int epi) {
-  if (M <= gemv_chain_max_m() || M > g_ws_small_m || (long)N * K > 32L * 1024 * 1024 || K % 512) return false;
-  if (epi == WS_ROPE) return N % 128 == 0;
-  return (epi == WS_NONE || epi == WS_RES) && N % 16 == 0;
+  if (M <= gemv_chain_max_m() || (long)N * K > 32L * 1024 * 1024 || K % 512) return false;
+  if (epi == WS_ROPE) return M <= g_ws_rope_m && N % 128 == 0;
+  return M <= g_ws_small_m && (epi == WS_NONE || epi == WS_RES) && N % 16 == 0;
 }
 
 void gemm_ws_plan(int rb, int u, int nt) {

@@ -129,6 +129,7 @@ bool ws_takes(int M, int N, int K, int epi);
 int gemm_ws_max_m(int set);
 void gemm_ws_plan(int rb, int u, int nt);
 int gemm_ws_small_m(int set);
+int gemm_ws_rope_m(int set);  // rows up to which QKV + RoPE takes the weight-streaming kernel
 // the plain (non-chain) decode projections this kernel takes instead of the planner
 bool ws_prefer(int M, int N, int K, int epi);
 // mid-M norm chain on the planner's small tiles (gemm.hip): epi 0 = O / down (split-K, the
