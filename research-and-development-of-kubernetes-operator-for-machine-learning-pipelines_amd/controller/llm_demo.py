@@ -30,12 +30,24 @@ FAULTS = {
     None: {},
     "latency": {"MLOP_INJECT_LATENCY_S": "0.25"},
     "errors": {"MLOP_INJECT_ERROR_RATE": "0.3"},
-    # device-only slowdown: every engine step of v2 also runs a 0.2 ms device delay kernel (a
-    # tiny-llama step is ~0.16 ms: TPOT x ~2), while the HTTP layer is untouched; the gate's
-    # latency thresholds are loosened for this case (GATES) so only the GPU-side TPOT guard can
-    # reject it (1.5 ms made p95 / mean 10x worse than v1: beyond any loosened latency bound)
+    # device-only slowdown: every engine step of v2 also runs a device delay kernel, while the
+    # HTTP layer is untouched; the gate's latency thresholds are loosened for this case (GATES)
+    # so only the GPU-side TPOT guard can reject it.  The delay scales with the model
+    # (_fault_env): 0.2 ms on the tiny shapes (a tiny-llama step is ~0.16 ms: TPOT x ~2; 1.5 ms
+    # made p95 / mean 10x worse than v1, beyond any loosened latency bound), 2 ms at real size
+    # (an 8B decode step at concurrency 16 is ~4.9 ms: 0.2 ms gave TPOT x 1.04-1.11 and the
+    # canary promoted)
     "tpot": {"MLOP_INJECT_STEP_DEVICE_US": "200"},
 }
+
+
+def _fault_env(regress: str | None, arch: str) -> dict:
+    env = dict(FAULTS[regress])
+    if regress == "tpot":
+        from ..models.config import get_config
+
+        env["MLOP_INJECT_STEP_DEVICE_US"] = "200" if get_config(arch).hidden_size <= 1024 else "2000"
+    return env
 
 # per-regression gate overrides: "tpot" keeps the TPOT guard at its 1.10 default and lets p95 /
 # mean latency rise 10x, i.e. the Seldon-executor latency gate alone would promote v2
@@ -87,7 +99,7 @@ async def run_llm_canary(arch: str = "tiny-llama", regress: str | None = None, d
     # time-shares its card between the two versions (both fit 288 GB)
     slots = gpu_slots or (1 if len(pool.devices) >= 2 else 2)
     pool.slots = slots
-    launcher = ProcessLauncher(scraper, extra_env=env, per_predictor_env={"v2": FAULTS[regress]}, gpus=pool)
+    launcher = ProcessLauncher(scraper, extra_env=env, per_predictor_env={"v2": _fault_env(regress, arch)}, gpus=pool)
     ctl = FakeSeldonController(kube, launcher, clock).start()
     router = Router(ctl)
     scraper.start()
