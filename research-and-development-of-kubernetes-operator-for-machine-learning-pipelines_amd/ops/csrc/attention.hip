@@ -728,6 +728,354 @@ __device__ __forceinline__ void flash32_item(
     }
 }
 
+// STREAM (flash_stream op): the persistent grid's tiles as ONE stream of K / V page pairs per
+// workgroup, so a tile's fixed cost hides under the previous tile's pairs (the 29 us fixed term
+// of profiles/r06_flash_persist.md):
+//   * the 3-deep LDS ring runs across tiles: while the last pairs of tile i are consumed, the
+//     first two pairs of tile i+1 (or i+2: one-pair tiles) are already being fetched;
+//   * tile i+1's Q rows arrive by LDS-DMA into a wave-private 8 KB while tile i runs, and are
+//     read into registers at tile i+1's start (80 KB of LDS: 2 workgroups per CU);
+//   * the loop is unrolled by the ring depth, so every step's stage is a constant (LDS read
+//     offsets in the instruction) and tile boundaries are a branch inside a step.
+// Every vector memory operation of a wave is counted (4 LDS-DMAs per pair, 8 Q DMAs per tile,
+// 16 O stores per tile: buffer stores, rows past the prompt dropped by the range check, so the
+// count never depends on the data), and a pair's wait is vmcnt(operations issued after its DMAs):
+// vmcnt(4) in the steady state.
+// Tiles per workgroup, boustrophedon order and the kv head per XCD as the PERSIST grid.
+//
+// s_waitcnt vmcnt(n) for a run-time n (a multiple of 4; rounded down, and capped at 60: waiting
+// for MORE retired operations than needed is always safe); n = 4 on the first compare
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  if (__builtin_expect(n == 4, 1)) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    return;
+  }
+  switch (n < 0 ? 0 : n > 60 ? 15 : n >> 2) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+  }
+}
+
+// item k of a persistent slot (boustrophedon rounds of S tiles), its causal extent in pairs and
+// pages; tile -1 past the end of the list
+struct FlashTile {
+  int tile, q0, ql, ctx, qs, n_pairs, n_pages, wg_min_pos, seq;
+};
+// metadata reads through the constant address space: scalar loads (the tables are not written
+// during the launch; as global pointers the loads after the first O store became vector loads,
+// each followed by a vmcnt(0) that drained the in-flight K / V ring)
+using cint_p = const __attribute__((address_space(4))) int*;
+__device__ __forceinline__ int ld_const(const int* p, int i) {
+  return ((cint_p)p)[__builtin_amdgcn_readfirstlane(i)];
+}
+template <int QB>
+__device__ __forceinline__ FlashTile flash_tile(int k, int slot, int S, int num_ptiles, const int* __restrict__ ptile_seq,
+                                                const int* __restrict__ ptile_q0, const int* __restrict__ q_start,
+                                                const int* __restrict__ q_len, const int* __restrict__ ctx_len) {
+  FlashTile it;
+  const int t = k * S + ((k & 1) ? S - 1 - slot : slot);
+  const bool ok = t < num_ptiles;
+  const int tt = ok ? t : num_ptiles - 1;  // loads stay in bounds; the fields are ignored past the end
+  it.tile = ok ? t : -1;
+  it.seq = ld_const(ptile_seq, tt);
+  it.q0 = ld_const(ptile_q0, tt);
+  it.ql = ld_const(q_len, it.seq);
+  it.ctx = ld_const(ctx_len, it.seq);
+  it.qs = ld_const(q_start, it.seq);
+  const int kv_end = it.ctx - it.ql + min(it.q0 + QB, it.ql);
+  it.n_pairs = (kv_end + 31) >> 5;
+  it.n_pages = (kv_end + kBS - 1) / kBS;
+  it.wg_min_pos = it.ctx - it.ql + it.q0;
+  return it;
+}
+
+template <int G>
+__global__ void __launch_bounds__(256, 2) flash32_stream_kernel(
+    uint16_t* __restrict__ out, const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ptile_seq, const int* __restrict__ ptile_q0,
+    const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, int Hq, int Hkv, float scale_log2, int num_blocks, int num_ptiles) {
+  constexpr int QB = 128 / G;
+  constexpr int STAGE = 4 * kBS * kD;  // bf16 per stage: K page A | K page B | V page A | V page B
+  constexpr int PAGE = kBS * kD;
+  constexpr int QW = 32 * kD;  // bf16 of one wave's 32 Q rows
+  __shared__ __attribute__((aligned(256))) uint16_t smem[3 * STAGE + 4 * QW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5, R = 32 * wid + col;
+  const int kvh = blockIdx.x % Hkv, slot = blockIdx.x / Hkv, S = gridDim.x / Hkv;
+  const size_t page_stride = (size_t)Hkv * PAGE;
+  const int kkey = wid * 4 + (lane >> 4);
+  const int k_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ (kkey & 15)) << 3);
+  const int v_off = kvh * PAGE + kkey * kD + (((lane & 15) ^ vswz(kkey)) << 3);
+#define MLOP_FT(k) flash_tile<QB>((k), slot, S, num_ptiles, ptile_seq, ptile_q0, q_start, q_len, ctx_len)
+
+  FlashTile cur = MLOP_FT(0);
+  if (cur.tile < 0) return;  // the whole workgroup, before any barrier
+
+  // the issue pointer of the pair stream: item iss_k, its next pair iss_p, whose pages pA / pB
+  // were looked up one issue ahead.  vm = vector memory operations this wave has issued; markS
+  // = vm right after the DMAs of the pair in ring stage S.  Pair n goes to stage n % 3 and is
+  // consumed by the loop's step n % 3.
+  FlashTile iss = cur;
+  int iss_k = 0, iss_p = 0, vm = 0, mark0 = 0, mark1 = 0, mark2 = 0;
+  const int* iss_bt = block_tables + (size_t)iss.seq * bt_stride;
+  int pA = min(max(ld_const(iss_bt, 0), 0), num_blocks - 1);
+  int pB = iss.n_pages > 1 ? min(max(ld_const(iss_bt, 1), 0), num_blocks - 1) : pA;
+  auto issue_next = [&](auto st_tag) __attribute__((always_inline)) {
+    constexpr int ST = decltype(st_tag)::value;
+    if (iss.tile < 0) return;
+    uint16_t* base = smem + ST * STAGE + wid * 512;
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pA * page_stride + k_off), (lds_void_t*)(base), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(kc + pB * page_stride + k_off), (lds_void_t*)(base + PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vc + pA * page_stride + v_off), (lds_void_t*)(base + 2 * PAGE), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vc + pB * page_stride + v_off), (lds_void_t*)(base + 3 * PAGE), 16, 0, 0);
+    vm += 4;
+    if constexpr (ST == 0) mark0 = vm;
+    else if constexpr (ST == 1) mark1 = vm;
+    else mark2 = vm;
+    if (++iss_p >= iss.n_pairs) {  // every item has >= 1 pair
+      iss = MLOP_FT(++iss_k);
+      iss_p = 0;
+      iss_bt = block_tables + (size_t)iss.seq * bt_stride;
+    }
+    if (iss.tile >= 0) {
+      const int a = 2 * iss_p, b = a + 1 < iss.n_pages ? a + 1 : a;
+      pA = min(max(ld_const(iss_bt, a), 0), num_blocks - 1);
+      pB = min(max(ld_const(iss_bt, b), 0), num_blocks - 1);
+    }
+  };
+  // the next tile's Q rows by LDS-DMA into this wave's private 8 KB (the compiler neither
+  // tracks nor copies them: as register loads its own wait for them became a vmcnt(0) that
+  // drained the ring at every tile start).  DMA t writes 1 KB, lane L's 16 B at 16 L: row
+  // 32 wid + (L & 31), dims 16 t + 8 (L >> 5) -- fragment t of lane L, read back linearly.
+  uint16_t* const q_lds = smem + 3 * STAGE + wid * QW;
+  int markQ = 0;
+  auto q_issue = [&](const FlashTile& it) __attribute__((always_inline)) {
+    const int qi = it.q0 + R / G;
+    const uint16_t* qrow = q + ((size_t)(it.qs + (qi < it.ql ? qi : 0)) * Hq + kvh * G + R % G) * kD + 8 * h;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      __builtin_amdgcn_global_load_lds((const void*)(qrow + 16 * t), (lds_void_t*)(q_lds + t * 512), 16, 0, 0);
+    vm += 8;
+    markQ = vm;
+  };
+  const uint32_t q_b0 = (uint32_t)(uintptr_t)q_lds + 16u * lane;
+  const int k15 = col & 15;
+  const uint32_t k_b0 = (uint32_t)(uintptr_t)smem + (uint32_t)((col >> 4) * PAGE * 2 + k15 * 256 + ((h ^ k15) << 4));
+  const uint32_t v_b0 = (uint32_t)(uintptr_t)smem + 2 * PAGE * 2 + vt32_base(lane);
+  // the O stores' range: every valid row below 2 GB (checked on the host), masked rows at 2 GB
+  const auto rsO = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+
+  // per-tile state: this lane's q row, its Q fragments, the accumulators
+  int qi = 0, pos_r = -1, pp = 0, k = 0;
+  bool q_ok = false;
+  bf16x8 qf[8];
+  f32x16 o[4];
+  float m = kNegBig, l = 0.f;
+  auto tile_start = [&]() __attribute__((always_inline)) {
+    qi = cur.q0 + R / G;
+    q_ok = qi < cur.ql;
+    pos_r = q_ok ? cur.ctx - cur.ql + qi : -1;
+    wait_vmcnt_rt(vm - markQ);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile(
+        "ds_read_b128 %0, %8\n"
+        "ds_read_b128 %1, %8 offset:1024\n"
+        "ds_read_b128 %2, %8 offset:2048\n"
+        "ds_read_b128 %3, %8 offset:3072\n"
+        "ds_read_b128 %4, %8 offset:4096\n"
+        "ds_read_b128 %5, %8 offset:5120\n"
+        "ds_read_b128 %6, %8 offset:6144\n"
+        "ds_read_b128 %7, %8 offset:7168\n"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(qf[0]), "=&v"(qf[1]), "=&v"(qf[2]), "=&v"(qf[3]), "=&v"(qf[4]), "=&v"(qf[5]), "=&v"(qf[6]),
+          "=&v"(qf[7])
+        : "v"(q_b0));
+    if (!q_ok) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) qf[t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
+    m = kNegBig;
+    l = 0.f;
+    pp = 0;
+  };
+  // epilogue: 16 buffer stores per lane, always issued (masked rows go past the range)
+  auto tile_end = [&]() __attribute__((always_inline)) {
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const uint32_t obase =
+        q_ok ? (uint32_t)((((size_t)(cur.qs + qi) * Hq + kvh * G + R % G) * kD + 4 * h) * 2) : 0x80000000u;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        u32x2 v;
+        v[0] = pack2(o[d][4 * b] * inv, o[d][4 * b + 1] * inv);
+        v[1] = pack2(o[d][4 * b + 2] * inv, o[d][4 * b + 3] * inv);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rsO, obase + (uint32_t)(32 * d + 8 * b) * 2u, 0, 0);
+      }
+    vm += 16;
+    asm volatile("" ::: "memory");
+  };
+
+  // one stream step: consume the pair in ring stage ST (true: the stream has ended)
+  FlashTile nxt;
+  auto step = [&](auto st_tag) __attribute__((always_inline)) -> bool {
+    constexpr int ST = decltype(st_tag)::value;
+    constexpr uint32_t so = (uint32_t)(ST * STAGE * 2);
+    wait_vmcnt_rt(vm - (ST == 0 ? mark0 : ST == 1 ? mark1 : mark2));
+    raw_barrier();  // pair visible to every wave; the stage consumed one step ago is free
+    issue_next(std::integral_constant<int, (ST + 2) % 3>{});
+    if (pp == 0 && nxt.tile >= 0) q_issue(nxt);  // the next tile's Q under this tile's pairs
+    // S^T = K . Q^T of this pair (flash32_item's qk)
+    f32x16 sc;
+    {
+      uint32_t kb = k_b0;
+      asm volatile("" : "+v"(kb));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sc[e] = 0.f;
+      bf16x8 kf[4];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[t]) : "v"(kb ^ (32u * t)), "n"(so));
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        bf16x8& f = kf[t & 3];
+        if (t <= 4) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(f));
+        else if (t == 5) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f));
+        else if (t == 6) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(f));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f));
+        sc = mfma32(f, qf[t], sc);
+        if (t + 4 < 8)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[t & 3]) : "v"(kb ^ (32u * (t + 4))), "n"(so));
+      }
+    }
+    // online softmax (flash32_item's, deferred rescale)
+    bf16x8 pf[2];
+    {
+      if (pp * 32 + 31 > cur.wg_min_pos) {
+        asm volatile("");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int tok = pp * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          sc[r] = tok <= pos_r ? sc[r] : -INFINITY;
+        }
+      }
+      float mx = fmaxf(fmaxf(sc[0], sc[1]), sc[2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+      mx = fmaxf(mx, sc[15]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      if (__ballot((mx - m) * scale_log2 > kRescaleLog2)) {
+        const float m_new = fmaxf(m, mx);
+        const float alpha = fast_exp2((m - m_new) * scale_log2);
+        m = m_new;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] *= alpha;
+        l *= alpha;
+      }
+      const float mc = -m * scale_log2;
+      float rs = 0.f;
+      u32x4 w[2];
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float p0 = fast_exp2(fmaf(sc[r], scale_log2, mc)), p1 = fast_exp2(fmaf(sc[r + 1], scale_log2, mc));
+        rs += p0 + p1;
+        w[r >> 3][(r & 7) >> 1] = cvt_pk_bf16(p0, p1);
+      }
+      pf[0] = __builtin_bit_cast(bf16x8, w[0]);
+      pf[1] = __builtin_bit_cast(bf16x8, w[1]);
+      l += rs;
+    }
+    // O^T += V^T . P^T (flash32_item's pv)
+    {
+      uint32_t vb = v_b0;
+      asm volatile("" : "+v"(vb));
+      v4s16 ra[4], rb[4];
+#define MLOP_VT_ISSUE(dblk, r)                                                              \
+  {                                                                                         \
+    const uint32_t a0 = vb ^ (64u * (dblk)), a1 = a0 ^ 32u;                                 \
+    asm volatile(                                                                           \
+        "ds_read_b64_tr_b16 %0, %4 offset:%6\n"                                             \
+        "ds_read_b64_tr_b16 %1, %5 offset:%7\n"                                             \
+        "ds_read_b64_tr_b16 %2, %4 offset:%8\n"                                             \
+        "ds_read_b64_tr_b16 %3, %5 offset:%9\n"                                             \
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])                                \
+        : "v"(a0), "v"(a1), "n"(so), "n"(so + 2048u), "n"(so + 4096u), "n"(so + 6144u));  \
+  }
+      MLOP_VT_ISSUE(0, ra)
+#pragma unroll
+      for (int dblk = 0; dblk < 4; ++dblk) {
+        v4s16 (&cv)[4] = (dblk & 1) ? rb : ra;
+        v4s16 (&nv)[4] = (dblk & 1) ? ra : rb;
+        if (dblk < 3) {
+          MLOP_VT_ISSUE(dblk + 1, nv)
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(cv[0]), "+v"(cv[1]), "+v"(cv[2]), "+v"(cv[3]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cv[0]), "+v"(cv[1]), "+v"(cv[2]), "+v"(cv[3]));
+        }
+        bf16x8 f0, f1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          f0[e] = cv[0][e];
+          f0[4 + e] = cv[1][e];
+          f1[e] = cv[2][e];
+          f1[4 + e] = cv[3][e];
+        }
+        o[dblk] = mfma32(f0, pf[0], o[dblk]);
+        o[dblk] = mfma32(f1, pf[1], o[dblk]);
+      }
+#undef MLOP_VT_ISSUE
+    }
+    if (++pp < cur.n_pairs) return false;
+    tile_end();
+    if (nxt.tile < 0) return true;
+    cur = nxt;
+    nxt = MLOP_FT(++k + 1);
+    tile_start();
+    return false;
+  };
+
+  q_issue(cur);
+  issue_next(std::integral_constant<int, 0>{});
+  issue_next(std::integral_constant<int, 1>{});
+  nxt = MLOP_FT(1);
+  tile_start();
+  for (;;) {
+    if (step(std::integral_constant<int, 0>{})) break;
+    if (step(std::integral_constant<int, 1>{})) break;
+    if (step(std::integral_constant<int, 2>{})) break;
+  }
+#undef MLOP_FT
+}
+
 // PERSIST: a persistent grid of S x Hkv workgroups (S slots per kv head; blockIdx % Hkv = kv
 // head, so each head stays on one XCD as in the one-item grid) walks the tile list in rounds of
 // S tiles, boustrophedon: slot j takes tile r S + j in even rounds and r S + S - 1 - j in odd
@@ -770,6 +1118,14 @@ int flash_persist(int set) {
   return g_flash_persist;
 }
 
+// flash_stream op: 1 = the persistent grid runs flash32_stream_kernel (cross-tile K / V ring and
+// Q prefetch, 2 workgroups per CU) instead of flash32_item per tile; 0 = off
+static int g_flash_stream = 0;
+int flash_stream(int set) {
+  if (set >= 0) g_flash_stream = set;
+  return g_flash_stream;
+}
+
 static int device_cus() {
   static int cus[16] = {};
   int dev = 0;
@@ -788,9 +1144,14 @@ void launch_flash_prefill(void* out, const void* q, const void* kc, const void* 
                     : g_flash_persist > 0 ? std::max(1, g_flash_persist * device_cus() / Hkv) : 0;
   const bool persist = slots > 0 && num_ptiles > slots;
   dim3 grid((persist ? slots : num_ptiles) * Hkv);
+  const bool stream = persist && g_flash_stream;
 #define MLOP_FLASH_CASE(GG)                                                                              \
   case GG:                                                                                               \
-    if (persist)                                                                                         \
+    if (stream)                                                                                          \
+      flash32_stream_kernel<GG><<<grid, 256, 0, st>>>(                                                   \
+          (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt, bt_stride,   \
+          ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks, num_ptiles);    \
+    else if (persist)                                                                                    \
       flash32_prefill_kernel<GG, 2, true><<<grid, 256, 0, st>>>(                                         \
           (uint16_t*)out, (const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, bt, bt_stride,   \
           ptile_seq, ptile_q0, q_start, q_len, ctx_len, Hq, Hkv, scale_log2, num_blocks, num_ptiles);    \

@@ -126,6 +126,8 @@ void flash_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor 
   TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "flash prefill: GQA group must be 1, 2, 4 or 8");
   TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
   TORCH_CHECK(ptile_seq.numel() == ptile_q0.numel(), "tile arrays");
+  // the stream kernel's O stores range-check at 2 GB (masked rows are stored past it)
+  TORCH_CHECK(!mlop::flash_stream(-1) || out.numel() * 2 < (int64_t)0x7fffff00, "flash_stream: output >= 2 GB");
   TORCH_CHECK(q_start.numel() == q_len.numel() && q_len.numel() == ctx_len.numel() &&
                   block_tables.size(0) >= q_len.numel(),
               "per-sequence arrays");
@@ -496,6 +498,7 @@ void gemm_ws_plan(int64_t rb, int64_t u, int64_t nt) { mlop::gemm_ws_plan((int)r
 int64_t gemm_ws_small_m(int64_t set) { return mlop::gemm_ws_small_m((int)set); }
 int64_t gemm_ws_rope_m(int64_t set) { return mlop::gemm_ws_rope_m((int)set); }
 int64_t flash_persist(int64_t set) { return mlop::flash_persist((int)set); }
+int64_t flash_stream(int64_t set) { return mlop::flash_stream((int)set); }
 int64_t gemm_mid_chain(int64_t set) { return mlop::gemm_mid_chain((int)set); }
 bool mid_chain_ok(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::mid_chain_ok((int)M, (int)N, (int)K, (int)epi);
@@ -888,6 +891,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("gemm_ws_small_m(int set=-1) -> int", &gemm_ws_small_m);
   m.def("gemm_ws_rope_m(int set=-1) -> int", &gemm_ws_rope_m);
   m.def("flash_persist(int set=-1) -> int", &flash_persist);
+  m.def("flash_stream(int set=-1) -> int", &flash_stream);
   m.def("gemm_mid_chain(int set=-1) -> int", &gemm_mid_chain);
   m.def("mid_chain_ok(int M, int N, int K, int epi) -> bool", &mid_chain_ok);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);

@@ -56,9 +56,12 @@ q = torch.randn(S * L, Hq, D, device=dev, dtype=bf)
 out = torch.empty_like(q)
 flops = 4 * S * (L * (L + 1) // 2) * D * Hq
 # PERSIST: flash_persist values to interleave (0 = one workgroup per item; n = the persistent
-# grid with n workgroups per CU), e.g. "0,2,3"
-for pv in [int(v) for v in os.environ.get("PERSIST", str(torch.ops.mlop.flash_persist(-1))).split(",")]:
+# grid with n workgroups per CU; an "s" suffix runs it as the cross-tile stream, flash_stream 1),
+# e.g. "0,3,2s"
+for pvs in os.environ.get("PERSIST", str(torch.ops.mlop.flash_persist(-1))).split(","):
+    pv = int(pvs.rstrip("s"))
     torch.ops.mlop.flash_persist(pv)
+    torch.ops.mlop.flash_stream(1 if pvs.endswith("s") else 0)
     for _ in range(3):
         ops.paged_attention(q, kc, vc, m, out=out)
     torch.cuda.synchronize()
@@ -71,7 +74,7 @@ for pv in [int(v) for v in os.environ.get("PERSIST", str(torch.ops.mlop.flash_pe
         ev[1].record()
         ev[1].synchronize()
         best = min(best, ev[0].elapsed_time(ev[1]) / ITERS * 1e3)
-    line = dict(S=S, L=L, order=os.environ.get("ORDER", "lpt"), persist=pv, tiles=len(pts), us=round(best, 1),
+    line = dict(S=S, L=L, order=os.environ.get("ORDER", "lpt"), persist=pvs, tiles=len(pts), us=round(best, 1),
                 tflops=round(flops / best / 1e6, 1))
     if os.environ.get("CHECK"):
         from mlopamd.ops import reference as ref

@@ -164,14 +164,19 @@ def make_meta(gpu, q_lens, ctx_lens, Hkv, G, NB, part_tokens=None, nparts=1, shu
     return m, t
 
 
-@pytest.fixture(params=[0, 3 * 64], ids=["grid", "persist3"])
+@pytest.fixture(params=[(0, 0), (3 * 64, 0), (3 * 64, 1), (64, 1)], ids=["grid", "persist3", "stream3", "stream1"])
 def flash_persist(request):
     """One workgroup per flash item, or the persistent grid forced to 3 slots per kv head (every
-    slot walks several boustrophedon rounds, a partial last one included)."""
-    prev = torch.ops.mlop.flash_persist(-1)
-    torch.ops.mlop.flash_persist(request.param)
+    slot walks several boustrophedon rounds, a partial last one included), per tile or as one
+    cross-tile stream of K / V pairs and Q (flash_stream); stream1: ONE slot per kv head streams
+    every tile of the launch, one-pair tiles included."""
+    persist, stream = request.param
+    prev, prev_s = torch.ops.mlop.flash_persist(-1), torch.ops.mlop.flash_stream(-1)
+    torch.ops.mlop.flash_persist(persist)
+    torch.ops.mlop.flash_stream(stream)
     yield request.param
     torch.ops.mlop.flash_persist(prev)
+    torch.ops.mlop.flash_stream(prev_s)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16), (32, 16), (16, 8)])
