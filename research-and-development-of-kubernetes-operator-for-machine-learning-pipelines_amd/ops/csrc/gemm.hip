@@ -681,6 +681,7 @@ struct SkArgs {
   int cus;      // CUs the split was planned for
   int min_half; // shortest K-range (K-tiles) the planner may cut
   int skip_dead;  // 1: quadrants past the last row issue no MFMAs (MLOP_GEMM_SKIP_DEAD=0: A/B)
+  int balance;    // grouped: an expert over c > 1 m-tiles gets c EQUAL row ranges (gemm_grouped_balance)
 };
 
 // d for the r = T % cus tail tiles of a T-tile launch: each is cut into d equal K-ranges
@@ -778,11 +779,29 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
         if (slot < before + c) break;
         before += c;
       }
-      m0 = offsets[e] + (slot - before) * BM;
+      const int rows_e = offsets[e + 1] - offsets[e], c = (rows_e + BM - 1) / BM, k = slot - before;
+      if (sk.balance && c > 1) {
+        // c near-equal row ranges instead of c - 1 full tiles + a spill tile: the tiles of one
+        // (expert, n-tile) then do near-equal work, stay in step on one XCD (adjacent lids) and
+        // share each B K-tile through L2; a 257-row expert was 256 + 1 rows, the spill tile a
+        // whole second walk of the B panel at HBM rate (profiles/r06_moe_spill.md).  Inner
+        // boundaries sit on 64-row quadrants (the fewest MFMA quadrants, ceil(rows / 64)), each
+        // tile at most BM rows.
+        auto bnd = [&](int kk) {
+          if (kk >= c) return rows_e;
+          int b = 64 * (int)(((long)kk * rows_e + 32L * c) / (64L * c));
+          b = min(b, BM * kk);
+          return max(b, rows_e - BM * (c - kk));
+        };
+        m0 = offsets[e] + (k > 0 ? bnd(k) : 0);
+        m_end = offsets[e] + bnd(k + 1);
+      } else {
+        m0 = offsets[e] + k * BM;
+        m_end = offsets[e + 1];
+      }
       n0 = (lid / S) * BN;
-      m_end = offsets[e + 1];
       Bg = B + (size_t)e * N * ldb;
-      b_once = offsets[e + 1] - offsets[e] <= BM;
+      b_once = rows_e <= BM;
     } else {
       const int band = lid / (group_m * n_tiles_x), in_band = lid % (group_m * n_tiles_x);
       const int gm_here = min(group_m, m_tiles - band * group_m);
@@ -1091,6 +1110,14 @@ static SkBuf g_sk[16];
 static int g_sk_mode = 1;
 static const int g_sk_min_iters = 16;
 static const int g_skip_dead = 1;
+// gemm_grouped_balance op (1, default): quadrant-aligned equal row ranges for an expert over
+// several m-tiles; 8 x 257 rows gate_up 677 -> 639 us, down 353 -> 308, real decode routing
+// -0.3 to -5 %, Mixtral batch 1024 +0.75 % (profiles/r06_moe_spill.md)
+static int g_grouped_balance = 1;
+int gemm_grouped_balance(int set) {
+  if (set >= 0) g_grouped_balance = set;
+  return g_grouped_balance;
+}
 
 int gemm_sk_mode(int set) {
   if (set >= 0) g_sk_mode = set;
@@ -1211,7 +1238,7 @@ static void run_pp(const uint16_t* A, int lda, const uint16_t* B, int ldb, uint1
     // split from offsets[] with the same sk_choose_d and idles the blocks it does not need
     SkBuf* b = sk_buf();
     const int T_max = gx * gy;
-    sk = SkArgs{T_max, T_max, 1, 0, nullptr, nullptr, T_max, 256, sk_min_half(), g_skip_dead};
+    sk = SkArgs{T_max, T_max, 1, 0, nullptr, nullptr, T_max, 256, sk_min_half(), g_skip_dead, g_grouped_balance};
     if (b) {
       sk.ws = b->ws;
       sk.cnt = b->cnt + (size_t)(b->next++ % kCntRegions) * kSkMaxWg;

@@ -36,8 +36,8 @@ CANDIDATES = {
     "mid": [("auto", -1, -1, -1, -1), ("128x64", 128, 64, -1, -1), ("64x64/s6", 64, 64, 6, -1),
             ("64x64/s3", 64, 64, 3, -1), ("256x128", 256, 128, -1, 1), ("256x64", 256, 64, -1, 1),
             ("256x256", 256, 256, -1, 1)],
-    "large": [("auto", -1, -1, -1, -1), ("256x128", 256, 128, -1, 1), ("256x64", 256, 64, -1, 1),
-              ("128x64", 128, 64, -1, 1), ("256x256", 256, 256, -1, 1)],
+    "large": [("auto", -1, -1, -1, -1), ("auto+bal", -1, -1, -1, -1), ("256x128", 256, 128, -1, 1),
+              ("256x64", 256, 64, -1, 1), ("128x64", 128, 64, -1, 1), ("256x256", 256, 256, -1, 1)],
 }
 
 
@@ -66,6 +66,7 @@ def main():
     dev = torch.device("cuda")
     bf = torch.bfloat16
     ops._sk_reserve(dev)
+    bal_default = torch.ops.mlop.gemm_grouped_balance(-1)
     rng = np.random.default_rng(0)
     shapes = (("gate_up", 28672, 4096, 1), ("down", 4096, 14336, 0))
     ws = {name: (0.02 * torch.randn(E, N, K, device=dev)).to(bf) for name, N, K, _ in shapes}
@@ -83,6 +84,8 @@ def main():
             for _ in range(2):  # interleaved rounds
                 for label, bm, bn, st, sp in CANDIDATES[group]:
                     torch.ops.mlop.gemm_grouped_plan(bm, bn, st, sp)
+                    # "+bal": equal row ranges per expert m-tile (gemm_grouped_balance)
+                    torch.ops.mlop.gemm_grouped_balance(1 if label.endswith("+bal") else 0)
                     try:
                         y = ops.grouped_gemm(x, w, off, epi=epi, avg_rows=rows // E)
                         if ref is None:
@@ -95,6 +98,7 @@ def main():
                     if label not in best or (best[label][0] is not None and t < best[label][0]):
                         best[label] = (t, err)
             torch.ops.mlop.gemm_grouped_plan(-1, -1, -1, -1)
+            torch.ops.mlop.gemm_grouped_balance(bal_default)
             wbytes = int((counts > 0).sum()) * N * K * 2
             for label, (t, err) in best.items():
                 if t is None:

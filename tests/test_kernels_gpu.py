@@ -674,9 +674,19 @@ def test_gemm_silu_mul(gpu, M, I, K):
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
 
+@pytest.fixture(params=[0, 1], ids=["spill", "balanced"])
+def grouped_balance(request):
+    """An expert over several 256-row m-tiles: full tiles + a spill tile, or equal row ranges
+    (gemm_grouped_balance)."""
+    prev = torch.ops.mlop.gemm_grouped_balance(-1)
+    torch.ops.mlop.gemm_grouped_balance(request.param)
+    yield request.param
+    torch.ops.mlop.gemm_grouped_balance(prev)
+
+
 @pytest.mark.parametrize("rows", [[520, 700, 0, 613], [1024, 1024, 1024, 1024], [512, 3, 900, 257]])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_grouped_gemm_large_groups(gpu, rows, epi):
+def test_grouped_gemm_large_groups(gpu, rows, epi, grouped_balance):
     """>= 512 rows per expert on average: the grouped ping-pong 256x256 kernel; ragged,
     empty and tiny groups included; vs per-group fp32 matmul."""
     torch.manual_seed(sum(rows))
@@ -706,7 +716,7 @@ def test_grouped_gemm_large_groups(gpu, rows, epi):
     ([120, 135, 160, 98, 140, 111, 130, 130], 0, 4096, 14336),    # ~128 rows: half-empty 256-row tiles
     ([257, 257, 257, 257, 257, 257, 257, 257], 1, 28672, 4096),   # decode-only spill: 1-row second tiles
 ])
-def test_grouped_gemm_stream_k(gpu, counts, epi, N, K):
+def test_grouped_gemm_stream_k(gpu, counts, epi, N, K, grouped_balance):
     """Mixtral-size grouped GEMM with the stream-K tail planned ON DEVICE from the routed
     offsets (the host only knows the worst-case grid), three launches in a row, vs fp32
     per expert and vs the data-parallel grid."""
