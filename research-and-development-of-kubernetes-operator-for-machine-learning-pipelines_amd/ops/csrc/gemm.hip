@@ -931,7 +931,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
       if (grp * 128 + mi * 64 < rows_here) {
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) {
+          // balance 2: 16-row blocks past the last row skipped too (wave-uniform; a 257-row
+          // expert's balanced tiles then do 8 and 9 blocks, near-equal, and stay in step)
+          if (i > 0 && sk.balance == 2 && grp * 128 + mi * 64 + i * 16 >= rows_here) continue;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -939,6 +942,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(
               acc[mi * 4 + i][j] = mfma16(fa[i][kk], fb0[j][kk], acc[mi * 4 + i][j]);
               acc[mi * 4 + i][2 + j] = mfma16(fa[i][kk], fb1[j][kk], acc[mi * 4 + i][2 + j]);
             }
+        }
         __builtin_amdgcn_s_setprio(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1110,10 +1114,12 @@ static SkBuf g_sk[16];
 static int g_sk_mode = 1;
 static const int g_sk_min_iters = 16;
 static const int g_skip_dead = 1;
-// gemm_grouped_balance op (1, default): quadrant-aligned equal row ranges for an expert over
-// several m-tiles; 8 x 257 rows gate_up 677 -> 639 us, down 353 -> 308, real decode routing
-// -0.3 to -5 %, Mixtral batch 1024 +0.75 % (profiles/r06_moe_spill.md)
-static int g_grouped_balance = 1;
+// gemm_grouped_balance op: 1 = quadrant-aligned equal row ranges for an expert over several
+// m-tiles (8 x 257 rows gate_up 677 -> 639 us, down 353 -> 308; Mixtral batch 1024 +0.75 %);
+// 2 (default) = that + 16-row blocks past the tile's last row skip their MFMAs, so the two
+// tiles of a 257-row expert do 8 and 9 blocks (gate_up 597 us; batch 1024 +0.3-0.5 % over 1)
+// (profiles/r06_moe_spill.md)
+static int g_grouped_balance = 2;
 int gemm_grouped_balance(int set) {
   if (set >= 0) g_grouped_balance = set;
   return g_grouped_balance;

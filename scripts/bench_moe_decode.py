@@ -36,7 +36,7 @@ CANDIDATES = {
     "mid": [("auto", -1, -1, -1, -1), ("128x64", 128, 64, -1, -1), ("64x64/s6", 64, 64, 6, -1),
             ("64x64/s3", 64, 64, 3, -1), ("256x128", 256, 128, -1, 1), ("256x64", 256, 64, -1, 1),
             ("256x256", 256, 256, -1, 1)],
-    "large": [("auto", -1, -1, -1, -1), ("auto+bal", -1, -1, -1, -1), ("256x128", 256, 128, -1, 1),
+    "large": [("auto", -1, -1, -1, -1), ("auto+bal", -1, -1, -1, -1), ("auto+bal2", -1, -1, -1, -1), ("256x128", 256, 128, -1, 1),
               ("256x64", 256, 64, -1, 1), ("128x64", 128, 64, -1, 1), ("256x256", 256, 256, -1, 1)],
 }
 
@@ -84,8 +84,9 @@ def main():
             for _ in range(2):  # interleaved rounds
                 for label, bm, bn, st, sp in CANDIDATES[group]:
                     torch.ops.mlop.gemm_grouped_plan(bm, bn, st, sp)
-                    # "+bal": equal row ranges per expert m-tile (gemm_grouped_balance)
-                    torch.ops.mlop.gemm_grouped_balance(1 if label.endswith("+bal") else 0)
+                    # "+bal" / "+bal2": equal row ranges per expert m-tile, + the 16-row MFMA skip
+                    # (gemm_grouped_balance 1 / 2); every other candidate runs with 0
+                    torch.ops.mlop.gemm_grouped_balance(2 if label.endswith("+bal2") else 1 if label.endswith("+bal") else 0)
                     try:
                         y = ops.grouped_gemm(x, w, off, epi=epi, avg_rows=rows // E)
                         if ref is None:

@@ -674,7 +674,7 @@ def test_gemm_silu_mul(gpu, M, I, K):
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
 
-@pytest.fixture(params=[0, 1], ids=["spill", "balanced"])
+@pytest.fixture(params=[0, 1, 2], ids=["spill", "balanced", "balanced16"])
 def grouped_balance(request):
     """An expert over several 256-row m-tiles: full tiles + a spill tile, or equal row ranges
     (gemm_grouped_balance)."""
