@@ -674,14 +674,19 @@ def test_gemm_silu_mul(gpu, M, I, K):
     close(y, ref.silu_mul(gu), atol=3e-2, rtol=3e-2)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["spill", "balanced", "balanced16"])
+@pytest.fixture(params=[(0, 0), (1, 0), (2, 0), (2, 1), (2, 2)],
+                ids=["spill", "balanced", "balanced16", "expert_major", "order_auto"])
 def grouped_balance(request):
     """An expert over several 256-row m-tiles: full tiles + a spill tile, or equal row ranges
-    (gemm_grouped_balance)."""
-    prev = torch.ops.mlop.gemm_grouped_balance(-1)
-    torch.ops.mlop.gemm_grouped_balance(request.param)
+    (gemm_grouped_balance); tiles in the slot-fastest or the expert-major order
+    (gemm_grouped_order)."""
+    bal, order = request.param
+    prev, prev_o = torch.ops.mlop.gemm_grouped_balance(-1), torch.ops.mlop.gemm_grouped_order(-1)
+    torch.ops.mlop.gemm_grouped_balance(bal)
+    torch.ops.mlop.gemm_grouped_order(order)
     yield request.param
     torch.ops.mlop.gemm_grouped_balance(prev)
+    torch.ops.mlop.gemm_grouped_order(prev_o)
 
 
 @pytest.mark.parametrize("rows", [[520, 700, 0, 613], [1024, 1024, 1024, 1024], [512, 3, 900, 257]])
