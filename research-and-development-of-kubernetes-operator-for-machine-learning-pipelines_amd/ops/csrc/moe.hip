@@ -444,9 +444,25 @@ __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
   const int n_slots = T * k;
   for (int e = threadIdx.x; e <= n_local; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
-  for (int s = threadIdx.x; s < n_slots; s += blockDim.x) {
-    const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_topi, (uint32_t)(s * 4), 0, 16 /* sc1 */) - e0;
-    inv[s] = (e >= 0 && e < n_local) ? atomicAdd(&cnt[e], 1) : -1;  // rank in its expert
+  // the sc1 loads in batches of kSortChunk per thread, all in flight before the first use: one
+  // at a time, each load's latency was paid per slot (a 3,060-token mixed step: 12 slots per
+  // thread and pass, ~40 of the launch's 52 us)
+  constexpr int kSortChunk = 8;
+  auto load_chunk = [&](int s0, int (&ev)[kSortChunk]) {
+#pragma unroll
+    for (int j = 0; j < kSortChunk; ++j) {
+      const int s = s0 + j * (int)blockDim.x + (int)threadIdx.x;  // past n_slots: out of range, reads 0
+      ev[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_topi, (uint32_t)(s * 4), 0, 16 /* sc1 */) - e0;
+    }
+  };
+  for (int s0 = 0; s0 < n_slots; s0 += kSortChunk * (int)blockDim.x) {
+    int ev[kSortChunk];
+    load_chunk(s0, ev);
+#pragma unroll
+    for (int j = 0; j < kSortChunk; ++j) {
+      const int s = s0 + j * (int)blockDim.x + (int)threadIdx.x, e = ev[j];
+      if (s < n_slots) inv[s] = (e >= 0 && e < n_local) ? atomicAdd(&cnt[e], 1) : -1;  // rank in its expert
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -459,12 +475,22 @@ __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
     offsets[n_local] = acc;
   }
   __syncthreads();
-  for (int s = threadIdx.x; s < n_slots; s += blockDim.x) {
-    const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_topi, (uint32_t)(s * 4), 0, 16 /* sc1 */) - e0;
-    if (e >= 0 && e < n_local) {
-      const int row = base[e] + inv[s];
-      inv[s] = row;
-      arow[row] = s / k;
+  for (int s0 = 0; s0 < n_slots; s0 += kSortChunk * (int)blockDim.x) {
+    int ev[kSortChunk], rk[kSortChunk];
+    load_chunk(s0, ev);
+#pragma unroll
+    for (int j = 0; j < kSortChunk; ++j) {  // this thread's own pass-1 stores: plain loads see them
+      const int s = s0 + j * (int)blockDim.x + (int)threadIdx.x;
+      rk[j] = s < n_slots ? inv[s] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kSortChunk; ++j) {
+      const int s = s0 + j * (int)blockDim.x + (int)threadIdx.x, e = ev[j];
+      if (s < n_slots && e >= 0 && e < n_local) {
+        const int row = base[e] + rk[j];
+        inv[s] = row;
+        arow[row] = s / k;
+      }
     }
   }
 }
