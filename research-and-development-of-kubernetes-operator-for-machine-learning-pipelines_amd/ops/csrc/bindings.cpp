@@ -501,6 +501,7 @@ int64_t flash_persist(int64_t set) { return mlop::flash_persist((int)set); }
 int64_t flash_stream(int64_t set) { return mlop::flash_stream((int)set); }
 int64_t gemm_grouped_balance(int64_t set) { return mlop::gemm_grouped_balance((int)set); }
 int64_t gemm_grouped_order(int64_t set) { return mlop::gemm_grouped_order((int)set); }
+int64_t moe_mid_tok(int64_t set) { return mlop::moe_mid_tok((int)set); }
 int64_t gemm_mid_chain(int64_t set) { return mlop::gemm_mid_chain((int)set); }
 bool mid_chain_ok(int64_t M, int64_t N, int64_t K, int64_t epi) {
   return mlop::mid_chain_ok((int)M, (int)N, (int)K, (int)epi);
@@ -896,6 +897,7 @@ TORCH_LIBRARY(mlop, m) {
   m.def("flash_stream(int set=-1) -> int", &flash_stream);
   m.def("gemm_grouped_balance(int set=-1) -> int", &gemm_grouped_balance);
   m.def("gemm_grouped_order(int set=-1) -> int", &gemm_grouped_order);
+  m.def("moe_mid_tok(int set=-1) -> int", &moe_mid_tok);
   m.def("gemm_mid_chain(int set=-1) -> int", &gemm_mid_chain);
   m.def("mid_chain_ok(int M, int N, int K, int epi) -> bool", &mid_chain_ok);
   m.def("moe_mid_max_tokens(int set=-1) -> int", &moe_mid_max_tokens);

@@ -31,6 +31,7 @@ int flash_persist(int set);  // 0: one workgroup per flash item; n: persistent g
 int flash_stream(int set);   // 1: the persistent grid streams K / V pairs and Q across tiles
 int gemm_grouped_balance(int set);  // 1: equal row ranges per expert m-tile; 2: + the 16-row MFMA skip
 int gemm_grouped_order(int set);    // grouped tile order: 0 slot fastest, 1 expert-major, 2 auto
+int moe_mid_tok(int set);            // tokens per workgroup of the mid MoE dispatch: 0 = by T, 2, 4, 8
 void launch_flash_prefill(void* out, const void* q, const void* kc, const void* vc, const int* bt,
                           int bt_stride, const int* ptile_seq, const int* ptile_q0,
                           const int* q_start, const int* q_len, const int* ctx_len, int num_ptiles,

@@ -311,7 +311,7 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
 // MoE dispatch for 16 < T <= kMidT tokens (decode batches and prefill chunks) in ONE launch.  At batch 64 the separate
 // route is five ~5 us graph nodes per layer (router GEMM + its split-K reduce, top-k, sort,
 // gather: profiles/r05_windows.md), each a few us of work at most.  Here:
-//   workgroup w (tokens kMidTok w ..): the optional add + RMSNorm prologue, router logits
+//   workgroup w (tokens kMidTok w .., moe_mid_tok): the optional add + RMSNorm prologue, router logits
 //     (wave e = expert e: the router row loaded once, bf16-rounded as the separate projection
 //     stores them), softmax / top-k / renormalise -> topw, topi (written through, sc1);
 //   the LAST workgroup (one agent-scope ticket per launch, reset by it: graph-safe; dispatch
@@ -320,14 +320,25 @@ void launch_moe_dispatch_small(float* topw, int* topi, void* xp, int* offsets, i
 // There is no gathered copy: the grouped gate_up GEMM reads x rows through arow.  Rows inside
 // an expert come in ticket order (LDS atomics), which changes no value: each row's product is
 // independent of its position and the combine gathers by inv.
-constexpr int kMidT = 16384, kMidTok = 2;
+constexpr int kMidT = 16384;
 static int g_mid_max_t = kMidT;  // moe_mid_max_tokens op: in-process A/B of the range
+// moe_mid_tok op: tokens per workgroup (2, 4 or 8; the router row is loaded once per
+// workgroup, token rows two at a time).  Fewer workgroups = fewer router-row reloads and
+// fewer agent-scope tickets on the one counter, more sequential prologue tokens per workgroup.
+// 0 (default) = by T: 8 from 2,048 tokens, 4 from 512, else 2.  Mixtral batch 1024 windows,
+// 2 / 4 / 8: the 3,060-token mixed step 42.3 / 32.3 / 29.3 us, the 1,024-token decode step
+// 17.6 / 13.7 / 14.7 us (profiles/r06_moe_spill.md)
+static int g_mid_tok = 0;
+int moe_mid_tok(int set) {
+  if (set == 0 || set == 2 || set == 4 || set == 8) g_mid_tok = set;
+  return g_mid_tok;
+}
 int moe_mid_max_tokens(int set) {
   if (set >= 0) g_mid_max_t = set < kMidT ? set : kMidT;
   return g_mid_max_t;
 }
 
-template <int CH>
+template <int CH, int kMidTok>
 __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
     float* __restrict__ topw, int* __restrict__ topi, int* __restrict__ offsets, int* __restrict__ arow,
     int* __restrict__ inv, const uint16_t* __restrict__ x, const uint16_t* __restrict__ wr, int T, int E, int k,
@@ -379,23 +390,27 @@ __global__ void __launch_bounds__(64 * kDispWaves) moe_dispatch_mid_kernel(
     u32x4 b[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) b[i] = *reinterpret_cast<const u32x4*>(we + i * 512);
-    // both token rows' chunks in flight together with the router row's (one latency, not three)
-    u32x4 a[kMidTok][CH];
+    // token rows two at a time, both rows' chunks in flight together (with the router row's
+    // on the first pair: one latency, not three)
+#pragma unroll 1
+    for (int tp = 0; tp < kMidTok; tp += 2) {
+      u32x4 a[2][CH];
 #pragma unroll
-    for (int t = 0; t < kMidTok; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < CH; ++i)
-        a[t][i] = *reinterpret_cast<const u32x4*>(x + (size_t)(t0 + min(t, nt - 1)) * H + lane * 8 + i * 512);
+        for (int i = 0; i < CH; ++i)
+          a[t][i] = *reinterpret_cast<const u32x4*>(x + (size_t)(t0 + min(tp + t, nt - 1)) * H + lane * 8 + i * 512);
 #pragma unroll
-    for (int t = 0; t < kMidTok; ++t) {
-      float acc = 0.f;
+      for (int t = 0; t < 2; ++t) {
+        float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < CH; ++i)
+        for (int i = 0; i < CH; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          acc += lo_bf(a[t][i][q]) * lo_bf(b[i][q]) + hi_bf(a[t][i][q]) * hi_bf(b[i][q]);
-      acc = wave_sum(acc);
-      if (lane == 0 && t < nt) lg[t][e] = bf2f(f2bf(acc));
+          for (int q = 0; q < 4; ++q)
+            acc += lo_bf(a[t][i][q]) * lo_bf(b[i][q]) + hi_bf(a[t][i][q]) * hi_bf(b[i][q]);
+        acc = wave_sum(acc);
+        if (lane == 0 && tp + t < nt) lg[tp + t][e] = bf2f(f2bf(acc));
+      }
     }
   }
   __syncthreads();
@@ -507,10 +522,14 @@ void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, in
   int cus = 0;
   if (!gemm_sk_scratch(&ws, &ticket, &cus)) throw std::runtime_error("moe_dispatch_mid: stream-K scratch not reserved");
   const MoePro pro{(const uint16_t*)pro_y, (uint16_t*)pro_res, (const uint16_t*)pro_w, pro_eps, (uint16_t*)pro_xn};
-  const int grid = (T + kMidTok - 1) / kMidTok;
-#define MLOP_DISP(CH)                                                                                           \
-  moe_dispatch_mid_kernel<CH><<<grid, 64 * kDispWaves, 0, st>>>(topw, topi, offsets, arow, inv, (const uint16_t*)x, \
-                                                                (const uint16_t*)wr, T, E, k, H, e0, n_local, pro, ticket)
+  const int tok = g_mid_tok ? g_mid_tok : T >= 2048 ? 8 : T >= 512 ? 4 : 2, grid = (T + tok - 1) / tok;
+#define MLOP_DISP_T(CH, TOK)                                                                                         \
+  moe_dispatch_mid_kernel<CH, TOK><<<grid, 64 * kDispWaves, 0, st>>>(topw, topi, offsets, arow, inv, (const uint16_t*)x, \
+                                                                     (const uint16_t*)wr, T, E, k, H, e0, n_local, pro, ticket)
+#define MLOP_DISP(CH)                       \
+  if (tok == 8) MLOP_DISP_T(CH, 8);         \
+  else if (tok == 4) MLOP_DISP_T(CH, 4);    \
+  else MLOP_DISP_T(CH, 2);
   switch (H) {
     case 1024: MLOP_DISP(2); break;
     case 2048: MLOP_DISP(4); break;
@@ -518,6 +537,7 @@ void launch_moe_dispatch_mid(float* topw, int* topi, int* offsets, int* arow, in
     default: MLOP_DISP(16); break;
   }
 #undef MLOP_DISP
+#undef MLOP_DISP_T
 }
 
 // combine fused with the decoder's residual add + RMSNorm (one workgroup per token row, 8

@@ -836,9 +836,18 @@ def _check_mid_layout(topi, off, arow, inv, T, k, e0, nl):
     assert torch.equal(arow.cpu().long()[rows], slots // k)
 
 
+@pytest.fixture(params=[0, 2, 4, 8], ids=["tok_auto", "tok2", "tok4", "tok8"])
+def mid_tok(request):
+    """Tokens per workgroup of the mid MoE dispatch (moe_mid_tok): 0 = by T (default), 2, 4, 8."""
+    prev = torch.ops.mlop.moe_mid_tok(-1)
+    torch.ops.mlop.moe_mid_tok(request.param)
+    yield request.param
+    torch.ops.mlop.moe_mid_tok(prev)
+
+
 @pytest.mark.parametrize("T,E,k,H", [(17, 8, 2, 4096), (64, 8, 2, 4096), (130, 8, 2, 1024), (1024, 8, 2, 4096), (5000, 8, 2, 4096),
                                      (40, 16, 4, 2048), (300, 8, 2, 8192)])
-def test_moe_dispatch_mid(gpu, T, E, k, H):
+def test_moe_dispatch_mid(gpu, T, E, k, H, mid_tok):
     """Multi-workgroup dispatch (router GEMV + route per workgroup, last-workgroup sort, no
     gather) against the separate router projection + moe_route, for the full and a partial
     (expert-parallel) local expert range; twice in a row (the ticket resets itself)."""
@@ -857,7 +866,7 @@ def test_moe_dispatch_mid(gpu, T, E, k, H):
 
 
 @pytest.mark.parametrize("T,H", [(33, 4096), (200, 2048)])
-def test_moe_dispatch_mid_prologue(gpu, T, H):
+def test_moe_dispatch_mid_prologue(gpu, T, H, mid_tok):
     """Mid dispatch with the residual add + RMSNorm prologue == add_rmsnorm, then route."""
     E, k = 8, 2
     torch.manual_seed(T + H)
